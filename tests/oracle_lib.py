@@ -1,0 +1,208 @@
+"""ctypes wrappers for the TEST-ONLY oracles (never imported by fhe_amd).
+
+* ``Ref``  -> oracle/_ref/libfhe_ref.so : the reference itself, compiled from
+  /root/reference by oracle/Makefile (only present where it was built; the
+  built .so travels to the GPU box with the snapshot).
+* ``Restatement`` -> oracle/_ref/libtfhe_oracle.so : our C restatement
+  (oracle/tfhe_oracle.c), pinned against ``Ref`` and tests/golden/.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libfhe_ref.so")
+RESTATE_SO = os.path.join(ROOT, "oracle", "_ref", "libtfhe_oracle.so")
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+TOY, STD128, STD128_LMKCDEY = 0, 3, 21
+GINX, LMKCDEY = 2, 3
+GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return a.ctypes.data_as(vp)
+
+
+def ref_available():
+    return os.path.exists(REF_SO)
+
+
+def restatement_available():
+    return os.path.exists(RESTATE_SO)
+
+
+class Ref:
+    def __init__(self, paramset, method):
+        self.L = ctypes.CDLL(REF_SO)
+        L = self.L
+        L.ref_ctx_create.restype = vp
+        L.ref_ctx_create.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.ref_last_error.restype = ctypes.c_char_p
+        L.ref_bsk_len.restype = ctypes.c_size_t
+        L.ref_bsk_len.argtypes = [vp]
+        L.ref_ntt_bench.restype = ctypes.c_double
+        L.ref_ntt_bench.argtypes = [ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int]
+        L.ref_time_gates.restype = ctypes.c_double
+        L.ref_time_gates.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        self.h = vp(L.ref_ctx_create(paramset, method)) if paramset is not None else None
+        if self.h is not None and not self.h.value:
+            raise RuntimeError(self.err())
+        if self.h is not None:
+            info = np.zeros(12, np.uint64)
+            self._chk(L.ref_ctx_info(self.h, _p(info)))
+            (self.n, self.N, self.q, self.Q, self.qKS, self.baseKS, self.digitsKS, self.baseG,
+             self.digitsG, self.psi, self.numAutoKeys, self.keyDist) = [int(x) for x in info]
+
+    def err(self):
+        return self.L.ref_last_error().decode()
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise RuntimeError("reference error: " + self.err())
+
+    def __del__(self):
+        try:
+            if self.h is not None:
+                self.L.ref_ctx_destroy(self.h)
+        except Exception:
+            pass
+
+    def bsk_len(self):
+        return int(self.L.ref_bsk_len(self.h))
+
+    def ntt(self, Q, polys, inverse=False):
+        polys = np.ascontiguousarray(polys, dtype=np.uint64).copy()
+        cnt, N = polys.shape
+        psi = ctypes.c_uint64()
+        self._chk(self.L.ref_ntt(ctypes.c_uint64(Q), ctypes.c_uint32(N), _p(polys), ctypes.c_size_t(cnt),
+                                 int(inverse), ctypes.byref(psi)))
+        return polys, psi.value
+
+    def keygen(self):
+        sk = np.zeros(self.n, np.uint64)
+        bsk = np.zeros(self.bsk_len(), np.uint64)
+        rows = self.N * self.baseKS * self.digitsKS
+        A = np.zeros(rows * self.n, np.uint64)
+        B = np.zeros(rows, np.uint64)
+        self._chk(self.L.ref_keygen(self.h, _p(sk), _p(bsk), _p(A), _p(B)))
+        return sk, bsk, A, B
+
+    def encrypt(self, bits):
+        a = np.zeros((len(bits), self.n), np.uint64)
+        b = np.zeros(len(bits), np.uint64)
+        for i, m in enumerate(bits):
+            self._chk(self.L.ref_encrypt(self.h, int(m), _p(a[i]), ctypes.byref(ctypes.c_uint64.from_buffer(b, 8 * i))))
+        return a, b
+
+    def load_keys(self, bsk, A, B):
+        self._chk(self.L.ref_load_keys(self.h, _p(bsk), _p(A), _p(B)))
+
+    def eval_gate(self, gate, a1, b1, a2, b2, extended=False, nthreads=0):
+        cnt = a1.shape[0]
+        L = self.N if extended else self.n
+        ao = np.zeros((cnt, L), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        self._chk(self.L.ref_eval_gate(self.h, ctypes.c_int(gate), ctypes.c_size_t(cnt), _p(a1), _p(b1), _p(a2),
+                                       _p(b2), _p(ao), _p(bo), ctypes.c_int(int(extended)), ctypes.c_int(nthreads)))
+        return ao, bo
+
+    def time_gates(self, gate, a1, b1, a2, b2, nthreads=0):
+        cnt = a1.shape[0]
+        ao = np.zeros((cnt, self.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        t = self.L.ref_time_gates(self.h, gate, cnt, _p(a1), _p(b1), _p(a2), _p(b2), _p(ao), _p(bo), nthreads)
+        if t < 0:
+            raise RuntimeError(self.err())
+        return t, ao, bo
+
+    def modswitch(self, q_from, q_to, a, b):
+        cnt, L = a.shape
+        ao = np.zeros_like(a)
+        bo = np.zeros_like(b)
+        self._chk(self.L.ref_modswitch(self.h, ctypes.c_uint64(q_from), ctypes.c_uint64(q_to), ctypes.c_uint32(L),
+                                       ctypes.c_size_t(cnt), _p(a), _p(b), _p(ao), _p(bo)))
+        return ao, bo
+
+    def keyswitch(self, a, b):
+        cnt = a.shape[0]
+        ao = np.zeros((cnt, self.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        self._chk(self.L.ref_keyswitch(self.h, ctypes.c_size_t(cnt), _p(a), _p(b), _p(ao), _p(bo)))
+        return ao, bo
+
+    def decrypt(self, sk, a, b, mod):
+        r = ctypes.c_int64()
+        self._chk(self.L.ref_decrypt(self.h, _p(np.ascontiguousarray(sk, np.uint64)),
+                                     _p(np.ascontiguousarray(a, np.uint64)), ctypes.c_uint64(int(b)),
+                                     ctypes.c_uint32(len(a)), ctypes.c_uint64(mod), ctypes.byref(r)))
+        return r.value
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint32) for f in
+                ("n", "N", "q", "qKS", "baseKS", "digitsKS", "baseG", "gBits", "digitsG", "numAutoKeys",
+                 "method", "paramset")] + [("Q", ctypes.c_uint64), ("psi", ctypes.c_uint64)]
+
+
+class Restatement:
+    """Our C restatement of the reference path (oracle/tfhe_oracle.c)."""
+
+    def __init__(self, paramset=None, method=None):
+        self.L = ctypes.CDLL(RESTATE_SO)
+        self.L.tfo_last_prime.restype = ctypes.c_uint64
+        self.L.tfo_root_of_unity.restype = ctypes.c_uint64
+        self.L.tfo_root_of_unity.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        self.L.tfo_decrypt.restype = ctypes.c_int64
+        self.L.tfo_decrypt.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64]
+        self.p = None
+        if paramset is not None:
+            self.p = _Params()
+            rc = self.L.tfo_params_init(paramset, method, ctypes.byref(self.p))
+            if rc != 0:
+                raise ValueError("bad params")
+            for f, _ in _Params._fields_:
+                setattr(self, f, getattr(self.p, f))
+
+    def ntt(self, Q, psi, polys, inverse=False, nthreads=8):
+        polys = np.ascontiguousarray(polys, dtype=np.uint64).copy()
+        cnt, N = polys.shape
+        self.L.tfo_ntt_batch(_p(polys), ctypes.c_size_t(cnt), ctypes.c_uint32(N), ctypes.c_uint64(Q),
+                             ctypes.c_uint64(psi), int(inverse), nthreads)
+        return polys
+
+    def eval_gate(self, bsk, A, B, gate, a1, b1, a2, b2, stage=0, nthreads=8):
+        cnt = a1.shape[0]
+        L = self.N if stage == 1 else self.n
+        ao = np.zeros((cnt, L), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        self.L.tfo_eval_gate_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_int(gate),
+                                   ctypes.c_size_t(cnt), _p(a1), _p(b1), _p(a2), _p(b2), _p(ao), _p(bo),
+                                   ctypes.c_int(stage), ctypes.c_int(nthreads))
+        return ao, bo
+
+    def modswitch(self, q_from, q_to, a, b):
+        cnt, L = a.shape
+        ao = np.zeros_like(a)
+        bo = np.zeros_like(b)
+        self.L.tfo_modswitch(ctypes.c_uint64(q_from), ctypes.c_uint64(q_to), ctypes.c_uint32(L), ctypes.c_size_t(cnt),
+                             _p(a), _p(b), _p(ao), _p(bo))
+        return ao, bo
+
+    def keyswitch(self, A, B, a, b):
+        cnt = a.shape[0]
+        ao = np.zeros((cnt, self.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        self.L.tfo_keyswitch(ctypes.byref(self.p), _p(A), _p(B), ctypes.c_size_t(cnt), _p(a), _p(b), _p(ao), _p(bo))
+        return ao, bo
+
+    def decrypt(self, sk, skmod, a, b, mod):
+        a = np.ascontiguousarray(a, np.uint64)
+        return int(self.L.tfo_decrypt(_p(np.ascontiguousarray(sk, np.uint64)), ctypes.c_uint64(skmod), _p(a),
+                                      ctypes.c_uint64(int(b)), ctypes.c_uint32(len(a)), ctypes.c_uint64(mod)))
