@@ -1,0 +1,94 @@
+// ubench.hip -- measures gfx950 VALU throughput of the integer/fp ops the NTT
+// and external product are built from (design input, not product code).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#define ITERS 2048
+#define OP_KERNEL(NAME, ASM)                                                              \
+    __global__ void NAME(unsigned* out, unsigned seed) {                                 \
+        unsigned a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;          \
+        unsigned a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7, b = seed | 1;        \
+        for (int i = 0; i < ITERS; ++i) {                                                 \
+            asm volatile(ASM " %0, %0, %8\n\t" ASM " %1, %1, %8\n\t" ASM " %2, %2, %8\n\t"  \
+                         ASM " %3, %3, %8\n\t" ASM " %4, %4, %8\n\t" ASM " %5, %5, %8\n\t"  \
+                         ASM " %6, %6, %8\n\t" ASM " %7, %7, %8"                          \
+                         : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5),   \
+                           "+v"(a6), "+v"(a7)                                             \
+                         : "v"(b));                                                       \
+        }                                                                                 \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7; \
+    }
+
+OP_KERNEL(k_add, "v_add_u32")
+OP_KERNEL(k_mul_lo, "v_mul_lo_u32")
+OP_KERNEL(k_mul_hi, "v_mul_hi_u32")
+OP_KERNEL(k_mul24, "v_mul_u32_u24")
+OP_KERNEL(k_mulhi24, "v_mul_hi_u32_u24")
+OP_KERNEL(k_fmul, "v_mul_f32")
+
+__global__ void k_mad64(unsigned long long* out, unsigned seed) {
+    unsigned long long a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    unsigned long long a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    unsigned b = seed | 1, c = seed * 3;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_mad_u64_u32 %0, vcc, %8, %9, %0\n\t v_mad_u64_u32 %1, vcc, %8, %9, %1\n\t"
+            "v_mad_u64_u32 %2, vcc, %8, %9, %2\n\t v_mad_u64_u32 %3, vcc, %8, %9, %3\n\t"
+            "v_mad_u64_u32 %4, vcc, %8, %9, %4\n\t v_mad_u64_u32 %5, vcc, %8, %9, %5\n\t"
+            "v_mad_u64_u32 %6, vcc, %8, %9, %6\n\t v_mad_u64_u32 %7, vcc, %8, %9, %7"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(b), "v"(c)
+            : "vcc");
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
+__global__ void k_fma64(double* out, unsigned seed) {
+    double a0 = threadIdx.x + seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    double a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7, b = 0.999, c = 1e-3;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_fma_f64 %0, %0, %8, %9\n\t v_fma_f64 %1, %1, %8, %9\n\t"
+            "v_fma_f64 %2, %2, %8, %9\n\t v_fma_f64 %3, %3, %8, %9\n\t"
+            "v_fma_f64 %4, %4, %8, %9\n\t v_fma_f64 %5, %5, %8, %9\n\t"
+            "v_fma_f64 %6, %6, %8, %9\n\t v_fma_f64 %7, %7, %8, %9"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(b), "v"(c));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+template <typename K, typename T>
+static void run(const char* name, K kern, T* buf, int blocks, int threads) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, buf, 7u);
+    hipDeviceSynchronize();
+    hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, buf, 7u);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    double ops = 5.0 * blocks * threads * ITERS * 8.0;
+    // lane-ops per ns; per CU per clock at 2.4 GHz: ops / (256 * 2.4e9 * s)
+    printf("%-18s %8.3f ms  %9.1f Glane-op/s  %6.2f lane-op/clk/CU (2.4GHz)\n", name, ms, ops / (ms * 1e6),
+           ops / (ms * 1e-3) / (256 * 2.4e9));
+}
+
+int main() {
+    const int blocks = 256 * 8, threads = 256;
+    void* buf;
+    hipMalloc(&buf, (size_t)blocks * threads * 8);
+    run("v_add_u32", k_add, (unsigned*)buf, blocks, threads);
+    run("v_mul_lo_u32", k_mul_lo, (unsigned*)buf, blocks, threads);
+    run("v_mul_hi_u32", k_mul_hi, (unsigned*)buf, blocks, threads);
+    run("v_mul_u32_u24", k_mul24, (unsigned*)buf, blocks, threads);
+    run("v_mul_hi_u32_u24", k_mulhi24, (unsigned*)buf, blocks, threads);
+    run("v_mul_f32", k_fmul, (unsigned*)buf, blocks, threads);
+    run("v_mad_u64_u32", k_mad64, (unsigned long long*)buf, blocks, threads);
+    run("v_fma_f64", k_fma64, (double*)buf, blocks, threads);
+    hipFree(buf);
+    return 0;
+}
