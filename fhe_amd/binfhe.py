@@ -1,0 +1,268 @@
+"""Host-side mirror of the reference's binfhe API over the HIP C-ABI.
+
+Names and argument meaning follow lux::fhe::BinFHEContext
+(src/binfhe/include/binfhecontext.h) and the batch API
+(src/binfhe/include/batch/binfhe-batch.h) so tests read like the reference's:
+
+    cc = BinFHEContext()
+    cc.GenerateBinFHEContext(STD128, GINX)
+    sk = cc.KeyGen(); cc.BTKeyGen(sk)
+    ct1, ct2 = cc.Encrypt(sk, 1), cc.Encrypt(sk, 0)
+    r = cc.EvalBinGate(AND, ct1, ct2)          # runs on the MI355X
+    cc.Decrypt(sk, r)
+
+Every evaluation goes through libfhe_amd.so on the GPU; there is no CPU
+fallback.  Key generation / encryption / decryption are host C++ (seeded).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import FheHipError, check, lib, ptr, sz, u64, vp
+
+# reference enum values (src/binfhe/include/binfhe-constants.h:49-126)
+TOY, STD128, STD128_LMKCDEY = 0, 3, 21
+AP, GINX, LMKCDEY = 1, 2, 3
+OR, AND, NOR, NAND, XOR, XNOR, MAJORITY, AND3, OR3, AND4, OR4, XOR_FAST, XNOR_FAST, CMUX = range(14)
+GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR}
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint32) for f in ("paramset", "method", "n", "N", "q", "qKS", "baseKS", "digitsKS",
+                                               "baseG", "digitsG", "numAutoKeys", "keyDist")] + \
+               [(f, ctypes.c_uint64) for f in ("Q", "psi", "bsk_words", "ksk_rows")]
+
+
+def _setup(L):
+    if getattr(L, "_binfhe_ready", False):
+        return L
+    P = ctypes.POINTER(_Params)
+    L.fhe_hip_params_get.argtypes = [ctypes.c_int, ctypes.c_int, P]
+    L.fhe_hip_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.fhe_hip_destroy.argtypes = [vp]
+    L.fhe_hip_destroy.restype = None
+    L.fhe_hip_get_params.argtypes = [vp, P]
+    L.fhe_hip_stream.argtypes = [vp]
+    L.fhe_hip_stream.restype = vp
+    L.fhe_hip_load_bsk.argtypes = [vp, vp, sz]
+    L.fhe_hip_load_ksk.argtypes = [vp, vp, sz, vp, sz]
+    L.fhe_hip_eval_bingate_batch.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_eval_bingate_batch_device.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_eval_bingate_extended.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_keyswitch_batch.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.fhe_hip_modswitch_batch.argtypes = [vp, u64, u64, ctypes.c_uint32, sz, vp, vp, vp, vp]
+    L.fhe_hip_keygen.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp, vp, vp, vp]
+    L.fhe_hip_encrypt.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, vp, vp]
+    L.fhe_hip_decrypt.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, sz, ctypes.c_uint32, u64, vp]
+    L._binfhe_ready = True
+    return L
+
+
+def L():
+    return _setup(lib())
+
+
+@dataclass(frozen=True)
+class Params:
+    paramset: int
+    method: int
+    n: int
+    N: int
+    q: int
+    qKS: int
+    baseKS: int
+    digitsKS: int
+    baseG: int
+    digitsG: int
+    numAutoKeys: int
+    keyDist: int
+    Q: int
+    psi: int
+    bsk_words: int
+    ksk_rows: int
+
+
+def params(paramset, method):
+    p = _Params()
+    check(L().fhe_hip_params_get(paramset, method, ctypes.byref(p)))
+    return Params(**{f: int(getattr(p, f)) for f, _ in _Params._fields_})
+
+
+def _u64(a):
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+@dataclass
+class KeySet:
+    sk: np.ndarray
+    bsk: np.ndarray
+    kskA: np.ndarray
+    kskB: np.ndarray
+
+
+def keygen(paramset, method, seed):
+    """Deterministic (sk, bsk, kskA, kskB) in the reference's raw layouts."""
+    P = params(paramset, method)
+    sk = np.zeros(P.n, np.uint64)
+    bsk = np.zeros(P.bsk_words, np.uint64)
+    A = np.zeros(P.ksk_rows * P.n, np.uint64)
+    B = np.zeros(P.ksk_rows, np.uint64)
+    check(L().fhe_hip_keygen(paramset, method, seed, ptr(sk), ptr(bsk), ptr(A), ptr(B)))
+    return KeySet(sk, bsk, A, B)
+
+
+def encrypt(paramset, method, sk, bits, seed):
+    P = params(paramset, method)
+    bits = np.ascontiguousarray(bits, dtype=np.int32)
+    a = np.zeros((len(bits), P.n), np.uint64)
+    b = np.zeros(len(bits), np.uint64)
+    check(L().fhe_hip_encrypt(paramset, method, ptr(_u64(sk)), ptr(bits), len(bits), seed, ptr(a), ptr(b)))
+    return a, b
+
+
+def decrypt(paramset, method, sk, a, b, mod=None):
+    P = params(paramset, method)
+    a = _u64(np.atleast_2d(a))
+    b = _u64(np.atleast_1d(b))
+    out = np.zeros(len(b), np.int64)
+    check(L().fhe_hip_decrypt(paramset, method, ptr(_u64(sk)), ptr(a), ptr(b), len(b), a.shape[1],
+                              mod if mod is not None else P.q, ptr(out)))
+    return out
+
+
+class GateEngine:
+    """One MI355X context (fhe_hip_ctx): resident keys + batched gate bootstrapping."""
+
+    def __init__(self, paramset, method, device=0):
+        self._h = vp()
+        check(L().fhe_hip_create(paramset, method, device, ctypes.byref(self._h)))
+        self.params = params(paramset, method)
+        self.device = device
+
+    def close(self):
+        if self._h:
+            L().fhe_hip_destroy(self._h)
+            self._h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return L().fhe_hip_stream(self._h)
+
+    def load_keys(self, bsk, kskA, kskB):
+        bsk, kskA, kskB = _u64(bsk), _u64(kskA), _u64(kskB)
+        check(L().fhe_hip_load_bsk(self._h, ptr(bsk), bsk.size))
+        check(L().fhe_hip_load_ksk(self._h, ptr(kskA), kskA.size, ptr(kskB), kskB.size))
+
+    def eval_gate(self, gate, a1, b1, a2, b2):
+        a1, b1, a2, b2 = _u64(a1), _u64(b1), _u64(a2), _u64(b2)
+        cnt = len(b1)
+        ao = np.zeros((cnt, self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_eval_bingate_batch(self._h, gate, cnt, ptr(a1), ptr(b1), ptr(a2), ptr(b2), ptr(ao),
+                                             ptr(bo)))
+        return ao, bo
+
+    def eval_gate_extended(self, gate, a1, b1, a2, b2):
+        a1, b1, a2, b2 = _u64(a1), _u64(b1), _u64(a2), _u64(b2)
+        cnt = len(b1)
+        ao = np.zeros((cnt, self.params.N), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_eval_bingate_extended(self._h, gate, cnt, ptr(a1), ptr(b1), ptr(a2), ptr(b2), ptr(ao),
+                                                ptr(bo)))
+        return ao, bo
+
+    def eval_gate_device(self, gate, count, d_a1, d_b1, d_a2, d_b2, d_ao, d_bo, stream=None):
+        check(L().fhe_hip_eval_bingate_batch_device(self._h, gate, count, vp(d_a1), vp(d_b1), vp(d_a2), vp(d_b2),
+                                                    vp(d_ao), vp(d_bo), vp(stream) if stream else None))
+
+    def keyswitch(self, a, b):
+        a, b = _u64(a), _u64(b)
+        cnt = len(b)
+        ao = np.zeros((cnt, self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_keyswitch_batch(self._h, cnt, ptr(a), ptr(b), ptr(ao), ptr(bo)))
+        return ao, bo
+
+    def modswitch(self, q_from, q_to, a, b):
+        a, b = _u64(a), _u64(b)
+        cnt, ln = a.shape
+        ao = np.zeros_like(a)
+        bo = np.zeros_like(b)
+        check(L().fhe_hip_modswitch_batch(self._h, q_from, q_to, ln, cnt, ptr(a), ptr(b), ptr(ao), ptr(bo)))
+        return ao, bo
+
+
+# ------------------------------------------------------------------------------------------
+# BinFHEContext mirror (binfhecontext.h)
+# ------------------------------------------------------------------------------------------
+@dataclass
+class LWECiphertext:
+    a: np.ndarray
+    b: int
+    modulus: int
+
+
+@dataclass
+class LWEPrivateKey:
+    s: np.ndarray  # stored mod qKS, as the reference stores it
+
+
+class BinFHEContext:
+    def __init__(self, device=0, seed=0x5EED):
+        self.device = device
+        self._seed = seed
+        self._ctr = 0
+        self.engine = None
+
+    def GenerateBinFHEContext(self, paramset=STD128, method=GINX):
+        self.paramset, self.method = paramset, method
+        self.params = params(paramset, method)
+        self.engine = GateEngine(paramset, method, self.device)
+
+    def _next_seed(self):
+        self._ctr += 1
+        return (self._seed * 1000003 + self._ctr) & 0xFFFFFFFFFFFFFFFF
+
+    def KeyGen(self):
+        self._keys = keygen(self.paramset, self.method, self._next_seed())
+        return LWEPrivateKey(self._keys.sk)
+
+    def BTKeyGen(self, sk):
+        if not np.array_equal(sk.s, self._keys.sk):
+            raise FheHipError(-4, "BTKeyGen: secret key was not produced by this context's KeyGen")
+        self.engine.load_keys(self._keys.bsk, self._keys.kskA, self._keys.kskB)
+
+    def BTKeyLoad(self, bsk, kskA, kskB):
+        self.engine.load_keys(bsk, kskA, kskB)
+
+    def Encrypt(self, sk, m):
+        a, b = encrypt(self.paramset, self.method, sk.s, [int(m)], self._next_seed())
+        return LWECiphertext(a[0], int(b[0]), self.params.q)
+
+    def Decrypt(self, sk, ct):
+        return int(decrypt(self.paramset, self.method, sk.s, ct.a[None, :], [ct.b], ct.modulus)[0])
+
+    def EvalBinGate(self, gate, ct1, ct2):
+        if ct1 is ct2:
+            raise FheHipError(-8, "Input ciphertexts should be independant")
+        return self.EvalBinGateBatch(gate, [ct1], [ct2])[0]
+
+    def EvalBinGateBatch(self, gate, ct1, ct2):
+        """EvalBinGateBatch (src/binfhe/lib/batch/batch.cpp:176-210) on the GPU."""
+        if len(ct1) != len(ct2):
+            raise FheHipError(-2, "Input size mismatch")
+        if not ct1:
+            return []
+        a1 = np.stack([c.a for c in ct1])
+        a2 = np.stack([c.a for c in ct2])
+        b1 = np.array([c.b for c in ct1], np.uint64)
+        b2 = np.array([c.b for c in ct2], np.uint64)
+        ao, bo = self.engine.eval_gate(gate, a1, b1, a2, b2)
+        return [LWECiphertext(ao[i], int(bo[i]), self.params.q) for i in range(len(bo))]

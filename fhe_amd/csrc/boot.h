@@ -1,0 +1,44 @@
+// boot.h -- device-side argument blocks and launchers for the gate bootstrap
+// (bootstrap.hip) and the LWE key switch (keyswitch.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fhe_amd {
+
+// Twiddle/monomial tables for the fused accumulator kernels (all u32,
+// Montgomery form x * 2^32 mod Q).
+struct BootTables {
+    const uint32_t* twA_fwd;  // Table[0..31]   (uniform stages on bits 9..5)
+    const uint32_t* twA_inv;  // TableI[0..31]
+    const uint32_t* twB_fwd;  // 992 words: lane-major Table entries of the stages on bits 4..0
+    const uint32_t* twB_inv;  // 992 words: same for TableI
+    const uint32_t* mono;     // [2N]: (psi^e - 1) -> EVAL(X^m - 1) = omega_j^m - 1
+    uint32_t Q, Q2, qinv;     // qinv = -Q^-1 mod 2^32
+    uint32_t ninvR, w1ninvR;  // N^-1 and TableI[1] * N^-1 (Montgomery) for the last iNTT stage
+};
+
+struct GateArgs {
+    uint32_t count, n, N, q, qKS;
+    uint32_t lb, ub, lv, uv, factor;  // BootstrapGateCore test-vector window (binfhe-base-scheme.cpp:535-567)
+    uint32_t b_const;                 // (Q >> 3) + 1 (binfhe-base-scheme.cpp:118-120)
+    uint32_t xor_double;              // XOR/XNOR: 2 (ct1 + ct2)
+    uint32_t msb_out;                 // 1: write ctExt mod-switched to qKS; 0: raw ctExt mod Q
+    uint32_t gbits;                   // log2(baseG)
+};
+
+// GINX/CGGI: inputs (u64, mod q) -> monomial exponents + test-vector b
+hipError_t launch_prep_ginx(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
+                            const uint64_t* b2, uint16_t* idx, uint32_t* tvb, hipStream_t s);
+// fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
+hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
+                                    const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
+// KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q) (:254-261), KSK as u16 rows of 512
+hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
+                            const uint32_t* ms_a, const uint32_t* ms_b, uint32_t q_out, uint64_t* a_out,
+                            uint64_t* b_out, hipStream_t s);
+// ModSwitch on u64 vectors (lwe-pke.cpp:41-46, 254-261)
+hipError_t launch_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, uint32_t count, const uint64_t* a,
+                            const uint64_t* b, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+
+}  // namespace fhe_amd

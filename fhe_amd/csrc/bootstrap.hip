@@ -1,0 +1,357 @@
+// bootstrap.hip -- fused TFHE gate bootstrap (GINX / CGGI) for gfx950.
+//
+// One wavefront per gate, for all n iterations of the accumulator loop
+// (RingGSWAccumulatorCGGI::EvalAcc, src/binfhe/lib/rgsw-acc-cggi.cpp:59-68):
+// the RLWE accumulator never leaves the CU.  Half-wave h (lanes 32h..32h+31)
+// owns polynomial component h (acc0 / acc1) as 32 registers x 32 lanes:
+//   layout A' (COEFFICIENT): lane l, register r  <->  coefficient x = (r << 5) | l
+//   layout B' (EVALUATION):  lane l, register r  <->  NTT slot      x = (l << 5) | r
+// (slot x is the reference's bit-reversed EVALUATION storage index).  A forward
+// NTT runs 5 radix-2 stages in A' (twiddles uniform over the wave: scalar
+// loads), one 32x32 LDS transpose, 5 stages in B' (per-lane twiddles from an
+// LDS table laid out lane-major: conflict-free); the inverse runs backwards.
+// Per iteration (AddToAccCGGI, rgsw-acc-cggi.cpp:102-151):
+//   iNTT(acc0 | acc1) -> signed approximate decomposition (rgsw-acc.cpp:54-91)
+//   -> NTT(D0 | D1), NTT(D2 | D3) -> per slot, all four digits gathered with
+//   v_permlane32_swap -> S1 = sum_d D_d K+[d][h], S2 = sum_d D_d K-[d][h] as
+//   64-bit v_mad_u64_u32 sums (keys in Montgomery form) -> one Montgomery
+//   reduction each -> acc_h += S1 (X^a - 1) + S2 (X^-a - 1), the monomials
+//   EVAL(X^m - 1) = omega_slot^m - 1 read from a 2N-entry LDS table instead of
+//   the reference's 16 MiB table of 2N NTT'd polynomials
+//   (rgsw-cryptoparameters.cpp:96-113).
+// All arithmetic is exact mod Q: lazy residues (< 4Q) inside the NTTs, canonical
+// [0, Q) at every point where the reference's values are observable (COEF acc
+// before decomposition, EVAL acc between iterations, outputs).
+#include "arith.h"
+#include "boot.h"
+
+namespace fhe_amd {
+
+namespace {
+
+constexpr int kTile = 32 * 33;  // one half-wave transpose tile (u32 words)
+
+struct Mod {
+    uint32_t Q, Q2, qinv;
+};
+
+// a * bR * 2^-32 mod Q, lazily: result < Q (1 + a / 2^32 * ...) < 2Q for a < 4Q, Q < 2^28
+FHE_DEV uint32_t mont_mul(uint32_t a, uint32_t bR, const Mod& m) {
+    uint64_t t  = (uint64_t)a * bR;
+    uint32_t mm = (uint32_t)t * m.qinv;
+    return (uint32_t)((t + (uint64_t)mm * m.Q) >> 32);
+}
+FHE_DEV uint32_t mont_red(uint64_t t, const Mod& m) {  // t < 16 Q^2 -> result < 2Q
+    uint32_t mm = (uint32_t)t * m.qinv;
+    return (uint32_t)((t + (uint64_t)mm * m.Q) >> 32);
+}
+// Cooley-Tukey (forward), Harvey-style lazy: x, y < 4Q in, < 4Q out
+FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
+    uint32_t xx = csub(x, m.Q2);
+    uint32_t t  = mont_mul(y, wR, m);
+    x           = xx + t;
+    y           = xx + m.Q2 - t;
+}
+// Gentleman-Sande (inverse): x, y < 2Q in, < 2Q out
+FHE_DEV void gs_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
+    uint32_t s = csub(x + y, m.Q2);
+    uint32_t d = x + m.Q2 - y;
+    x          = s;
+    y          = mont_mul(d, wR, m);
+}
+
+// intra-wave LDS hand-off: orders the compiler's LDS accesses; the LDS
+// executes one wave's DS instructions in issue order.
+FHE_DEV void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+FHE_DEV void transpose32(uint32_t (&v)[32], uint32_t* tile, int l) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) tile[l * 33 + r] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = tile[r * 33 + l];
+    wave_lds_sync();
+}
+
+// offset of stage b's lane-major twiddle block: 32 * (2^(4-b) - 1)
+constexpr int twb_off(int b) { return 32 * ((1 << (4 - b)) - 1); }
+
+// forward NTT: A' (COEF) -> B' (EVAL), outputs < 4Q
+FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
+                      const uint32_t* s_twB, const Mod& m) {
+#pragma unroll
+    for (int b = 9; b >= 5; --b) {
+        const int rb = b - 5;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
+            ct_bf(v[r], v[r | (1 << rb)], w, m);
+        }
+    }
+    transpose32(v, tile, l);
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << b)) continue;
+            const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+            ct_bf(v[r], v[r | (1 << b)], w, m);
+        }
+    }
+}
+
+// inverse NTT: B' (EVAL, inputs < 2Q) -> A' (COEF), outputs canonical [0, Q)
+FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
+                      const uint32_t* s_twB, uint32_t ninvR, uint32_t w1ninvR, const Mod& m) {
+#pragma unroll
+    for (int b = 0; b <= 4; ++b) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << b)) continue;
+            const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+            gs_bf(v[r], v[r | (1 << b)], w, m);
+        }
+    }
+    transpose32(v, tile, l);
+#pragma unroll
+    for (int b = 5; b <= 8; ++b) {
+        const int rb = b - 5;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
+            gs_bf(v[r], v[r | (1 << rb)], w, m);
+        }
+    }
+    // bit 9 with N^-1 folded in (transformnat-impl.h:599-623)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        uint32_t x = v[r], y = v[r | 16];
+        v[r]      = csub(mont_mul(x + y, ninvR, m), m.Q);
+        v[r | 16] = csub(mont_mul(x + m.Q2 - y, w1ninvR, m), m.Q);
+    }
+}
+
+FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
+
+// ModSwitch RoundqQ (lwe-pke.cpp:41-46): floor(0.5 + v*to/from) mod to, in IEEE double in
+// the reference.  For v*to < 2^53, v < from and odd `from` (or power-of-two from/to) the
+// double expression never crosses a rounding boundary, so it equals the exact integer
+// floor((2 v to + from) / (2 from)) (proof in DESIGN.md, exhaustively tested).
+FHE_DEV uint32_t mod_switch(uint64_t v, uint64_t from, uint64_t to) {
+    uint64_t r = (2 * v * to + from) / (2 * from);
+    return (uint32_t)(r % to);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// prep: ct = ct1 + ct2 (XOR/XNOR: 2(ct1 + ct2)) mod q (binfhe-base-scheme.cpp:95-107);
+// monomial exponent per i: ((q - a_i) mod q) * (2N / q) (rgsw-acc-cggi.cpp:62-66)
+// ---------------------------------------------------------------------------
+__global__ void k_prep_ginx(const uint64_t* __restrict__ a1, const uint64_t* __restrict__ b1,
+                            const uint64_t* __restrict__ a2, const uint64_t* __restrict__ b2, GateArgs g,
+                            uint16_t* __restrict__ idx, uint32_t* __restrict__ tvb) {
+    const uint64_t total = (uint64_t)g.count * g.n;
+    const uint32_t qm = g.q - 1, mbymod = 2 * g.N / g.q;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t a = (uint32_t)((a1[t] + a2[t]) & qm);
+        if (g.xor_double) a = (2 * a) & qm;
+        idx[t] = (uint16_t)(((g.q - a) & qm) * mbymod);
+    }
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < g.count; t += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t b = (uint32_t)((b1[t] + b2[t]) & qm);
+        if (g.xor_double) b = (2 * b) & qm;
+        tvb[t] = b;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fused blind rotation, 4 gates (waves) per 256-thread workgroup
+// ---------------------------------------------------------------------------
+constexpr int kWaves = 4;
+constexpr size_t kBootLds = (size_t)(992 * 2 + 2048 + kWaves * 2 * kTile) * 4;
+
+__global__ void __launch_bounds__(256, 2)
+    k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
+                        const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_twBf = sm;
+    uint32_t* s_twBi = sm + 992;
+    uint32_t* s_mono = sm + 1984;
+    uint32_t* s_tile = sm + 4032;
+    for (int i = threadIdx.x; i < 992; i += 256) {
+        s_twBf[i] = T.twB_fwd[i];
+        s_twBi[i] = T.twB_inv[i];
+    }
+    for (int i = threadIdx.x; i < 2048; i += 256) s_mono[i] = T.mono[i];
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
+    const uint32_t gate = blockIdx.x * kWaves + wave;
+    if (gate >= g.count) return;  // no workgroup barrier below this point
+    uint32_t* tileW = s_tile + wave * 2 * kTile;
+    uint32_t* tile  = tileW + h * kTile;
+    const Mod m{T.Q, T.Q2, T.qinv};
+
+    // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
+    uint32_t acc[32];
+    {
+        const uint32_t b = tvb[gate], qm = g.q - 1;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t x = (uint32_t)(r << 5) | l;
+            uint32_t v       = 0;
+            if (h == 1 && x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & qm;
+                v                 = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            acc[r] = v;
+        }
+        fwd_pass(acc, tile, l, T.twA_fwd, s_twBf, m);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(acc[r], m.Q2), m.Q);
+    }
+
+    const uint16_t* gidx = idx + (size_t)gate * g.n;
+    const uint32_t lbase = 2 * brv5(l) + 1;
+    const int32_t sh     = 32 - (int32_t)g.gbits;
+    const int32_t Qs     = (int32_t)m.Q;
+    const uint32_t Qh    = m.Q >> 1;
+    for (uint32_t i = 0; i < g.n; ++i) {
+        const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
+        uint32_t dA[32], dB[32];
+        // --- iNTT of a copy of acc -> canonical COEF (AddToAccCGGI :104-106)
+#pragma unroll
+        for (int r = 0; r < 32; ++r) dA[r] = acc[r];
+        inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+        // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
+        //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            int32_t d  = dA[r] < Qh ? (int32_t)dA[r] : (int32_t)dA[r] - Qs;
+            int32_t r0 = (d << sh) >> sh;
+            d          = (d - r0) >> g.gbits;
+            r0         = (d << sh) >> sh;
+            d          = (d - r0) >> g.gbits;
+            int32_t r1 = (d << sh) >> sh;
+            dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
+            dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
+        }
+        // --- NTT of the four digit polynomials (two per pass, one per half)
+#ifndef ABL_NO_FWD
+        fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
+        fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
+#endif
+        // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
+        //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
+        //     out so that each load instruction reads 1 KiB contiguous.
+#ifndef ABL_NO_MAC
+        const uint2* ki   = bsk + (size_t)i * (2 * 4 * 16 * 64) + lane;
+        const uint32_t ab = (a * lbase) & 2047;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            // one 2-slot step of keys live at a time (register budget)
+            asm volatile("" ::: "memory");
+            uint2 kp[4], kn[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                kp[d] = ki[((0 * 4 + d) * 16 + k) * 64];
+                kn[d] = ki[((1 * 4 + d) * 16 + k) * 64];
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r = 2 * k + e;
+                // all four digits in every lane: D0/D1 = digit A of acc0/acc1, D2/D3 = digit B
+                auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
+                const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
+                uint64_t S1 = (uint64_t)D0 * (e ? kp[0].y : kp[0].x) + (uint64_t)D1 * (e ? kp[1].y : kp[1].x) +
+                              (uint64_t)D2 * (e ? kp[2].y : kp[2].x) + (uint64_t)D3 * (e ? kp[3].y : kp[3].x);
+                uint64_t S2 = (uint64_t)D0 * (e ? kn[0].y : kn[0].x) + (uint64_t)D1 * (e ? kn[1].y : kn[1].x) +
+                              (uint64_t)D2 * (e ? kn[2].y : kn[2].x) + (uint64_t)D3 * (e ? kn[3].y : kn[3].x);
+                const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
+                // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
+                const uint32_t e1 = (ab + ((a * (uint32_t)(__builtin_bitreverse32(r) >> 27)) << 6)) & 2047;
+                const uint32_t e2 = (2048 - e1) & 2047;
+                const uint64_t S  = (uint64_t)t1 * s_mono[e1] + (uint64_t)t2 * s_mono[e2];
+                acc[r]            = add_mod(acc[r], csub(mont_red(S, m), m.Q), m.Q);
+            }
+        }
+#else
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] ^= dA[r] + dB[r] + a;
+#endif
+    }
+
+    // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
+    // 2N-1), both to COEF; ctExt = (acc0 coefficients, (Q>>3)+1 + acc1[0]); then ModSwitch to qKS.
+    // In COEF, Transpose maps coefficient k to -a_(N-k) (k >= 1), a_0 to itself.
+    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+    wave_lds_sync();
+    if (h == 0) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) tileW[(r << 5) | l] = acc[r];
+    } else if (l == 0) {
+        tileW[1024] = acc[0];
+    }
+    wave_lds_sync();
+    uint32_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+        const uint32_t j = (uint32_t)lane + 64u * t;
+        const uint32_t c = tileW[j == 0 ? 0 : g.N - j];
+        const uint32_t v = (j == 0 || c == 0) ? c : m.Q - c;
+        oa[j]            = g.msb_out ? mod_switch(v, m.Q, g.qKS) : v;
+    }
+    if (lane == 0) {
+        const uint32_t bb = add_mod(g.b_const, tileW[1024], m.Q);
+        ext_b[gate]       = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+hipError_t launch_prep_ginx(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
+                            const uint64_t* b2, uint16_t* idx, uint32_t* tvb, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    const uint64_t total = (uint64_t)g.count * g.n;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_prep_ginx, dim3(blocks), dim3(256), 0, s, a1, b1, a2, b2, g, idx, tvb);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
+                                    const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(k_blind_rotate_ginx, dim3(blocks), dim3(256), kBootLds, s, g, t,
+                       reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ModSwitch on u64 vectors (standalone entry point)
+// ---------------------------------------------------------------------------
+__global__ void k_modswitch(uint64_t from, uint64_t to, uint32_t len, uint32_t count, const uint64_t* __restrict__ a,
+                            const uint64_t* __restrict__ b, uint64_t* __restrict__ ao, uint64_t* __restrict__ bo) {
+    const uint64_t total = (uint64_t)len * count;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x)
+        ao[t] = mod_switch(a[t], from, to);
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < count; t += (uint64_t)gridDim.x * blockDim.x)
+        bo[t] = mod_switch(b[t], from, to);
+}
+
+hipError_t launch_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, uint32_t count, const uint64_t* a,
+                            const uint64_t* b, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint64_t total = (uint64_t)len * count;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_modswitch, dim3(blocks), dim3(256), 0, s, q_from, q_to, len, count, a, b, a_out, b_out);
+    return hipGetLastError();
+}
+
+}  // namespace fhe_amd

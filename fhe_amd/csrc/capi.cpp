@@ -4,9 +4,14 @@
 #include <exception>
 #include <new>
 #include <string>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/fhe_hip.h"
+#include "engine.h"
+#include "keygen.h"
 #include "ntt.h"
+#include "boot.h"
 
 using namespace fhe_amd;
 
@@ -24,6 +29,11 @@ template <typename F>
 int guarded(F&& f) {
     try {
         return f();
+    } catch (const HipError& e) {
+        return fail(FHE_HIP_ERR_DEVICE, e.what());
+    } catch (const std::logic_error& e) {
+        if (dynamic_cast<const std::invalid_argument*>(&e)) return fail(FHE_HIP_ERR_INVALID_PARAM, e.what());
+        return fail(FHE_HIP_ERR_NOT_INIT, e.what());
     } catch (const std::bad_alloc&) {
         return fail(FHE_HIP_ERR_ALLOC, "host allocation failed");
     } catch (const std::exception& e) {
@@ -33,6 +43,18 @@ int guarded(F&& f) {
     }
 }
 }  // namespace
+
+struct fhe_hip_ctx {
+    Engine eng;
+    fhe_hip_ctx(int ps, int m, int dev) : eng(ps, m, dev) {}
+};
+
+static void fill_params(const Params& p, fhe_hip_params* o) {
+    o->paramset = p.paramset; o->method = p.method; o->n = p.n; o->N = p.N; o->q = p.q; o->qKS = p.qKS;
+    o->baseKS = p.baseKS; o->digitsKS = p.digitsKS; o->baseG = p.baseG; o->digitsG = p.digitsG;
+    o->numAutoKeys = p.numAutoKeys; o->keyDist = p.keyDist; o->Q = p.Q; o->psi = p.psi;
+    o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows();
+}
 
 struct fhe_hip_ntt_plan {
     NttPlan plan;
@@ -147,6 +169,157 @@ int fhe_hip_ntt_batch(fhe_hip_ntt_plan* p, uint64_t* polys, size_t count, int in
     if (e == hipSuccess) e = hipMemcpyAsync(polys, p->d_buf, bytes, hipMemcpyDeviceToHost, p->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
     return e == hipSuccess ? FHE_HIP_OK : hip_fail(e, "ntt batch");
+}
+
+int fhe_hip_params_get(int paramset, int method, fhe_hip_params* out) {
+    return guarded([&]() -> int {
+        if (!out) return fail(FHE_HIP_ERR_NULL_PTR, "out is null");
+        fill_params(make_params(paramset, method), out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_create(int paramset, int method, int device, fhe_hip_ctx** out) {
+    return guarded([&]() -> int {
+        if (!out) return fail(FHE_HIP_ERR_NULL_PTR, "out is null");
+        *out = nullptr;
+        *out = new fhe_hip_ctx(paramset, method, device);
+        return FHE_HIP_OK;
+    });
+}
+
+void fhe_hip_destroy(fhe_hip_ctx* ctx) {
+    try {
+        delete ctx;
+    } catch (...) {
+    }
+}
+
+int fhe_hip_get_params(const fhe_hip_ctx* ctx, fhe_hip_params* out) {
+    if (!ctx || !out) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    fill_params(ctx->eng.params(), out);
+    return FHE_HIP_OK;
+}
+
+void* fhe_hip_stream(fhe_hip_ctx* ctx) { return ctx ? (void*)ctx->eng.stream() : nullptr; }
+
+int fhe_hip_load_bsk(fhe_hip_ctx* ctx, const uint64_t* bsk, size_t n_words) {
+    if (!ctx || !bsk) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int { ctx->eng.load_bsk(bsk, n_words); return FHE_HIP_OK; });
+}
+
+int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint64_t* B, size_t nB) {
+    if (!ctx || !A || !B) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int { ctx->eng.load_ksk(A, nA, B, nB); return FHE_HIP_OK; });
+}
+
+static bool io_ok(size_t count, const void* a, const void* b, const void* c, const void* d, const void* e,
+                  const void* f) {
+    return count == 0 || (a && b && c && d && e && f);
+}
+
+int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
+                               const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a1, b1, a2, b2, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.eval_gate_host(gate, count, a1, b1, a2, b2, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
+                                      const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2,
+                                      uint64_t* d_a_out, uint64_t* d_b_out, void* stream) {
+    if (!ctx || !io_ok(count, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.eval_gate_device(gate, count, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
+                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
+                                  const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b) {
+    if (!ctx || !io_ok(count, a1, b1, a2, b2, ext_a, ext_b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.bootstrap_extended_host(gate, count, a1, b1, a2, b2, ext_a, ext_b);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
+                            uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.keyswitch_host(count, a, b, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, uint32_t len, size_t count,
+                            const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (q_from == 0 || q_to == 0 || q_from >= (1ull << 40) || q_to >= (1ull << 20))
+        return fail(FHE_HIP_ERR_INVALID_PARAM, "modswitch: moduli out of the exact-integer range");
+    return guarded([&]() -> int {
+        if (count == 0) return FHE_HIP_OK;
+        const size_t words = count * (size_t)len;
+        for (size_t i = 0; i < words; ++i)
+            if (a[i] >= q_from) return fail(FHE_HIP_ERR_INVALID_PARAM, "modswitch input not reduced");
+        uint64_t* d = nullptr;
+        FHE_HIP_CHECK(hipSetDevice(ctx->eng.device()));
+        FHE_HIP_CHECK(hipMalloc(&d, (2 * words + 2 * count) * 8));
+        hipStream_t s = ctx->eng.stream();
+        hipError_t e = hipMemcpyAsync(d, a, words * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(d + words, b, count * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = launch_modswitch(q_from, q_to, len, (uint32_t)count, d, d + words, d + words + count,
+                                 d + 2 * words + count, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(a_out, d + words + count, words * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(b_out, d + 2 * words + count, count * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        (void)hipFree(d);
+        if (e != hipSuccess) return hip_fail(e, "modswitch");
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_keygen(int paramset, int method, uint64_t seed, uint64_t* sk, uint64_t* bsk, uint64_t* kskA,
+                   uint64_t* kskB) {
+    if (!sk || !bsk || !kskA || !kskB) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        Params p = make_params(paramset, method);
+        KeySet ks;
+        std::vector<uint64_t> s;
+        keygen_secret(p, seed, s);
+        keygen_bootstrap(p, s, seed, ks);
+        std::copy(ks.sk.begin(), ks.sk.end(), sk);
+        std::copy(ks.bsk.begin(), ks.bsk.end(), bsk);
+        std::copy(ks.kskA.begin(), ks.kskA.end(), kskA);
+        std::copy(ks.kskB.begin(), ks.kskB.end(), kskB);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_encrypt(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
+                    uint64_t* a, uint64_t* b) {
+    if (!sk || (count && (!bits || !a || !b))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        encrypt(make_params(paramset, method), sk, bits, count, seed, a, b);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_decrypt(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b, size_t count,
+                    uint32_t len, uint64_t mod, int64_t* out) {
+    if (!sk || (count && (!a || !b || !out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        Params p = make_params(paramset, method);
+        if (len != p.n && len != p.N) return fail(FHE_HIP_ERR_INVALID_PARAM, "len must be n or N");
+        for (size_t i = 0; i < count; ++i) out[i] = decrypt(p, sk, a + i * len, b[i], len, mod);
+        return FHE_HIP_OK;
+    });
 }
 
 }  // extern "C"

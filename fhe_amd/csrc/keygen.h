@@ -1,0 +1,42 @@
+// keygen.h -- deterministic, seeded host key generation / encryption / decryption.
+//
+// Produces keys with exactly the reference's structure and raw layout, so that
+// the reference itself can consume them through BTKeyLoad
+// (src/binfhe/include/binfhecontext.h:273-275):
+//   LWE secret  : LWEEncryptionScheme::KeyGen / KeyGenGaussian   (lwe-pke.cpp:48-56), stored mod qKS
+//   RLWE secret : skN (BinFHEScheme::KeyGen, binfhe-base-scheme.cpp:39-73), stored mod Q
+//   GINX BSK    : RingGSWAccumulatorCGGI::KeyGenAcc/KeyGenCGGI   (rgsw-acc-cggi.cpp:39-96)
+//   LMKCDEY BSK : RingGSWAccumulatorLMKCDEY::KeyGenAcc/KeyGenLMKCDEY/KeyGenAuto
+//                                                                (rgsw-acc-lmkcdey.cpp:39-226)
+//   KSK         : LWEEncryptionScheme::KeySwitchGen             (lwe-pke.cpp:264-344)
+//   Encrypt     : LWEEncryptionScheme::Encrypt                  (lwe-pke.cpp:116-146)
+// Differences from the reference, which do not affect evaluation parity
+// (evaluation is deterministic given the keys): randomness comes from a
+// seeded counter-based generator instead of BLAKE2, Gaussian samples are a
+// centred binomial with k = 20 (sigma ~ 3.16 vs the reference's 3.19), and the
+// uniform mask of each RGSW row is drawn directly in the EVALUATION domain
+// (the NTT of a uniform polynomial is uniform).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "params.h"
+
+namespace fhe_amd {
+
+struct KeySet {
+    std::vector<uint64_t> sk;    // n, mod qKS
+    std::vector<uint64_t> skN;   // N, mod Q
+    std::vector<uint64_t> bsk;   // Params::bsk_words()
+    std::vector<uint64_t> kskA;  // ksk_rows() * n
+    std::vector<uint64_t> kskB;  // ksk_rows()
+};
+
+void keygen_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& sk);
+void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed, KeySet& out);
+void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
+             uint64_t* b);
+int64_t decrypt(const Params& p, const uint64_t* sk, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod);
+
+}  // namespace fhe_amd

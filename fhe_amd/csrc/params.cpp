@@ -1,0 +1,71 @@
+// params.cpp -- see params.h.
+#include "params.h"
+
+#include <cmath>
+#include <stdexcept>
+
+#include "nt.h"
+
+namespace fhe_amd {
+
+size_t Params::bsk_words() const {
+    if (method == M_GINX) return (size_t)n * 2 * digitsG2 * 2 * N;
+    return (size_t)n * digitsG2 * 2 * N + (size_t)(numAutoKeys + 1) * (digitsG - 1) * 2 * N;
+}
+
+uint64_t Params::gate_const(int gate) const {
+    switch (gate) {
+        case G_OR: return 5ull * (q >> 3);
+        case G_AND: return 7ull * (q >> 3);
+        case G_NOR: return 1ull * (q >> 3);
+        case G_NAND: return 3ull * (q >> 3);
+        case G_XOR: return 6ull * (q >> 3);
+        case G_XNOR: return 2ull * (q >> 3);
+        case G_MAJORITY: return 7ull * (q >> 3);
+        case G_AND3: return 11ull * (q / 12);
+        case G_OR3: return 7ull * (q / 12);
+        case G_AND4: return 15ull * (q >> 4);
+        case G_OR4: return 9ull * (q >> 4);
+        case G_XOR_FAST: return 6ull * (q >> 3);
+        case G_XNOR_FAST: return 2ull * (q >> 3);
+        default: throw std::invalid_argument("unsupported gate");
+    }
+}
+
+Params make_params(int paramset, int method) {
+    //            bits cyc   n    q     qKS    Bks  Bg    nAuto keyDist   (binfhecontext.cpp:113-159)
+    uint32_t bits, cyc, n, q, qks, bks, bg, nauto;
+    int kd;
+    switch (paramset) {
+        case PS_TOY:            bits = 27; cyc = 1024; n = 64;  q = 512;  qks = 0;     bks = 25; bg = 512;  nauto = 9;  kd = KD_UNIFORM_TERNARY; break;
+        case PS_STD128:         bits = 27; cyc = 2048; n = 503; q = 1024; qks = 16384; bks = 32; bg = 512;  nauto = 10; kd = KD_UNIFORM_TERNARY; break;
+        case PS_STD128_LMKCDEY: bits = 28; cyc = 2048; n = 447; q = 2048; qks = 16384; bks = 32; bg = 1024; nauto = 10; kd = KD_GAUSSIAN; break;
+        default: throw std::invalid_argument("unsupported parameter set (TOY, STD128, STD128_LMKCDEY)");
+    }
+    if (method != M_GINX && method != M_LMKCDEY) throw std::invalid_argument("unsupported method (GINX, LMKCDEY)");
+    Params p;
+    p.paramset = paramset;
+    p.method = method;
+    p.n = n;
+    p.N = cyc / 2;
+    p.q = q;
+    p.Q = last_prime(bits, cyc);
+    p.qKS = qks ? qks : (uint32_t)p.Q;  // modKS == PRIME -> Q
+    p.baseKS = bks;
+    p.digitsKS = (uint32_t)std::ceil(std::log((double)p.qKS) / std::log((double)bks));  // lwe-pke.cpp:354
+    p.baseG = bg;
+    p.gBits = ilog2(bg);
+    p.digitsG = (uint32_t)std::ceil(std::log((double)p.Q) / std::log((double)bg));      // rgsw-cryptoparameters.h:93-94
+    p.digitsG2 = (p.digitsG - 1) * 2;
+    p.numAutoKeys = nauto;
+    p.keyDist = kd;
+    p.psi = root_of_unity(cyc, p.Q);
+    uint64_t v = 1;
+    for (uint32_t i = 0; i < p.digitsG; ++i) {
+        p.gpow.push_back(v);
+        v = mulmod(v, bg, p.Q);
+    }
+    return p;
+}
+
+}  // namespace fhe_amd

@@ -63,6 +63,72 @@ int fhe_hip_ntt_batch_device(fhe_hip_ntt_plan* plan, const uint64_t* d_in, uint6
 void* fhe_hip_ntt_plan_stream(fhe_hip_ntt_plan* plan);
 
 /* ------------------------------------------------------------------------ */
+/* Gate bootstrapping context (one per device).                             */
+/*   Replaces BinFHEContext::EvalBinGate / EvalBinGateBatch and the seam's   */
+/*   BlindRotateBatch + KeySwitchBatch + ModSwitchBatch (backend.h:177-211). */
+/* Parameter sets / methods / gates use the reference's enum values         */
+/*   (src/binfhe/include/binfhe-constants.h:49-126):                         */
+/*   paramset TOY=0, STD128=3, STD128_LMKCDEY=21; method GINX=2, LMKCDEY=3;   */
+/*   gate OR=0 AND=1 NOR=2 NAND=3 XOR=4 XNOR=5 XOR_FAST=11 XNOR_FAST=12.      */
+/* Raw key layouts (u64 words, the reference's values):                     */
+/*   GINX bsk    [n][2 (s=+1, s=-1)][digitsG2][2][N]  EVAL (bit-reversed)   */
+/*               = (*BSkey)[0][0..1][i] (rgsw-acc-cggi.cpp:39-57)           */
+/*   LMKCDEY bsk [n][digitsG2][2][N] ++ [numAutoKeys+1][digitsG-1][2][N]    */
+/*               = (*BSkey)[0][0][i] ++ (*BSkey)[0][1][k] (rgsw-acc-lmkcdey.cpp:39-68) */
+/*   ksk A [N][baseKS][digitsKS][n], ksk B [N][baseKS][digitsKS]            */
+/*               = LWESwitchingKeyImpl::GetElementsA/B (lwe-keyswitchkey.h:49) */
+/* Ciphertexts: a[count][len], b[count] (len n for gate inputs/outputs).    */
+/* ------------------------------------------------------------------------ */
+typedef struct fhe_hip_ctx fhe_hip_ctx;
+
+typedef struct {
+    uint32_t paramset, method, n, N, q, qKS, baseKS, digitsKS, baseG, digitsG, numAutoKeys, keyDist;
+    uint64_t Q, psi, bsk_words, ksk_rows;
+} fhe_hip_params;
+
+/* parameters of a set (host only; GenerateBinFHEContext, binfhecontext.cpp:107-179) */
+int fhe_hip_params_get(int paramset, int method, fhe_hip_params* out);
+int fhe_hip_create(int paramset, int method, int device, fhe_hip_ctx** out);
+void fhe_hip_destroy(fhe_hip_ctx* ctx);
+int fhe_hip_get_params(const fhe_hip_ctx* ctx, fhe_hip_params* out);
+/* the context's stream (hipStream_t) */
+void* fhe_hip_stream(fhe_hip_ctx* ctx);
+/* upload keys (BTKeyLoad, binfhecontext.h:273-275; Backend::PackBootstrappingKey) */
+int fhe_hip_load_bsk(fhe_hip_ctx* ctx, const uint64_t* bsk, size_t n_words);
+int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint64_t* B, size_t nB);
+/* EvalBinGate over count independent pairs (binfhe-base-scheme.cpp:76-126).
+ * Inputs mod q, dimension n; outputs likewise.  ct1 and ct2 must not alias
+ * (the reference's ct1 == ct2 check, :85-86, becomes a documented precondition). */
+int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
+                               const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out);
+/* same on device buffers, asynchronous on stream (NULL = context stream) */
+int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
+                                      const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2,
+                                      uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* EvalBinGate(..., extended = true): ctExt before SwitchCTtoqn, dimension N, mod Q */
+int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
+                                  const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b);
+/* LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372): (N, qKS) -> (n, qKS) */
+int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
+                            uint64_t* b_out);
+/* LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:254-261) */
+int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, uint32_t len, size_t count,
+                            const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
+
+/* ------------------------------------------------------------------------ */
+/* Deterministic host key material (KeyGen / BTKeyGen / Encrypt / Decrypt,   */
+/*   binfhecontext.cpp:185-307) -- seeded, same structure as the reference. */
+/* ------------------------------------------------------------------------ */
+/* sk[n] (mod qKS), bsk[bsk_words], kskA[ksk_rows*n], kskB[ksk_rows] */
+int fhe_hip_keygen(int paramset, int method, uint64_t seed, uint64_t* sk, uint64_t* bsk, uint64_t* kskA,
+                   uint64_t* kskB);
+/* a[count][n], b[count] mod q, plaintext modulus 4 */
+int fhe_hip_encrypt(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
+                    uint64_t* a, uint64_t* b);
+int fhe_hip_decrypt(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b, size_t count,
+                    uint32_t len, uint64_t mod, int64_t* out);
+
+/* ------------------------------------------------------------------------ */
 /* Device memory (Backend::Allocate/Free/CopyToDevice/CopyToHost/Synchronize, */
 /*   backend.h:94-114)                                                       */
 /* ------------------------------------------------------------------------ */

@@ -14,6 +14,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle_lib import GINX, LMKCDEY, STD128, STD128_LMKCDEY, Ref  # noqa: E402
 
 NTT_MODULI = {
@@ -42,7 +43,54 @@ def make_ntt():
         print(name, Q, psi, "ok")
 
 
+GATE_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY)}
+GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}
+PER_GATE = 8
+
+
+def gate_inputs(ps, m, key_seed):
+    """Deterministic keys (fhe_amd host keygen, seeded) + encrypted inputs."""
+    from fhe_amd import binfhe as bf
+    keys = bf.keygen(ps, m, key_seed)
+    rng = np.random.default_rng(key_seed)
+    bits1 = rng.integers(0, 2, size=(len(GATES), PER_GATE))
+    bits2 = rng.integers(0, 2, size=(len(GATES), PER_GATE))
+    a1, b1 = bf.encrypt(ps, m, keys.sk, bits1.ravel(), key_seed + 1)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, bits2.ravel(), key_seed + 2)
+    return keys, bits1, bits2, a1, b1, a2, b2
+
+
+def make_gates(names=("std128", "lmkcdey")):
+    for name in names:
+        ps, m = GATE_SETS[name]
+        key_seed = 0xB0070000 + ps
+        keys, bits1, bits2, a1, b1, a2, b2 = gate_inputs(ps, m, key_seed)
+        ref = Ref(ps, m)
+        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        outs, exts, extb, outb = [], [], [], []
+        for gi, (gname, g) in enumerate(GATES.items()):
+            sl = slice(gi * PER_GATE, (gi + 1) * PER_GATE)
+            ao, bo = ref.eval_gate(g, a1[sl], b1[sl], a2[sl], b2[sl])
+            ea, eb = ref.eval_gate(g, a1[sl], b1[sl], a2[sl], b2[sl], extended=True)
+            outs.append(ao); outb.append(bo); exts.append(ea); extb.append(eb)
+        outs, outb, exts, extb = map(np.concatenate, (outs, outb, exts, extb))
+        # intermediates of SwitchCTtoqn on ctExt: ModSwitch(Q -> qKS), KeySwitch, ModSwitch(qKS -> q)
+        ms_a, ms_b = ref.modswitch(ref.Q, ref.qKS, exts, extb)
+        ks_a, ks_b = ref.keyswitch(ms_a, ms_b)
+        np.savez_compressed(os.path.join(HERE, f"gates_{name}.npz"), paramset=ps, method=m, key_seed=np.uint64(key_seed),
+                            gates=np.array(list(GATES.values())), bits1=bits1, bits2=bits2,
+                            out_a=outs.astype(np.uint16), out_b=outb.astype(np.uint16),
+                            ext_a=exts[::PER_GATE // 2].astype(np.uint32), ext_b=extb.astype(np.uint32),
+                            ext_sha=np.array(sha(exts)), ks_sha=np.array(sha(ks_a) + sha(ks_b)),
+                            ms_sha=np.array(sha(ms_a) + sha(ms_b)),
+                            keys_sha=np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB)),
+                            in_sha=np.array(sha(a1) + sha(b1) + sha(a2) + sha(b2)))
+        print(name, "ok", outs.shape)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("ntt", "all"):
         make_ntt()
+    if what in ("gates", "all"):
+        make_gates(sys.argv[2:] or ("std128",))

@@ -1,0 +1,205 @@
+"""EvalBinGate parity: fhe_amd (HIP) vs the reference (golden vectors produced by
+the reference itself, tests/golden/make_golden.py) and vs the oracle restatement."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TRUTH = {0: np.logical_or, 1: np.logical_and, 2: lambda a, b: ~(a | b) & 1, 3: lambda a, b: ~(a & b) & 1,
+         4: np.logical_xor, 5: lambda a, b: ~(a ^ b) & 1}
+SETS = ["std128"]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.uint64).tobytes()).hexdigest()
+
+
+_cache = {}
+
+
+def fixture(name):
+    """(golden npz, keys, inputs) -- keys/inputs regenerated from the recorded seeds."""
+    if name not in _cache:
+        import sys
+        sys.path.insert(0, GOLD)
+        from make_golden import gate_inputs
+        g = np.load(os.path.join(GOLD, f"gates_{name}.npz"))
+        keys, bits1, bits2, a1, b1, a2, b2 = gate_inputs(int(g["paramset"]), int(g["method"]), int(g["key_seed"]))
+        _cache[name] = (g, keys, (a1, b1, a2, b2))
+    return _cache[name]
+
+
+def per_gate(g):
+    pg = g["bits1"].shape[1]
+    return [(i, int(gate), slice(i * pg, (i + 1) * pg)) for i, gate in enumerate(g["gates"])]
+
+
+# ----------------------------------------------------------------- CPU ----
+@pytest.mark.parametrize("name", SETS)
+def test_keygen_and_inputs_deterministic(name):
+    g, keys, (a1, b1, a2, b2) = fixture(name)
+    assert sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB) == str(g["keys_sha"])
+    assert sha(a1) + sha(b1) + sha(a2) + sha(b2) == str(g["in_sha"])
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_reference_outputs_decrypt_to_truth_table(name):
+    """the reference, run on our keys, computes the gates correctly (our keys are valid)."""
+    from fhe_amd import binfhe as bf
+    g, keys, _ = fixture(name)
+    dec = bf.decrypt(int(g["paramset"]), int(g["method"]), keys.sk, g["out_a"].astype(np.uint64),
+                     g["out_b"].astype(np.uint64))
+    for i, gate, sl in per_gate(g):
+        exp = TRUTH[gate](g["bits1"][i], g["bits2"][i]).astype(np.int64)
+        assert np.array_equal(dec[sl], exp), (gate, dec[sl], exp)
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_oracle_matches_reference_golden(name, restatement):
+    from oracle_lib import Restatement
+    g, keys, (a1, b1, a2, b2) = fixture(name)
+    O = Restatement(int(g["paramset"]), int(g["method"]))
+    exts = []
+    for i, gate, sl in per_gate(g):
+        ao, bo = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        assert np.array_equal(ao, g["out_a"][sl]) and np.array_equal(bo, g["out_b"][sl])
+        ea, eb = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, gate, a1[sl], b1[sl], a2[sl], b2[sl], stage=1)
+        exts.append(ea)
+        assert np.array_equal(eb, g["ext_b"][sl])
+    assert sha(np.concatenate(exts)) == str(g["ext_sha"])
+
+
+def test_modswitch_integer_form_equals_reference_double():
+    """RoundqQ (lwe-pke.cpp:41-46) is floor(0.5 + v*q/Q) in IEEE double; the kernels use the
+    integer form floor((2 v q + Q) / (2 Q)) mod q.  Exhaustive over every v for each switch
+    on the path (Q -> qKS for both STD128 moduli, qKS -> q for q = 1024, 2048)."""
+    for Q, q in ((134215681, 16384), (268369921, 16384), (16384, 1024), (16384, 2048)):
+        for lo in range(0, Q, 1 << 24):
+            v = np.arange(lo, min(Q, lo + (1 << 24)), dtype=np.uint64)
+            dbl = np.floor(0.5 + v.astype(np.float64) * float(q) / float(Q)).astype(np.uint64) % q
+            it = ((2 * v * q + Q) // (2 * Q)) % q
+            assert np.array_equal(dbl, it), (Q, q, lo)
+
+
+# ----------------------------------------------------------------- GPU ----
+_engines = {}
+
+
+def engine(name):
+    from fhe_amd import binfhe as bf
+    if name not in _engines:
+        g, keys, _ = fixture(name)
+        e = bf.GateEngine(int(g["paramset"]), int(g["method"]))
+        e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        _engines[name] = e
+    return _engines[name]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_gates_bit_exact_vs_reference(name):
+    g, keys, (a1, b1, a2, b2) = fixture(name)
+    e = engine(name)
+    for i, gate, sl in per_gate(g):
+        ao, bo = e.eval_gate(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        assert np.array_equal(ao, g["out_a"][sl]), f"gate {gate} a mismatch"
+        assert np.array_equal(bo, g["out_b"][sl]), f"gate {gate} b mismatch"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_extended_bit_exact_vs_reference(name):
+    """EvalBinGate(extended=true): the blind-rotated accumulator after Transpose/iNTT (ctExt)."""
+    g, keys, (a1, b1, a2, b2) = fixture(name)
+    e = engine(name)
+    exts = []
+    for i, gate, sl in per_gate(g):
+        ea, eb = e.eval_gate_extended(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        exts.append(ea)
+        assert np.array_equal(eb, g["ext_b"][sl])
+    exts = np.concatenate(exts)
+    assert np.array_equal(exts[::exts.shape[0] // len(g["ext_a"])], g["ext_a"])
+    assert sha(exts) == str(g["ext_sha"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_keyswitch_and_modswitch_vs_reference(name):
+    """SwitchCTtoqn stages on the reference's own ctExt: ModSwitch(Q->qKS), KeySwitch."""
+    g, keys, (a1, b1, a2, b2) = fixture(name)
+    e = engine(name)
+    P = e.params
+    # rebuild the reference's ctExt for the gates whose full ext is stored, via our extended path
+    exts, extb = [], []
+    for i, gate, sl in per_gate(g):
+        ea, eb = e.eval_gate_extended(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        exts.append(ea)
+        extb.append(eb)
+    exts, extb = np.concatenate(exts), np.concatenate(extb)
+    ms_a, ms_b = e.modswitch(P.Q, P.qKS, exts, extb)
+    assert sha(ms_a) + sha(ms_b) == str(g["ms_sha"])
+    ks_a, ks_b = e.keyswitch(ms_a, ms_b)
+    assert sha(ks_a) + sha(ks_b) == str(g["ks_sha"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_ragged_batches_vs_oracle(name, restatement):
+    from fhe_amd import binfhe as bf
+    from oracle_lib import Restatement
+    g, keys, _ = fixture(name)
+    ps, m = int(g["paramset"]), int(g["method"])
+    O = Restatement(ps, m)
+    e = engine(name)
+    rng = np.random.default_rng(11)
+    for count, gate in ((1, 1), (3, 4), (5, 3), (7, 0), (13, 5)):   # partial workgroups
+        x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+        a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 100 + count)
+        a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 200 + count)
+        ao, bo = e.eval_gate(gate, a1, b1, a2, b2)
+        oa, ob = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, gate, a1, b1, a2, b2)
+        assert np.array_equal(ao, oa) and np.array_equal(bo, ob)
+        dec = bf.decrypt(ps, m, keys.sk, ao, bo)
+        assert np.array_equal(dec, TRUTH[gate](x1, x2).astype(np.int64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_large_batch_truth_and_determinism(name):
+    """size-independent properties at a bench-sized batch: every gate decrypts to its
+    truth value, and two runs are bit-identical."""
+    from fhe_amd import binfhe as bf
+    g, keys, _ = fixture(name)
+    ps, m = int(g["paramset"]), int(g["method"])
+    e = engine(name)
+    count = 4096
+    rng = np.random.default_rng(5)
+    x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+    a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 31)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 32)
+    ao, bo = e.eval_gate(3, a1, b1, a2, b2)
+    ao2, bo2 = e.eval_gate(3, a1, b1, a2, b2)
+    assert np.array_equal(ao, ao2) and np.array_equal(bo, bo2)
+    dec = bf.decrypt(ps, m, keys.sk, ao, bo)
+    assert np.array_equal(dec, TRUTH[3](x1, x2).astype(np.int64))
+
+
+@pytest.mark.gpu
+def test_gpu_binfhecontext_api_truth_tables():
+    """the reference-shaped API (UnitTestFHEW.cpp:175-239 truth tables)."""
+    from fhe_amd import binfhe as bf
+    cc = bf.BinFHEContext()
+    cc.GenerateBinFHEContext(bf.STD128, bf.GINX)
+    sk = cc.KeyGen()
+    cc.BTKeyGen(sk)
+    for gate in (bf.AND, bf.OR, bf.NAND, bf.NOR, bf.XOR, bf.XNOR):
+        for x in (0, 1):
+            for y in (0, 1):
+                r = cc.EvalBinGate(gate, cc.Encrypt(sk, x), cc.Encrypt(sk, y))
+                assert cc.Decrypt(sk, r) == int(TRUTH[gate](np.array(x), np.array(y))), (gate, x, y)
+    ct = cc.Encrypt(sk, 1)
+    with pytest.raises(Exception):
+        cc.EvalBinGate(bf.AND, ct, ct)
+    assert cc.EvalBinGateBatch(bf.AND, [], []) == []
