@@ -49,6 +49,8 @@ def _setup(L):
     L.fhe_hip_load_ksk.argtypes = [vp, vp, sz, vp, sz]
     L.fhe_hip_eval_bingate_batch.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp]
     L.fhe_hip_eval_bingate_batch_device.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_blind_rotate_batch_device.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp]
+    L.fhe_hip_keyswitch_workspace_device.argtypes = [vp, sz, vp, vp, vp]
     L.fhe_hip_eval_bingate_extended.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp]
     L.fhe_hip_keyswitch_batch.argtypes = [vp, sz, vp, vp, vp, vp]
     L.fhe_hip_modswitch_batch.argtypes = [vp, u64, u64, ctypes.c_uint32, sz, vp, vp, vp, vp]
@@ -181,6 +183,14 @@ class GateEngine:
     def eval_gate_device(self, gate, count, d_a1, d_b1, d_a2, d_b2, d_ao, d_bo, stream=None):
         check(L().fhe_hip_eval_bingate_batch_device(self._h, gate, count, vp(d_a1), vp(d_b1), vp(d_a2), vp(d_b2),
                                                     vp(d_ao), vp(d_bo), vp(stream) if stream else None))
+
+    def blind_rotate_device(self, gate, count, d_a1, d_b1, d_a2, d_b2, stream=None):
+        check(L().fhe_hip_blind_rotate_batch_device(self._h, gate, count, vp(d_a1), vp(d_b1), vp(d_a2), vp(d_b2),
+                                                    vp(stream) if stream else None))
+
+    def keyswitch_workspace_device(self, count, d_ao, d_bo, stream=None):
+        check(L().fhe_hip_keyswitch_workspace_device(self._h, count, vp(d_ao), vp(d_bo),
+                                                     vp(stream) if stream else None))
 
     def keyswitch(self, a, b):
         a, b = _u64(a), _u64(b)

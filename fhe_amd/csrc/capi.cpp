@@ -239,6 +239,26 @@ int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, 
     });
 }
 
+int fhe_hip_blind_rotate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
+                                      const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2, void* stream) {
+    if (!ctx || !io_ok(count, d_a1, d_b1, d_a2, d_b2, d_a1, d_b1)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.bootstrap_device(gate, count, d_a1, d_b1, d_a2, d_b2, true,
+                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_keyswitch_workspace_device(fhe_hip_ctx* ctx, size_t count, uint64_t* d_a_out, uint64_t* d_b_out,
+                                       void* stream) {
+    if (!ctx || (count && (!d_a_out || !d_b_out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.keyswitch_workspace_device(count, d_a_out, d_b_out,
+                                            stream ? (hipStream_t)stream : ctx->eng.stream());
+        return FHE_HIP_OK;
+    });
+}
+
 int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
                                   const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b) {
     if (!ctx || !io_ok(count, a1, b1, a2, b2, ext_a, ext_b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");

@@ -205,13 +205,21 @@ void Engine::bootstrap_device(int gate, size_t count, const uint64_t* a1, const 
     FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
 }
 
+void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    if (!d_ksk_) throw std::logic_error("key-switching key not loaded");
+    if (count == 0) return;
+    if (count > cap_) throw std::logic_error("workspace holds fewer ciphertexts than requested");
+    GateArgs g = gate_args(G_AND, count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, p_.q, a_out, b_out, s));
+}
+
 void Engine::eval_gate_device(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
                               const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
     if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
     if (count == 0) return;
     bootstrap_device(gate, count, a1, b1, a2, b2, true, s);
-    GateArgs g = gate_args(gate, count);
-    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, p_.q, a_out, b_out, s));
+    keyswitch_workspace_device(count, a_out, b_out, s);
 }
 
 void Engine::eval_gate_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,

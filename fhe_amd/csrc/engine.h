@@ -54,6 +54,8 @@ public:
     // stage outputs on device: ctExt (count x N, mod Q) or mod-switched to qKS
     void bootstrap_device(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
                           const uint64_t* b2, bool modswitch, hipStream_t s);
+    // KeySwitch + ModSwitch(qKS -> q) of the workspace left by bootstrap_device(modswitch = true)
+    void keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
     const uint32_t* ext_a() const { return d_ext_a_; }
     const uint32_t* ext_b() const { return d_ext_b_; }
 

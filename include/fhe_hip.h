@@ -105,6 +105,14 @@ int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const u
 int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
                                       const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2,
                                       uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* The two stages of fhe_hip_eval_bingate_batch_device, separately launchable
+ * (Backend::BlindRotateBatch, then KeySwitchBatch + ModSwitchBatch):
+ * blind_rotate leaves the mod-switched ctExt (N+1 values mod qKS per gate) in
+ * the context's workspace; keyswitch consumes it. */
+int fhe_hip_blind_rotate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
+                                      const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2, void* stream);
+int fhe_hip_keyswitch_workspace_device(fhe_hip_ctx* ctx, size_t count, uint64_t* d_a_out, uint64_t* d_b_out,
+                                       void* stream);
 /* EvalBinGate(..., extended = true): ctExt before SwitchCTtoqn, dimension N, mod Q */
 int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
                                   const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b);
