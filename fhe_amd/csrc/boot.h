@@ -33,6 +33,13 @@ hipError_t launch_prep_ginx(const GateArgs& g, const uint64_t* a1, const uint64_
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
+// LMKCDEY: per-gate op schedule (EXT(i) / AUTO(t)), then the fused accumulator
+hipError_t launch_prep_lmk(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
+                           const uint64_t* b2, const int16_t* logGen, uint16_t* scratch, uint16_t* ops,
+                           uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys, hipStream_t s);
+hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const void* bsk, const void* autok,
+                                   const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                   uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q) (:254-261), KSK as u16 rows of 512
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
                             const uint32_t* ms_a, const uint32_t* ms_b, uint32_t q_out, uint64_t* a_out,

@@ -244,14 +244,11 @@ __global__ void __launch_bounds__(256, 2)
             dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
         }
         // --- NTT of the four digit polynomials (two per pass, one per half)
-#ifndef ABL_NO_FWD
         fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
         fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
-#endif
         // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
         //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
         //     out so that each load instruction reads 1 KiB contiguous.
-#ifndef ABL_NO_MAC
         const uint2* ki   = bsk + (size_t)i * (2 * 4 * 16 * 64) + lane;
         const uint32_t ab = (a * lbase) & 2047;
 #pragma unroll
@@ -283,10 +280,6 @@ __global__ void __launch_bounds__(256, 2)
                 acc[r]            = add_mod(acc[r], csub(mont_red(S, m), m.Q), m.Q);
             }
         }
-#else
-#pragma unroll
-        for (int r = 0; r < 32; ++r) acc[r] ^= dA[r] + dB[r] + a;
-#endif
     }
 
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
@@ -330,6 +323,278 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
     hipLaunchKernelGGL(k_blind_rotate_ginx, dim3(blocks), dim3(256), kBootLds, s, g, t,
                        reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
+    return hipGetLastError();
+}
+
+
+// ===========================================================================
+// LMKCDEY (RingGSWAccumulatorLMKCDEY::EvalAcc, src/binfhe/lib/rgsw-acc-lmkcdey.cpp:70-158)
+// ===========================================================================
+// Schedule ops, per gate, in the reference's exact order:
+//   EXT(i)  (i < 0x8000): AddToAccLMKCDEY with (*ek)[0][0][i]            (:228-254)
+//   AUTO(t) (0x8000 | t): Automorphism by 5^t (t >= 1) or by 2N-5 (t = 0)
+//                         with (*ek)[0][1][t]                              (:257-287)
+// k_prep_lmk builds them with a stable counting sort of the a_i into the
+// logGen groups (permuteMap, :83-94) and replays the nSkips logic (:99-157).
+__global__ void k_prep_lmk(const uint64_t* __restrict__ a1, const uint64_t* __restrict__ b1,
+                           const uint64_t* __restrict__ a2, const uint64_t* __restrict__ b2, GateArgs g,
+                           const int16_t* __restrict__ logGen, uint16_t* __restrict__ scratch,
+                           uint16_t* __restrict__ ops, uint32_t* __restrict__ nops, uint32_t* __restrict__ tvb,
+                           uint32_t maxops, uint32_t numAutoKeys) {
+    const uint32_t gate = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gate >= g.count) return;
+    const uint32_t N = g.N, M = 2 * N, Nh = N / 2, n = g.n, qm = g.q - 1;
+    uint16_t* end    = scratch + (size_t)gate * (N + n);  // per position: counts -> bucket ends
+    uint16_t* sorted = end + N;
+    for (uint32_t p = 0; p < N; ++p) end[p] = 0;
+    const uint64_t* A1 = a1 + (size_t)gate * n;
+    const uint64_t* A2 = a2 + (size_t)gate * n;
+    auto pos_of = [&](uint32_t i) -> uint32_t {
+        uint32_t a = (uint32_t)((A1[i] + A2[i]) & qm);
+        if (g.xor_double) a = (2 * a) & qm;
+        const uint32_t aodd = ((M - a) & (M - 1)) | 1u;  // (0 - a_i) mod 2N, made odd
+        const int32_t v     = logGen[aodd];
+        if (v == (int32_t)M) return Nh - 1;                          // -1
+        if (v < 0) return Nh - 1 - (uint32_t)(-v);                   // -5^i
+        return 2 * Nh - 1 - (uint32_t)v;                             // +5^i (v = 0 -> N-1)
+    };
+    for (uint32_t i = 0; i < n; ++i) end[pos_of(i)]++;
+    uint32_t run = 0;
+    for (uint32_t p = 0; p < N; ++p) {
+        const uint32_t c = end[p];
+        end[p]           = (uint16_t)run;
+        run += c;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t p = pos_of(i);
+        sorted[end[p]++] = (uint16_t)i;  // stable: increasing i within a group
+    }
+    uint16_t* o = ops + (size_t)gate * maxops;
+    uint32_t k = 0, nSkips = 0;
+    auto emit_group = [&](uint32_t p) {
+        const uint32_t s = p ? end[p - 1] : 0u;
+        for (uint32_t j = s; j < end[p]; ++j) o[k++] = sorted[j];
+    };
+    for (int half = 0; half < 2; ++half) {
+        const uint32_t base = half ? Nh : 0u;
+        for (uint32_t i = Nh - 1; i > 0; --i) {
+            const uint32_t p = base + (Nh - 1 - i);
+            const uint32_t s = p ? end[p - 1] : 0u;
+            if (end[p] > s) {
+                if (nSkips != 0) {
+                    o[k++] = (uint16_t)(0x8000u | nSkips);
+                    nSkips = 0;
+                }
+                emit_group(p);
+            }
+            nSkips++;
+            if (nSkips == numAutoKeys || i == 1) {
+                o[k++] = (uint16_t)(0x8000u | nSkips);
+                nSkips = 0;
+            }
+        }
+        if (half == 0) {
+            emit_group(Nh - 1);       // -1
+            o[k++] = (uint16_t)0x8000u;  // automorphism by 2N - 5 with key 0
+        } else {
+            emit_group(N - 1);        // 0
+        }
+    }
+    nops[gate] = k;
+    uint32_t b = (uint32_t)((b1[gate] + b2[gate]) & qm);
+    if (g.xor_double) b = (2 * b) & qm;
+    tvb[gate] = b;
+}
+
+namespace {
+// EVAL-domain automorphism X -> X^k (poly-impl.h:350-356 / PrecomputeAutoMap, nbtheory2.cpp:264-275):
+// out[slot brv(j)] = in[slot brv(((2j+1)k mod 2N) >> 1)].  Through the half-wave's LDS region
+// (row stride 33: conflict-free writes).
+FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint32_t k) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) region[l * 33 + r] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const uint32_t x  = (uint32_t)(l << 5) | r;            // output slot
+        const uint32_t j  = __builtin_bitreverse32(x) >> 22;   // brv10
+        const uint32_t t  = (((2 * j + 1) * k) & 2047) >> 1;
+        const uint32_t sx = __builtin_bitreverse32(t) >> 22;   // source slot
+        v[r]              = region[sx + (sx >> 5)];
+    }
+    wave_lds_sync();
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256, 2)
+    k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
+                       const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
+                       const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_twBf = sm;
+    uint32_t* s_twBi = sm + 992;
+    uint32_t* s_tile = sm + 1984;
+    for (int i = threadIdx.x; i < 992; i += 256) {
+        s_twBf[i] = T.twB_fwd[i];
+        s_twBi[i] = T.twB_inv[i];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
+    const uint32_t gate = blockIdx.x * kWaves + wave;
+    if (gate >= g.count) return;
+    uint32_t* tileW = s_tile + wave * 2 * kTile;
+    uint32_t* tile  = tileW + h * kTile;
+    const Mod m{T.Q, T.Q2, T.qinv};
+    const uint32_t M = 2 * g.N;
+
+    uint32_t acc[32];
+    {
+        const uint32_t b = tvb[gate], qm = g.q - 1;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t x = (uint32_t)(r << 5) | l;
+            uint32_t v       = 0;
+            if (h == 1 && x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & qm;
+                v                 = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            acc[r] = v;
+        }
+        fwd_pass(acc, tile, l, T.twA_fwd, s_twBf, m);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(acc[r], m.Q2), m.Q);
+        // acc1 <- acc1(X^(2N-5))   (:99); applied to both halves, acc0 = 0 is invariant
+        automorphism_eval(acc, tile, l, M - 5);
+    }
+
+    const int32_t sh  = 32 - (int32_t)g.gbits;
+    const int32_t Qs  = (int32_t)m.Q;
+    const uint32_t Qh = m.Q >> 1;
+    const uint16_t* gops = ops + (size_t)gate * maxops;
+    const uint32_t cnt   = nops[gate];
+    for (uint32_t it = 0; it < cnt; ++it) {
+        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+        uint32_t dA[32], dB[32];
+        if (!(op & 0x8000u)) {
+            // ---- AddToAccLMKCDEY: acc <- sum_d D_d * ek[i][d]   (acc replaced)
+#pragma unroll
+            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
+            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                int32_t d  = dA[r] < Qh ? (int32_t)dA[r] : (int32_t)dA[r] - Qs;
+                int32_t r0 = (d << sh) >> sh;
+                d          = (d - r0) >> g.gbits;
+                r0         = (d << sh) >> sh;
+                d          = (d - r0) >> g.gbits;
+                int32_t r1 = (d << sh) >> sh;
+                dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
+                dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
+            }
+            fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
+            fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
+            const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                asm volatile("" ::: "memory");
+                uint2 kk[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) kk[d] = ki[(d * 16 + k) * 64];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * k + e;
+                    auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
+                    uint64_t S = (uint64_t)p01[0] * (e ? kk[0].y : kk[0].x) + (uint64_t)p01[1] * (e ? kk[1].y : kk[1].x) +
+                                 (uint64_t)p23[0] * (e ? kk[2].y : kk[2].x) + (uint64_t)p23[1] * (e ? kk[3].y : kk[3].x);
+                    acc[r] = csub(mont_red(S, m), m.Q);
+                }
+            }
+        } else {
+            // ---- Automorphism(5^t or 2N-5, autokey[t])
+            const uint32_t t = op & 0x7fffu;
+            uint32_t kexp    = M - 5;
+            if (t) {
+                kexp = 1;
+                for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
+            }
+            automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
+#pragma unroll
+            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
+            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);  // half 0: COEF acc0'
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                int32_t d  = dA[r] < Qh ? (int32_t)dA[r] : (int32_t)dA[r] - Qs;
+                int32_t r0 = (d << sh) >> sh;
+                d          = (d - r0) >> g.gbits;
+                r0         = (d << sh) >> sh;
+                d          = (d - r0) >> g.gbits;
+                int32_t r1 = (d << sh) >> sh;
+                dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
+                dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
+                // (half 0's digit A, half 0's digit B) -> lower / upper half of dA
+                auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
+                dA[r]   = sw[0];
+            }
+            fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
+            const uint2* ki = autok + (size_t)t * (2 * 16 * 64) + lane;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                asm volatile("" ::: "memory");
+                const uint2 k0 = ki[(0 * 16 + k) * 64], k1 = ki[(1 * 16 + k) * 64];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * k + e;
+                    auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    uint64_t S = (uint64_t)p[0] * (e ? k0.y : k0.x) + (uint64_t)p[1] * (e ? k1.y : k1.x);
+                    const uint32_t v = csub(mont_red(S, m), m.Q);
+                    acc[r] = h ? add_mod(acc[r], v, m.Q) : v;
+                }
+            }
+        }
+    }
+
+    // extraction, identical to GINX
+    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+    wave_lds_sync();
+    if (h == 0) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) tileW[(r << 5) | l] = acc[r];
+    } else if (l == 0) {
+        tileW[1024] = acc[0];
+    }
+    wave_lds_sync();
+    uint32_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+        const uint32_t j = (uint32_t)lane + 64u * t;
+        const uint32_t c = tileW[j == 0 ? 0 : g.N - j];
+        const uint32_t v = (j == 0 || c == 0) ? c : m.Q - c;
+        oa[j]            = g.msb_out ? mod_switch(v, m.Q, g.qKS) : v;
+    }
+    if (lane == 0) {
+        const uint32_t bb = add_mod(g.b_const, tileW[1024], m.Q);
+        ext_b[gate]       = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+hipError_t launch_prep_lmk(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
+                           const uint64_t* b2, const int16_t* logGen, uint16_t* scratch, uint16_t* ops,
+                           uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prep_lmk, dim3((g.count + 63) / 64), dim3(64), 0, s, a1, b1, a2, b2, g, logGen, scratch, ops,
+                       nops, tvb, maxops, numAutoKeys);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const void* bsk, const void* autok,
+                                   const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                   uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
+    const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile) * 4;
+    hipLaunchKernelGGL(k_blind_rotate_lmk, dim3(blocks), dim3(256), lds, s, g, t, reinterpret_cast<const uint2*>(bsk),
+                       reinterpret_cast<const uint2*>(autok), ops, nops, maxops, tvb, ext_a, ext_b);
     return hipGetLastError();
 }
 

@@ -21,17 +21,19 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     if (p_.Q >= (1ull << 28)) throw std::invalid_argument("device path needs Q < 2^28");
     if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
     if (p_.q & (p_.q - 1)) throw std::invalid_argument("device path needs a power-of-two q");
-    if (p_.method != M_GINX) throw std::invalid_argument("device path: method not implemented yet");
+    if (p_.digitsG != 3) throw std::invalid_argument("device path expects digitsG = 3");
     FHE_HIP_CHECK(hipSetDevice(device_));
     FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     build_tables();
+    maxops_ = p_.N + p_.n + 128;
 }
 
 Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_})
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
+                      (void*)d_scratch_})
         if (ptr) (void)hipFree(ptr);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -66,6 +68,19 @@ void Engine::build_tables() {
         mono[e] = to_mont(submod(x, 1, Q), Q);
         x = mulmod(x, p_.psi, Q);
     }
+    if (p_.method == M_LMKCDEY) {  // rgsw-cryptoparameters.cpp:115-127
+        const uint32_t M = 2 * p_.N;
+        std::vector<int16_t> lg(M, 0);
+        uint32_t gp = 1;
+        lg[M - gp] = (int16_t)M;
+        for (uint32_t i = 1; i < p_.N / 2; ++i) {
+            gp = (gp * 5) % M;
+            lg[gp] = (int16_t)i;
+            lg[M - gp] = (int16_t)-(int32_t)i;
+        }
+        FHE_HIP_CHECK(hipMalloc(&d_logGen_, M * sizeof(int16_t)));
+        FHE_HIP_CHECK(hipMemcpy(d_logGen_, lg.data(), M * sizeof(int16_t), hipMemcpyHostToDevice));
+    }
     FHE_HIP_CHECK(hipMalloc(&d_tables_, t.size() * 4));
     FHE_HIP_CHECK(hipMemcpy(d_tables_, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     const uint32_t* d = static_cast<const uint32_t*>(d_tables_);
@@ -87,22 +102,31 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
     const uint64_t Q = p_.Q;
     if (dG2 != 4) throw std::invalid_argument("device path expects digitsG = 3");
-    // GINX raw [n][2][dG2][2][N] -> device uint2 [n][2][dG2][16][64 lanes] (lane = h*32 + l,
-    // slots l*32 + 2k, +1 of component h)
-    std::vector<uint32_t> dev((size_t)n * 2 * dG2 * 2 * N);
+    // device uint2 blocks [..][d][16][64 lanes]: lane = h*32 + l holds slots l*32 + 2k, +1 of
+    // component h -- one 512-byte coalesced load per wave-instruction in the kernels.
+    //   GINX   raw [n][2][dG2][2][N]                 -> [n][2][dG2][16][64]
+    //   LMKCDEY raw [n][dG2][2][N] ++ [nA+1][2][2][N] -> [n][dG2][16][64] ++ [nA+1][2][16][64]
+    const size_t nrgsw = p_.method == M_GINX ? (size_t)n * 2 : (size_t)n;  // RGSW keys of dG2 rows
+    const size_t nauto = p_.method == M_GINX ? 0 : (size_t)p_.numAutoKeys + 1;
+    const uint32_t dA = p_.digitsG - 1;
+    std::vector<uint32_t> dev(nrgsw * dG2 * 2 * N + nauto * dA * 2 * N);
+    auto pack = [&](const uint64_t* src_key, uint32_t rows, uint32_t* dst_key) {
+        for (uint32_t d = 0; d < rows; ++d)
+            for (uint32_t k = 0; k < 16; ++k)
+                for (uint32_t lane = 0; lane < 64; ++lane) {
+                    const uint32_t h = lane >> 5, l = lane & 31;
+                    const size_t src = ((size_t)d * 2 + h) * N + l * 32 + 2 * k;
+                    const size_t dst = (((size_t)d * 16 + k) * 64 + lane) * 2;
+                    dst_key[dst] = to_mont(src_key[src] % Q, Q);
+                    dst_key[dst + 1] = to_mont(src_key[src + 1] % Q, Q);
+                }
+    };
 #pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < (int64_t)n; ++i)
-        for (uint32_t ks = 0; ks < 2; ++ks)
-            for (uint32_t d = 0; d < dG2; ++d)
-                for (uint32_t k = 0; k < 16; ++k)
-                    for (uint32_t lane = 0; lane < 64; ++lane) {
-                        const uint32_t h = lane >> 5, l = lane & 31;
-                        const size_t src = ((((size_t)i * 2 + ks) * dG2 + d) * 2 + h) * N + l * 32 + 2 * k;
-                        const size_t dst = (((((size_t)i * 2 + ks) * dG2 + d) * 16 + k) * 64 + lane) * 2;
-                        if (bsk[src] >= Q || bsk[src + 1] >= Q) continue;  // validated below
-                        dev[dst] = to_mont(bsk[src], Q);
-                        dev[dst + 1] = to_mont(bsk[src + 1], Q);
-                    }
+    for (int64_t i = 0; i < (int64_t)nrgsw; ++i)
+        pack(bsk + (size_t)i * dG2 * 2 * N, dG2, dev.data() + (size_t)i * dG2 * 2 * N);
+    const uint64_t* asrc = bsk + nrgsw * dG2 * 2 * N;
+    uint32_t* adst = dev.data() + nrgsw * dG2 * 2 * N;
+    for (size_t t = 0; t < nauto; ++t) pack(asrc + t * dA * 2 * N, dA, adst + t * dA * 2 * N);
     for (size_t i = 0; i < words; ++i)
         if (bsk[i] >= Q) throw std::invalid_argument("bsk coefficient not reduced mod Q");
     FHE_HIP_CHECK(hipSetDevice(device_));
@@ -110,6 +134,7 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     d_bsk_ = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d_bsk_, dev.size() * 4));
     FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+    d_autok_ = static_cast<uint32_t*>(d_bsk_) + nrgsw * dG2 * 2 * N;
 }
 
 void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB) {
@@ -178,6 +203,14 @@ void Engine::ensure_work(size_t count) {
     FHE_HIP_CHECK(hipMalloc(&d_tvb_, count * sizeof(uint32_t)));
     FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
     FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
+    if (p_.method == M_LMKCDEY) {
+        for (void* ptr : {(void*)d_ops_, (void*)d_nops_, (void*)d_scratch_})
+            if (ptr) FHE_HIP_CHECK(hipFree(ptr));
+        d_ops_ = nullptr; d_nops_ = nullptr; d_scratch_ = nullptr;
+        FHE_HIP_CHECK(hipMalloc(&d_ops_, count * maxops_ * sizeof(uint16_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_nops_, count * sizeof(uint32_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_scratch_, count * (p_.N + p_.n) * sizeof(uint16_t)));
+    }
     cap_ = count;
 }
 
@@ -201,8 +234,15 @@ void Engine::bootstrap_device(int gate, size_t count, const uint64_t* a1, const 
     if (count == 0) return;
     ensure_work(count);
     FHE_HIP_CHECK(hipSetDevice(device_));
-    FHE_HIP_CHECK(launch_prep_ginx(g, a1, b1, a2, b2, d_idx_, d_tvb_, s));
-    FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+    if (p_.method == M_GINX) {
+        FHE_HIP_CHECK(launch_prep_ginx(g, a1, b1, a2, b2, d_idx_, d_tvb_, s));
+        FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+    } else {
+        FHE_HIP_CHECK(launch_prep_lmk(g, a1, b1, a2, b2, d_logGen_, d_scratch_, d_ops_, d_nops_, d_tvb_, maxops_,
+                                      p_.numAutoKeys, s));
+        FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_bsk_, d_autok_, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
+                                              d_ext_b_, s));
+    }
 }
 
 void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {

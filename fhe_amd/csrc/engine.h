@@ -78,6 +78,12 @@ private:
     BootTables tabs_{};
     void* d_tables_ = nullptr;
     void* d_bsk_ = nullptr;
+    void* d_autok_ = nullptr;   // LMKCDEY automorphism keys (inside the d_bsk_ allocation)
+    int16_t* d_logGen_ = nullptr;
+    uint32_t maxops_ = 0;
+    uint16_t* d_ops_ = nullptr;
+    uint32_t* d_nops_ = nullptr;
+    uint16_t* d_scratch_ = nullptr;
     uint16_t* d_ksk_ = nullptr;
     // workspace
     size_t cap_ = 0;
