@@ -19,7 +19,6 @@ Also measured in the same run and reported beside `value`:
                     built from /root/reference) on the host cores, rank 0, N=1.
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -63,15 +62,24 @@ def main():
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from fhe_amd.dist import barrier, env, max_over_ranks
+    rank, world, local = env()
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} differs from --gpus={args.gpus}; using WORLD_SIZE")
+    # rehearsal knobs (not used by the driver): FHE_BENCH_DEVICE_MAP="0,0" puts ranks on
+    # chosen devices, FHE_BENCH_BACKEND=gloo for a one-GPU box
+    dmap = os.environ.get("FHE_BENCH_DEVICE_MAP")
+    if dmap:
+        local = int(dmap.split(",")[local])
+    backend = os.environ.get("FHE_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else None
 
     from fhe_amd import binfhe as bf
     from fhe_amd import NttPlan
@@ -114,15 +122,13 @@ def main():
     torch.cuda.synchronize(dev)
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    barrier()
     elapsed = time.perf_counter() - t_start
     br_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     ks_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
@@ -132,10 +138,8 @@ def main():
     bo = d_bo.cpu().numpy().view(np.uint64)
     verified = bool(np.array_equal(bf.decrypt(ps, method, keys.sk, ao, bo), (x1 & x2).astype(np.int64)))
 
-    if world > 1:
-        t = torch.tensor([elapsed, 0.0 if verified else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, verified = float(t[0]), bool(t[1] == 0.0)
+    elapsed, bad = max_over_ranks([elapsed, 0.0 if verified else 1.0], device=red_dev)
+    verified = bad == 0.0
 
     total_gates = B * world * args.steps
     value = total_gates / elapsed
@@ -179,7 +183,7 @@ def main():
         }
         print(json.dumps(result), flush=True)
     if world > 1:
-        dist.barrier()
+        barrier()
         dist.destroy_process_group()
     return result
 

@@ -57,6 +57,11 @@ def _setup(L):
     L.fhe_hip_keygen.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp, vp, vp, vp]
     L.fhe_hip_encrypt.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, vp, vp]
     L.fhe_hip_decrypt.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, sz, ctypes.c_uint32, u64, vp]
+    L.fhe_hip_multi_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.fhe_hip_multi_destroy.argtypes = [vp]
+    L.fhe_hip_multi_destroy.restype = None
+    L.fhe_hip_multi_load_keys.argtypes = [vp, vp, sz, vp, sz, vp, sz]
+    L.fhe_hip_multi_eval_bingate_batch.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp]
     L._binfhe_ready = True
     return L
 
@@ -206,6 +211,42 @@ class GateEngine:
         ao = np.zeros_like(a)
         bo = np.zeros_like(b)
         check(L().fhe_hip_modswitch_batch(self._h, q_from, q_to, ln, cnt, ptr(a), ptr(b), ptr(ao), ptr(bo)))
+        return ao, bo
+
+
+class MultiGateEngine:
+    """Single-process multi-GPU gate bootstrapping (fhe_hip_multi): one host thread + stream
+    per device, contiguous shards, keys replicated, no collectives."""
+
+    def __init__(self, paramset, method, devices):
+        self._h = vp()
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        check(L().fhe_hip_multi_create(paramset, method, ptr(devs), len(devs), ctypes.byref(self._h)))
+        self.params = params(paramset, method)
+        self.devices = list(devices)
+
+    def close(self):
+        if self._h:
+            L().fhe_hip_multi_destroy(self._h)
+            self._h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_keys(self, bsk, kskA, kskB):
+        bsk, kskA, kskB = _u64(bsk), _u64(kskA), _u64(kskB)
+        check(L().fhe_hip_multi_load_keys(self._h, ptr(bsk), bsk.size, ptr(kskA), kskA.size, ptr(kskB), kskB.size))
+
+    def eval_gate(self, gate, a1, b1, a2, b2):
+        a1, b1, a2, b2 = _u64(a1), _u64(b1), _u64(a2), _u64(b2)
+        cnt = len(b1)
+        ao = np.zeros((cnt, self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_multi_eval_bingate_batch(self._h, gate, cnt, ptr(a1), ptr(b1), ptr(a2), ptr(b2), ptr(ao),
+                                                   ptr(bo)))
         return ao, bo
 
 

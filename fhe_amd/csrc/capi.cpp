@@ -9,6 +9,7 @@
 
 #include "../../include/fhe_hip.h"
 #include "engine.h"
+#include "multi.h"
 #include "keygen.h"
 #include "ntt.h"
 #include "boot.h"
@@ -55,6 +56,11 @@ static void fill_params(const Params& p, fhe_hip_params* o) {
     o->numAutoKeys = p.numAutoKeys; o->keyDist = p.keyDist; o->Q = p.Q; o->psi = p.psi;
     o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows();
 }
+
+struct fhe_hip_multi {
+    MultiEngine eng;
+    fhe_hip_multi(int ps, int m, const int* d, int n) : eng(ps, m, d, n) {}
+};
 
 struct fhe_hip_ntt_plan {
     NttPlan plan;
@@ -301,6 +307,37 @@ int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, ui
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         (void)hipFree(d);
         if (e != hipSuccess) return hip_fail(e, "modswitch");
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_multi_create(int paramset, int method, const int* devices, int ndev, fhe_hip_multi** out) {
+    if (!out || !devices) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        *out = nullptr;
+        *out = new fhe_hip_multi(paramset, method, devices, ndev);
+        return FHE_HIP_OK;
+    });
+}
+
+void fhe_hip_multi_destroy(fhe_hip_multi* m) {
+    try {
+        delete m;
+    } catch (...) {
+    }
+}
+
+int fhe_hip_multi_load_keys(fhe_hip_multi* m, const uint64_t* bsk, size_t n_words, const uint64_t* A, size_t nA,
+                            const uint64_t* B, size_t nB) {
+    if (!m || !bsk || !A || !B) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int { m->eng.load_keys(bsk, n_words, A, nA, B, nB); return FHE_HIP_OK; });
+}
+
+int fhe_hip_multi_eval_bingate_batch(fhe_hip_multi* m, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
+                                     const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out) {
+    if (!m || !io_ok(count, a1, b1, a2, b2, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        m->eng.eval_gate_host(gate, count, a1, b1, a2, b2, a_out, b_out);
         return FHE_HIP_OK;
     });
 }

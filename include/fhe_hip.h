@@ -123,6 +123,17 @@ int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, c
 int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, uint32_t len, size_t count,
                             const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
 
+/* Single-process multi-device: one host thread + stream per device,
+ * contiguous shards, keys replicated on every device, no collectives.
+ * devices may repeat (several contexts on one GPU). */
+typedef struct fhe_hip_multi fhe_hip_multi;
+int fhe_hip_multi_create(int paramset, int method, const int* devices, int ndev, fhe_hip_multi** out);
+void fhe_hip_multi_destroy(fhe_hip_multi* m);
+int fhe_hip_multi_load_keys(fhe_hip_multi* m, const uint64_t* bsk, size_t n_words, const uint64_t* A, size_t nA,
+                            const uint64_t* B, size_t nB);
+int fhe_hip_multi_eval_bingate_batch(fhe_hip_multi* m, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
+                                     const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out);
+
 /* ------------------------------------------------------------------------ */
 /* Deterministic host key material (KeyGen / BTKeyGen / Encrypt / Decrypt,   */
 /*   binfhecontext.cpp:185-307) -- seeded, same structure as the reference. */

@@ -203,3 +203,23 @@ def test_gpu_binfhecontext_api_truth_tables():
     with pytest.raises(Exception):
         cc.EvalBinGate(bf.AND, ct, ct)
     assert cc.EvalBinGateBatch(bf.AND, [], []) == []
+
+
+@pytest.mark.gpu
+def test_gpu_multi_engine_shards_match_single():
+    """single-process multi-device engine (here two contexts on device 0, so the
+    thread/shard/reassembly logic runs on a one-GPU box) == single-context output."""
+    from fhe_amd import binfhe as bf
+    g, keys, _ = fixture("std128")
+    ps, m = int(g["paramset"]), int(g["method"])
+    me = bf.MultiGateEngine(ps, m, [0, 0, 0])
+    me.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    rng = np.random.default_rng(21)
+    count = 301                                   # uneven shards
+    x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+    a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 41)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 42)
+    ao, bo = me.eval_gate(5, a1, b1, a2, b2)
+    sa, sb = engine("std128").eval_gate(5, a1, b1, a2, b2)
+    assert np.array_equal(ao, sa) and np.array_equal(bo, sb)
+    assert np.array_equal(bf.decrypt(ps, m, keys.sk, ao, bo), TRUTH[5](x1, x2).astype(np.int64))
