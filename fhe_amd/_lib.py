@@ -3,7 +3,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, "libfhe_amd.so")
+# FHE_AMD_LIB: an alternative in-tree build of the same library (A/B experiments only)
+lib_path = os.environ.get("FHE_AMD_LIB") or os.path.join(_HERE, "libfhe_amd.so")
 
 vp = ctypes.c_void_p
 u64 = ctypes.c_uint64

@@ -25,9 +25,27 @@
 #include "arith.h"
 #include "boot.h"
 
+#ifndef FHE_BF_GROUP
+#define FHE_BF_GROUP 0   // >0: sched_barrier after every FHE_BF_GROUP butterflies (bounds live temps)
+#endif
+#ifndef FHE_KEY_PF
+#define FHE_KEY_PF 1     // key chunks (2 slots each) requested ahead of use in the CMUX loop
+#endif
+#ifndef FHE_WAVES_PER_EU
+#define FHE_WAVES_PER_EU 2
+#endif
+
 namespace fhe_amd {
 
 namespace {
+
+FHE_DEV void bf_fence(int idx) {
+#if FHE_BF_GROUP > 0
+    if ((idx + 1) % FHE_BF_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+#else
+    (void)idx;
+#endif
+}
 
 constexpr int kTile = 32 * 33;  // one half-wave transpose tile (u32 words)
 
@@ -91,6 +109,7 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             if (r & (1 << rb)) continue;
             const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
             ct_bf(v[r], v[r | (1 << rb)], w, m);
+            bf_fence(r);
         }
     }
     transpose32(v, tile, l);
@@ -101,6 +120,7 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             if (r & (1 << b)) continue;
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
             ct_bf(v[r], v[r | (1 << b)], w, m);
+            bf_fence(r);
         }
     }
 }
@@ -115,6 +135,7 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             if (r & (1 << b)) continue;
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
             gs_bf(v[r], v[r | (1 << b)], w, m);
+            bf_fence(r);
         }
     }
     transpose32(v, tile, l);
@@ -126,6 +147,7 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             if (r & (1 << rb)) continue;
             const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
             gs_bf(v[r], v[r | (1 << rb)], w, m);
+            bf_fence(r);
         }
     }
     // bit 9 with N^-1 folded in (transformnat-impl.h:599-623)
@@ -177,7 +199,7 @@ __global__ void k_prep_ginx(const uint64_t* __restrict__ a1, const uint64_t* __r
 constexpr int kWaves = 4;
 constexpr size_t kBootLds = (size_t)(992 * 2 + 2048 + kWaves * 2 * kTile) * 4;
 
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
                         const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -223,7 +245,10 @@ __global__ void __launch_bounds__(256, 2)
     const int32_t sh     = 32 - (int32_t)g.gbits;
     const int32_t Qs     = (int32_t)m.Q;
     const uint32_t Qh    = m.Q >> 1;
+    const uint2* ki      = bsk + lane;
+    const uint2* kinext  = ki + 2 * 4 * 16 * 64;
     for (uint32_t i = 0; i < g.n; ++i) {
+        uint2 kbuf[FHE_KEY_PF + 1][8];
         const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
         uint32_t dA[32], dB[32];
         // --- iNTT of a copy of acc -> canonical COEF (AddToAccCGGI :104-106)
@@ -249,18 +274,37 @@ __global__ void __launch_bounds__(256, 2)
         // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
         //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
         //     out so that each load instruction reads 1 KiB contiguous.
-        const uint2* ki   = bsk + (size_t)i * (2 * 4 * 16 * 64) + lane;
         const uint32_t ab = (a * lbase) & 2047;
+#if FHE_KEY_PF > 0
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            // one 2-slot step of keys live at a time (register budget)
-            asm volatile("" ::: "memory");
-            uint2 kp[4], kn[4];
+        for (int k = 0; k < FHE_KEY_PF; ++k)
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-                kp[d] = ki[((0 * 4 + d) * 16 + k) * 64];
-                kn[d] = ki[((1 * 4 + d) * 16 + k) * 64];
+                kbuf[k][d]     = ki[((0 * 4 + d) * 16 + k) * 64];
+                kbuf[k][4 + d] = ki[((1 * 4 + d) * 16 + k) * 64];
             }
+#endif
+#pragma clang loop unroll(full)
+        for (int k = 0; k < 16; ++k) {
+            // software pipeline: chunk k+PF is requested while chunk k is consumed
+#if FHE_KEY_PF > 0
+            if (k + FHE_KEY_PF < 16) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d]     = ki[((0 * 4 + d) * 16 + k + FHE_KEY_PF) * 64];
+                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][4 + d] = ki[((1 * 4 + d) * 16 + k + FHE_KEY_PF) * 64];
+                }
+            }
+#else
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                kbuf[0][d]     = ki[((0 * 4 + d) * 16 + k) * 64];
+                kbuf[0][4 + d] = ki[((1 * 4 + d) * 16 + k) * 64];
+            }
+#endif
+            asm volatile("" ::: "memory");
+#define KP(d) kbuf[k % (FHE_KEY_PF + 1)][d]
+#define KN(d) kbuf[k % (FHE_KEY_PF + 1)][4 + (d)]
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * k + e;
@@ -268,10 +312,10 @@ __global__ void __launch_bounds__(256, 2)
                 auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                 auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
                 const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
-                uint64_t S1 = (uint64_t)D0 * (e ? kp[0].y : kp[0].x) + (uint64_t)D1 * (e ? kp[1].y : kp[1].x) +
-                              (uint64_t)D2 * (e ? kp[2].y : kp[2].x) + (uint64_t)D3 * (e ? kp[3].y : kp[3].x);
-                uint64_t S2 = (uint64_t)D0 * (e ? kn[0].y : kn[0].x) + (uint64_t)D1 * (e ? kn[1].y : kn[1].x) +
-                              (uint64_t)D2 * (e ? kn[2].y : kn[2].x) + (uint64_t)D3 * (e ? kn[3].y : kn[3].x);
+                uint64_t S1 = (uint64_t)D0 * (e ? KP(0).y : KP(0).x) + (uint64_t)D1 * (e ? KP(1).y : KP(1).x) +
+                              (uint64_t)D2 * (e ? KP(2).y : KP(2).x) + (uint64_t)D3 * (e ? KP(3).y : KP(3).x);
+                uint64_t S2 = (uint64_t)D0 * (e ? KN(0).y : KN(0).x) + (uint64_t)D1 * (e ? KN(1).y : KN(1).x) +
+                              (uint64_t)D2 * (e ? KN(2).y : KN(2).x) + (uint64_t)D3 * (e ? KN(3).y : KN(3).x);
                 const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
                 const uint32_t e1 = (ab + ((a * (uint32_t)(__builtin_bitreverse32(r) >> 27)) << 6)) & 2047;
@@ -279,7 +323,11 @@ __global__ void __launch_bounds__(256, 2)
                 const uint64_t S  = (uint64_t)t1 * s_mono[e1] + (uint64_t)t2 * s_mono[e2];
                 acc[r]            = add_mod(acc[r], csub(mont_red(S, m), m.Q), m.Q);
             }
+#undef KP
+#undef KN
         }
+        ki = kinext;
+        kinext += 2 * 4 * 16 * 64;
     }
 
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
@@ -426,7 +474,7 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
 }
 }  // namespace
 
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
                        const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
@@ -494,19 +542,25 @@ __global__ void __launch_bounds__(256, 2)
             fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
             fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
             const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
+            uint2 kk[2][4];
 #pragma unroll
+            for (int d = 0; d < 4; ++d) kk[0][d] = ki[(d * 16 + 0) * 64];
+#pragma clang loop unroll(full)
             for (int k = 0; k < 16; ++k) {
-                asm volatile("" ::: "memory");
-                uint2 kk[4];
+                if (k + 1 < 16) {  // request chunk k+1 while chunk k is consumed
 #pragma unroll
-                for (int d = 0; d < 4; ++d) kk[d] = ki[(d * 16 + k) * 64];
+                    for (int d = 0; d < 4; ++d) kk[(k + 1) & 1][d] = ki[(d * 16 + k + 1) * 64];
+                }
+                asm volatile("" ::: "memory");
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int r = 2 * k + e;
                     auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                     auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
-                    uint64_t S = (uint64_t)p01[0] * (e ? kk[0].y : kk[0].x) + (uint64_t)p01[1] * (e ? kk[1].y : kk[1].x) +
-                                 (uint64_t)p23[0] * (e ? kk[2].y : kk[2].x) + (uint64_t)p23[1] * (e ? kk[3].y : kk[3].x);
+                    uint64_t S = (uint64_t)p01[0] * (e ? kk[k & 1][0].y : kk[k & 1][0].x) +
+                                 (uint64_t)p01[1] * (e ? kk[k & 1][1].y : kk[k & 1][1].x) +
+                                 (uint64_t)p23[0] * (e ? kk[k & 1][2].y : kk[k & 1][2].x) +
+                                 (uint64_t)p23[1] * (e ? kk[k & 1][3].y : kk[k & 1][3].x);
                     acc[r] = csub(mont_red(S, m), m.Q);
                 }
             }
@@ -538,10 +592,17 @@ __global__ void __launch_bounds__(256, 2)
             }
             fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
             const uint2* ki = autok + (size_t)t * (2 * 16 * 64) + lane;
-#pragma unroll
+            uint2 ka[2][2];
+            ka[0][0] = ki[(0 * 16 + 0) * 64];
+            ka[0][1] = ki[(1 * 16 + 0) * 64];
+#pragma clang loop unroll(full)
             for (int k = 0; k < 16; ++k) {
+                if (k + 1 < 16) {
+                    ka[(k + 1) & 1][0] = ki[(0 * 16 + k + 1) * 64];
+                    ka[(k + 1) & 1][1] = ki[(1 * 16 + k + 1) * 64];
+                }
                 asm volatile("" ::: "memory");
-                const uint2 k0 = ki[(0 * 16 + k) * 64], k1 = ki[(1 * 16 + k) * 64];
+                const uint2 k0 = ka[k & 1][0], k1 = ka[k & 1][1];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int r = 2 * k + e;
