@@ -197,7 +197,8 @@ __global__ void k_prep_ginx(const uint64_t* __restrict__ a1, const uint64_t* __r
 // fused blind rotation, 4 gates (waves) per 256-thread workgroup
 // ---------------------------------------------------------------------------
 constexpr int kWaves = 4;
-constexpr size_t kBootLds = (size_t)(992 * 2 + 2048 + kWaves * 2 * kTile) * 4;
+constexpr int kMonoWords = 2176;  // 2N+1 entries padded by one word per 32, rounded to 16 B
+constexpr size_t kBootLds = (size_t)(992 * 2 + kMonoWords + kWaves * 2 * kTile) * 4;
 
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
@@ -206,12 +207,12 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     uint32_t* s_twBf = sm;
     uint32_t* s_twBi = sm + 992;
     uint32_t* s_mono = sm + 1984;
-    uint32_t* s_tile = sm + 4032;
+    uint32_t* s_tile = sm + 1984 + kMonoWords;
     for (int i = threadIdx.x; i < 992; i += 256) {
         s_twBf[i] = T.twB_fwd[i];
         s_twBi[i] = T.twB_inv[i];
     }
-    for (int i = threadIdx.x; i < 2048; i += 256) s_mono[i] = T.mono[i];
+    for (int i = threadIdx.x; i < kMonoWords; i += 256) s_mono[i] = T.mono[i];
     __syncthreads();
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
@@ -274,7 +275,14 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
         //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
         //     out so that each load instruction reads 1 KiB contiguous.
-        const uint32_t ab = (a * lbase) & 2047;
+        // monomial addressing: a = 2a' (factor 2N/q = 2), slot exponent e = a (2 brv(x) + 1) mod 2N
+        // = 2 f with f = a'(2 brv5(l) + 1) + 64 ((a' brv5(r)) mod 16): lane part fl + uniform part.
+        // s_mono holds M[2f mod 2N] at f + (f >> 5) for f in [0, 2N] (padded: few bank conflicts).
+        const uint32_t ah = a >> 1;
+        const uint32_t fl = (ah * lbase) & 1023;
+        const uint32_t Pp = fl + (fl >> 5);                    // f1 = fl + 64u  -> pos = Pp + 66u
+        const uint32_t gl = 2048 - fl;
+        const uint32_t Pn = gl + (gl >> 5);                    // f2 = gl - 64u  -> pos = Pn - 66u
 #if FHE_KEY_PF > 0
 #pragma unroll
         for (int k = 0; k < FHE_KEY_PF; ++k)
@@ -318,9 +326,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                               (uint64_t)D2 * (e ? KN(2).y : KN(2).x) + (uint64_t)D3 * (e ? KN(3).y : KN(3).x);
                 const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
-                const uint32_t e1 = (ab + ((a * (uint32_t)(__builtin_bitreverse32(r) >> 27)) << 6)) & 2047;
-                const uint32_t e2 = (2048 - e1) & 2047;
-                const uint64_t S  = (uint64_t)t1 * s_mono[e1] + (uint64_t)t2 * s_mono[e2];
+                const uint32_t u  = __builtin_amdgcn_readfirstlane((ah * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & 15) * 66;
+                const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
                 acc[r]            = add_mod(acc[r], csub(mont_red(S, m), m.Q), m.Q);
             }
 #undef KP

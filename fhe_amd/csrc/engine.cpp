@@ -22,6 +22,8 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
     if (p_.q & (p_.q - 1)) throw std::invalid_argument("device path needs a power-of-two q");
     if (p_.digitsG != 3) throw std::invalid_argument("device path expects digitsG = 3");
+    if (p_.method == M_GINX && ((2 * p_.N / p_.q) & 1))
+        throw std::invalid_argument("GINX device path needs an even 2N/q (monomial table)");
     FHE_HIP_CHECK(hipSetDevice(device_));
     FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     build_tables();
@@ -42,7 +44,7 @@ void Engine::build_tables() {
     const uint64_t Q = p_.Q;
     HostNtt h;
     h.init(p_.N, Q, p_.psi);
-    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2048);
+    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2176, 0);
     uint32_t* twAf = t.data();
     uint32_t* twAi = twAf + 32;
     uint32_t* twBf = twAi + 32;
@@ -62,11 +64,16 @@ void Engine::build_tables() {
                 twBi[off + k * 32 + l] = to_mont(h.tabI[idx], Q);
             }
     }
-    // EVAL(X^m - 1) at slot j = omega_j^m - 1 with omega_j = psi^(2 brv(j) + 1): table over psi^e - 1
-    uint64_t x = 1;
-    for (uint32_t e = 0; e < 2 * p_.N; ++e) {
-        mono[e] = to_mont(submod(x, 1, Q), Q);
-        x = mulmod(x, p_.psi, Q);
+    // EVAL(X^m - 1) at slot j = omega_j^m - 1 with omega_j = psi^(2 brv(j) + 1).  GINX exponents
+    // are even (m = a_i * 2N/q), so the table holds psi^(2f) - 1 for f in [0, 2N], entry f at
+    // f + (f >> 5) (bootstrap.hip, monomial addressing).
+    {
+        const uint64_t psi2 = mulmod(p_.psi, p_.psi, Q);
+        uint64_t x = 1;
+        for (uint32_t f = 0; f <= 2 * p_.N; ++f) {
+            mono[f + (f >> 5)] = to_mont(submod(x, 1, Q), Q);
+            x = mulmod(x, psi2, Q);
+        }
     }
     if (p_.method == M_LMKCDEY) {  // rgsw-cryptoparameters.cpp:115-127
         const uint32_t M = 2 * p_.N;
@@ -88,7 +95,7 @@ void Engine::build_tables() {
     tabs_.twA_inv = d + 32;
     tabs_.twB_fwd = d + 64;
     tabs_.twB_inv = d + 64 + 992;
-    tabs_.mono = d + 64 + 1984;
+    tabs_.mono = d + 64 + 1984;  // 2176 words
     tabs_.Q = (uint32_t)Q;
     tabs_.Q2 = (uint32_t)(2 * Q);
     tabs_.qinv = neg_inv32((uint32_t)Q);
