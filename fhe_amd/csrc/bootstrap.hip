@@ -31,6 +31,9 @@
 #ifndef FHE_KEY_PF
 #define FHE_KEY_PF 1     // key chunks (2 slots each) requested ahead of use in the CMUX loop
 #endif
+#ifndef FHE_FWD_SHARED
+#define FHE_FWD_SHARED 0
+#endif
 #ifndef FHE_WAVES_PER_EU
 #define FHE_WAVES_PER_EU 2
 #endif
@@ -63,12 +66,13 @@ FHE_DEV uint32_t mont_red(uint64_t t, const Mod& m) {  // t < 16 Q^2 -> result <
     uint32_t mm = (uint32_t)t * m.qinv;
     return (uint32_t)((t + (uint64_t)mm * m.Q) >> 32);
 }
-// Cooley-Tukey (forward), Harvey-style lazy: x, y < 4Q in, < 4Q out
+// Cooley-Tukey (forward), lazy: t = y w < 2Q for any y < 2^32, so x, y < B in gives
+// x + t, x + 2Q - t < B + 2Q out (no reduction; fwd_pass bounds the growth)
 FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
-    uint32_t xx = csub(x, m.Q2);
-    uint32_t t  = mont_mul(y, wR, m);
-    x           = xx + t;
-    y           = xx + m.Q2 - t;
+    uint32_t t = mont_mul(y, wR, m);
+    uint32_t s = x + m.Q2;
+    y          = s - t;
+    x          = x + t;
 }
 // Gentleman-Sande (inverse): x, y < 2Q in, < 2Q out
 FHE_DEV void gs_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
@@ -80,13 +84,28 @@ FHE_DEV void gs_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 
 // intra-wave LDS hand-off: orders the compiler's LDS accesses; the LDS
 // executes one wave's DS instructions in issue order.
+#ifndef FHE_LDS_SYNC
+#define FHE_LDS_SYNC 0
+#endif
 FHE_DEV void wave_lds_sync() {
+#if FHE_LDS_SYNC == 0
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
+    // one wave's DS instructions are executed by the LDS in issue order, so a
+    // read issued after a write (or a write after a read) of the same tile by
+    // the same wave is ordered without waiting for completion; only the
+    // compiler must not move LDS accesses across this point.
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#endif
 }
 
 FHE_DEV void transpose32(uint32_t (&v)[32], uint32_t* tile, int l) {
+#if defined(FHE_ABL) && (FHE_ABL & 4)
+    return;  // ablation: no transposes
+#endif
 #pragma unroll
     for (int r = 0; r < 32; ++r) tile[l * 33 + r] = v[r];
     wave_lds_sync();
@@ -98,7 +117,8 @@ FHE_DEV void transpose32(uint32_t (&v)[32], uint32_t* tile, int l) {
 // offset of stage b's lane-major twiddle block: 32 * (2^(4-b) - 1)
 constexpr int twb_off(int b) { return 32 * ((1 << (4 - b)) - 1); }
 
-// forward NTT: A' (COEF) -> B' (EVAL), outputs < 4Q
+// forward NTT: A' (COEF, inputs < Q) -> B' (EVAL), outputs < 14Q (< 2^32 for Q < 2^28):
+// 5 stages (< 11Q), reduce to < 4Q at the transpose, 5 stages (< 14Q)
 FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
                       const uint32_t* s_twB, const Mod& m) {
 #pragma unroll
@@ -112,13 +132,19 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             bf_fence(r);
         }
     }
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = csub(csub(v[r], 4 * m.Q2), m.Q2);  // < 11Q -> < 4Q
     transpose32(v, tile, l);
 #pragma unroll
     for (int b = 4; b >= 0; --b) {
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << b)) continue;
+#if defined(FHE_ABL) && (FHE_ABL & 8)
+            const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;  // ablation: no per-lane twiddle reads
+#else
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+#endif
             ct_bf(v[r], v[r | (1 << b)], w, m);
             bf_fence(r);
         }
@@ -133,7 +159,11 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << b)) continue;
+#if defined(FHE_ABL) && (FHE_ABL & 8)
+            const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;
+#else
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+#endif
             gs_bf(v[r], v[r | (1 << b)], w, m);
             bf_fence(r);
         }
@@ -238,7 +268,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         }
         fwd_pass(acc, tile, l, T.twA_fwd, s_twBf, m);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(acc[r], m.Q2), m.Q);
+        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), m.Q);
     }
 
     const uint16_t* gidx = idx + (size_t)gate * g.n;
@@ -270,8 +300,23 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
         }
         // --- NTT of the four digit polynomials (two per pass, one per half)
+#if FHE_FWD_SHARED
+        // one copy of the forward-pass code for both digit polynomials (instruction-cache
+        // footprint): transform dA, swap, transform (old dB), swap back
+#pragma clang loop unroll(disable)
+        for (int pass = 0; pass < 2; ++pass) {
+            fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const uint32_t t = dA[r];
+                dA[r]            = dB[r];
+                dB[r]            = t;
+            }
+        }
+#else
         fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
         fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
+#endif
         // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
         //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
         //     out so that each load instruction reads 1 KiB contiguous.
@@ -299,8 +344,13 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             if (k + FHE_KEY_PF < 16) {
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
+#if defined(FHE_ABL) && (FHE_ABL & 1)
+                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d]     = make_uint2(d * 7 + k + i, lane);  // ablation: no key loads
+                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][4 + d] = make_uint2(d * 5 + k, lane + i);
+#else
                     kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d]     = ki[((0 * 4 + d) * 16 + k + FHE_KEY_PF) * 64];
                     kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][4 + d] = ki[((1 * 4 + d) * 16 + k + FHE_KEY_PF) * 64];
+#endif
                 }
             }
 #else
@@ -327,8 +377,13 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                 const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
                 const uint32_t u  = __builtin_amdgcn_readfirstlane((ah * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & 15) * 66;
+#if defined(FHE_ABL) && (FHE_ABL & 2)
+                const uint64_t S  = (uint64_t)t1 * (Pp + u) + (uint64_t)t2 * (Pn - u);  // ablation: no monomial reads
+#else
                 const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
-                acc[r]            = add_mod(acc[r], csub(mont_red(S, m), m.Q), m.Q);
+#endif
+                // t1, t2 < 4.5Q (digits < 14Q) -> S < 9Q^2 -> mont_red < 1.6Q; acc kept in [0, 2Q)
+                acc[r]            = csub(acc[r] + mont_red(S, m), m.Q2);
             }
 #undef KP
 #undef KN
@@ -517,7 +572,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         }
         fwd_pass(acc, tile, l, T.twA_fwd, s_twBf, m);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(acc[r], m.Q2), m.Q);
+        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), m.Q);
         // acc1 <- acc1(X^(2N-5))   (:99); applied to both halves, acc0 = 0 is invariant
         automorphism_eval(acc, tile, l, M - 5);
     }
@@ -568,7 +623,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                                  (uint64_t)p01[1] * (e ? kk[k & 1][1].y : kk[k & 1][1].x) +
                                  (uint64_t)p23[0] * (e ? kk[k & 1][2].y : kk[k & 1][2].x) +
                                  (uint64_t)p23[1] * (e ? kk[k & 1][3].y : kk[k & 1][3].x);
-                    acc[r] = csub(mont_red(S, m), m.Q);
+                    acc[r] = csub(csub(mont_red(S, m), 2 * m.Q2), m.Q2);  // < 4.5Q -> [0, 2Q)
                 }
             }
         } else {
@@ -615,8 +670,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                     const int r = 2 * k + e;
                     auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                     uint64_t S = (uint64_t)p[0] * (e ? k0.y : k0.x) + (uint64_t)p[1] * (e ? k1.y : k1.x);
-                    const uint32_t v = csub(mont_red(S, m), m.Q);
-                    acc[r] = h ? add_mod(acc[r], v, m.Q) : v;
+                    const uint32_t v = csub(mont_red(S, m), m.Q2);     // < 2.75Q -> < 2Q
+                    acc[r] = h ? csub(acc[r] + v, m.Q2) : v;           // [0, 2Q)
                 }
             }
         }
