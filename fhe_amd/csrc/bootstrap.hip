@@ -31,6 +31,9 @@
 #ifndef FHE_KEY_PF
 #define FHE_KEY_PF 1     // key chunks (2 slots each) requested ahead of use in the CMUX loop
 #endif
+#ifndef FHE_FWD_FUSED
+#define FHE_FWD_FUSED 1
+#endif
 #ifndef FHE_FWD_SHARED
 #define FHE_FWD_SHARED 0
 #endif
@@ -147,6 +150,44 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 #endif
             ct_bf(v[r], v[r | (1 << b)], w, m);
             bf_fence(r);
+        }
+    }
+}
+
+// two forward NTTs at once (the digit polynomials D_h and D_{2+h}): each twiddle
+// load feeds two butterflies and every stage has 32 independent butterflies
+FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int l,
+                       const uint32_t* __restrict__ twA, const uint32_t* s_twB, const Mod& m) {
+#pragma unroll
+    for (int b = 9; b >= 5; --b) {
+        const int rb = b - 5;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
+            ct_bf(v[r], v[r | (1 << rb)], w, m);
+            ct_bf(u[r], u[r | (1 << rb)], w, m);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        v[r] = csub(csub(v[r], 4 * m.Q2), m.Q2);
+        u[r] = csub(csub(u[r], 4 * m.Q2), m.Q2);
+    }
+    transpose32(v, tile, l);
+    transpose32(u, tile, l);
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << b)) continue;
+#if defined(FHE_ABL) && (FHE_ABL & 8)
+            const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;
+#else
+            const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+#endif
+            ct_bf(v[r], v[r | (1 << b)], w, m);
+            ct_bf(u[r], u[r | (1 << b)], w, m);
         }
     }
 }
@@ -300,7 +341,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
         }
         // --- NTT of the four digit polynomials (two per pass, one per half)
-#if FHE_FWD_SHARED
+#if FHE_FWD_FUSED
+        fwd_pass2(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+#elif FHE_FWD_SHARED
         // one copy of the forward-pass code for both digit polynomials (instruction-cache
         // footprint): transform dA, swap, transform (old dB), swap back
 #pragma clang loop unroll(disable)
@@ -601,8 +644,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                 dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
                 dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
             }
-            fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
-            fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
+            fwd_pass2(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
             const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
             uint2 kk[2][4];
 #pragma unroll
