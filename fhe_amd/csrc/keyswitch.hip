@@ -50,15 +50,143 @@ __global__ void __launch_bounds__(256)
     else if (c1 == g.n) b_out[gate] = v1;
 }
 
+// ---------------------------------------------------------------------------
+// Gate-tiled key switch: a workgroup handles G gates x 64 columns.  For each
+// (i, j) the 32 candidate row slices KSK[i][0..31][j][cols] (32 x 128 B) are
+// staged in LDS once and every gate (one thread) subtracts the slice its digit
+// selects.  KSK gather traffic drops from 3 MB per gate to 12.6 MB per 256
+// gates; accumulation is packed u16 (v_pk_sub_u16: mod 2^16, hence exact mod
+// qKS = 2^14) with two columns per VGPR.  The kernel is bound by the LDS reads
+// (128 B per gate per step); prefetch depth beyond 2 steps measured no gain.
+// Below 4096 gates the per-gate kernel above fills the chip better.
+// ---------------------------------------------------------------------------
+// two independent u16 subtractions (mod 2^16) in one VALU op
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+constexpr int kKsCols  = 64;         // columns per workgroup (32 packed u32)
+constexpr int kKsRowB  = 144;        // LDS bytes per staged slice (128 + 16 pad: conflict-light b128 reads)
+#ifndef FHE_KS_STEPS
+#define FHE_KS_STEPS 2
+#endif
+constexpr int kKsStep  = FHE_KS_STEPS;  // (i, j) steps per LDS buffer / barrier (= prefetch depth)
+constexpr int kKsParts = 32 * kKsCols * 2 / 16;  // uint4 parts staged per step (32 slices x 128 B)
+
+// G gates (threads) per workgroup; each thread stages kKsParts / G parts per step
+template <int G>
+__global__ void __launch_bounds__(G)
+    k_keyswitch_tiled(GateArgs g, uint32_t logBase, uint32_t digitsKS, const uint16_t* __restrict__ ksk,
+                      const uint32_t* __restrict__ ms_a, const uint32_t* __restrict__ ms_b, uint32_t q_out,
+                      uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
+    constexpr int P = kKsParts / G;
+    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][32 * kKsRowB];
+    const uint32_t t = threadIdx.x;
+    const uint32_t gate = blockIdx.x * G + t;
+    const bool valid = gate < g.count;
+    const uint32_t col0 = blockIdx.y * kKsCols;
+    const uint32_t base = 1u << logBase, mask = base - 1;
+    const uint32_t steps = g.N * digitsKS;                 // (i, j) pairs, i-major
+    const uint32_t* ga = ms_a + (size_t)(valid ? gate : 0) * g.N;
+
+    // staging role: part index x = t + G*r -> slice x / 8, 16-byte part x % 8
+    auto slice_src = [&](uint32_t step, int r) -> const uint4* {
+        const uint32_t x = t + G * r, sd = x >> 3, sp = x & 7;
+        const uint32_t i = step / digitsKS, j = step - i * digitsKS;
+        const size_t row = ((size_t)i * base + sd) * digitsKS + j;
+        return reinterpret_cast<const uint4*>(ksk + row * 512 + col0) + sp;
+    };
+    auto slice_dst = [&](unsigned char* sb, int r) -> uint4* {
+        const uint32_t x = t + G * r;
+        return reinterpret_cast<uint4*>(sb + (x >> 3) * kKsRowB + (x & 7) * 16);
+    };
+
+    uint32_t acc[kKsCols / 2];
+#pragma unroll
+    for (int k = 0; k < kKsCols / 2; ++k) acc[k] = 0;
+
+    uint4 st[kKsStep][P];
+#pragma unroll
+    for (int q = 0; q < kKsStep; ++q)
+#pragma unroll
+        for (int r = 0; r < P; ++r) st[q][r] = *slice_src(q, r);
+    uint32_t aval = valid ? ga[0] : 0;
+
+    auto consume = [&](const unsigned char* sb, uint32_t step) {
+        const uint32_t i = step / digitsKS, j = step - i * digitsKS;
+        if (j == 0 && valid) aval = ga[i];
+        const uint32_t dig = (aval >> (logBase * j)) & mask;
+        const uint4* src = reinterpret_cast<const uint4*>(sb + dig * kKsRowB);
+#pragma unroll
+        for (int k = 0; k < kKsCols / 8; ++k) {
+            const uint4 w = src[k];
+            acc[4 * k + 0] = pk_sub_u16(acc[4 * k + 0], w.x);
+            acc[4 * k + 1] = pk_sub_u16(acc[4 * k + 1], w.y);
+            acc[4 * k + 2] = pk_sub_u16(acc[4 * k + 2], w.z);
+            acc[4 * k + 3] = pk_sub_u16(acc[4 * k + 3], w.w);
+        }
+    };
+
+    // one barrier per round: buffer buf is rewritten two rounds later, after every thread
+    // has passed the next round's barrier (and so finished consuming it)
+    for (uint32_t s0 = 0, buf = 0; s0 < steps; s0 += kKsStep, buf ^= 1) {
+#pragma unroll
+        for (int q = 0; q < kKsStep; ++q)
+#pragma unroll
+            for (int r = 0; r < P; ++r) *slice_dst(s_buf[buf][q], r) = st[q][r];
+        __syncthreads();
+        if (s0 + kKsStep < steps) {
+#pragma unroll
+            for (int q = 0; q < kKsStep; ++q)
+#pragma unroll
+                for (int r = 0; r < P; ++r) st[q][r] = *slice_src(s0 + kKsStep + q, r);
+        }
+#pragma unroll
+        for (int q = 0; q < kKsStep; ++q) consume(s_buf[buf][q], s0 + q);
+    }
+    if (!valid) return;
+    const uint32_t qm = g.qKS - 1;
+    const uint32_t b = ms_b[gate];
+    uint64_t* oa = a_out + (size_t)gate * g.n;
+#pragma unroll
+    for (int k = 0; k < kKsCols / 2; ++k) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t c = col0 + 2 * k + h;
+            const uint32_t neg = h ? (acc[k] >> 16) : (acc[k] & 0xffffu);  // -sum mod 2^16
+            uint32_t v = ((c == g.n ? b : 0u) + neg) & qm;
+            if (q_out) v = ((2 * v * q_out + g.qKS) / (2 * g.qKS)) % q_out;  // ModSwitch qKS -> q
+            if (c < g.n) oa[c] = v;
+            else if (c == g.n) b_out[gate] = v;
+        }
+    }
+}
+
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
                             const uint32_t* ms_a, const uint32_t* ms_b, uint32_t q_out, uint64_t* a_out,
                             uint64_t* b_out, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (baseKS & (baseKS - 1)) return hipErrorInvalidValue;
     if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 512 || g.N > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(256), 0, s, g, (uint32_t)__builtin_ctz(baseKS), digitsKS,
-                       reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
-    return hipGetLastError();
+    const uint32_t logBase = (uint32_t)__builtin_ctz(baseKS);
+#ifndef FHE_KS_TILE
+#define FHE_KS_TILE 0   // 0: choose by batch size; 1: per-gate kernel; 256: gate tile
+#endif
+    int tile = FHE_KS_TILE;
+    if (tile == 0) tile = g.count >= 4096 ? 256 : 1;  // tiles need >= 16 x 8 workgroups to pay
+    if (tile > 1 && (baseKS != 32 || (g.N * digitsKS) % kKsStep)) tile = 1;
+    const uint32_t ytiles = 512 / kKsCols;
+    switch (tile) {
+        case 256:
+            hipLaunchKernelGGL(k_keyswitch_tiled<256>, dim3((g.count + 255) / 256, ytiles), dim3(256), 0, s, g,
+                               logBase, digitsKS, ksk, ms_a, ms_b, q_out, a_out, b_out);
+            break;
+        default:
+            hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(256), 0, s, g, logBase, digitsKS,
+                               reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
+    }    return hipGetLastError();
 }
 
 }  // namespace fhe_amd

@@ -167,6 +167,25 @@ def test_gpu_ragged_batches_vs_oracle(name, restatement):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", SETS)
+def test_gpu_keyswitch_kernels_vs_oracle(name, restatement):
+    """both key-switch kernels (per-gate below 4096 ciphertexts, gate-tiled at and above,
+    keyswitch.hip) on uniform inputs mod qKS, incl. a ragged last tile, vs the oracle."""
+    from oracle_lib import Restatement
+    g, keys, _ = fixture(name)
+    O = Restatement(int(g["paramset"]), int(g["method"]))
+    e = engine(name)
+    P = e.params
+    rng = np.random.default_rng(77)
+    for count in (300, 4096 + 259):
+        a = rng.integers(0, P.qKS, (count, P.N), dtype=np.uint64)
+        b = rng.integers(0, P.qKS, count, dtype=np.uint64)
+        ga, gb = e.keyswitch(a, b)
+        oa, ob = O.keyswitch(keys.kskA, keys.kskB, a, b)
+        assert np.array_equal(ga, oa) and np.array_equal(gb, ob), count
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
 def test_gpu_large_batch_truth_and_determinism(name):
     """size-independent properties at a bench-sized batch: every gate decrypts to its
     truth value, and two runs are bit-identical."""
