@@ -8,13 +8,14 @@ namespace fhe_amd {
 struct NttPlan {
     uint64_t Q = 0, psi = 0;
     uint32_t N = 0;
-    bool wide = false;  // Q >= 2^31: 64-bit arithmetic path
+    bool wide = false;  // Q >= 2^30: 64-bit arithmetic path (the 32-bit path keeps values < 4Q)
     // device tables: Table[i] / TableI[i] (reference order, transformnat-impl.h:777-831)
     // paired with Shoup precon; uint2 (32-bit path) or ulonglong2 (64-bit path)
     void* d_tab_fwd = nullptr;
     void* d_tab_inv = nullptr;
     uint64_t ninv = 0, ninv_pre = 0, w1ninv = 0, w1ninv_pre = 0;
     int device = 0;
+    int cus = 256;      // compute units of the device (grid sizing)
 };
 
 // Builds tables on the host and uploads them; psi == 0 selects the reference's

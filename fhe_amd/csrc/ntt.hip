@@ -9,7 +9,7 @@
 // forward output j (bit-reversed order) is a(psi^(2*brv(j)+1)); inverse is its exact inverse.
 //
 // Work decomposition (one polynomial per half-wave of 32 lanes, 32 coefficients
-// per lane, PPB polynomials per workgroup):
+// per lane, 4 waves = 8 polynomials per workgroup iteration, persistent grid):
 //   index x = (h << 6) | (l << 1) | b0           ("layout A": lane l = x bits 5..1,
 //                                                  register r = (h << 1) | b0)
 //   "layout B" swaps register and lane:   lane = (h << 1) | b0, register = x bits 5..1.
@@ -29,36 +29,71 @@ namespace fhe_amd {
 template <typename T>
 struct ModT;
 
+#ifndef FHE_NTT_COPY
+#define FHE_NTT_COPY 0      // experiment: skip the arithmetic (memory-only timing)
+#endif
+#ifndef FHE_NTT_WAVESYNC
+#define FHE_NTT_WAVESYNC 1  // transposes synchronise the wave only (tiles are half-wave private)
+#endif
+
+// 32-bit path (Q < 2^30): Harvey-style lazy butterflies.  Forward values live in
+// [0, 4Q), inverse values in [0, 2Q); one correction at the end gives [0, Q).
+// Shoup's lazy product x*w - floor(x*w'/2^32)*Q is in [0, 2Q) for any x < 2^32.
 template <>
 struct ModT<uint32_t> {
     using TW = uint2;  // (w, w' = floor(w 2^32 / Q))
-    uint32_t Q;
-    FHE_DEV uint32_t mul(uint32_t x, TW w) const { return mul_shoup(x, w.x, w.y, Q); }
-    FHE_DEV uint32_t add(uint32_t a, uint32_t b) const { return add_mod(a, b, Q); }
-    FHE_DEV uint32_t sub(uint32_t a, uint32_t b) const { return sub_mod(a, b, Q); }
+    uint32_t Q, Q2;
+    FHE_DEV uint32_t lazy_mul(uint32_t x, TW w) const { return mul_shoup_lazy(x, w.x, w.y, Q); }
+    // CT: (x, y) in [0,4Q)^2 -> (x + wy, x - wy) in [0,4Q)^2
+    FHE_DEV void ct(uint32_t& x, uint32_t& y, TW w) const {
+        if (FHE_NTT_COPY) return;
+        x = csub(x, Q2);
+        const uint32_t t = lazy_mul(y, w);
+        y = x + Q2 - t;
+        x = x + t;
+    }
+    // GS: (x, y) in [0,2Q)^2 -> (x + y, (x - y) w) in [0,2Q)^2
+    FHE_DEV void gs(uint32_t& x, uint32_t& y, TW w) const {
+        if (FHE_NTT_COPY) return;
+        const uint32_t d = x + Q2 - y;
+        x = csub(x + y, Q2);
+        y = lazy_mul(d, w);
+    }
+    // last inverse stage with N^-1 folded: ((x + y) n^-1, (x - y) w1 n^-1) in [0,Q)
+    FHE_DEV void gs_last(uint32_t& x, uint32_t& y, TW lo, TW hi) const {
+        if (FHE_NTT_COPY) return;
+        const uint32_t d = x + Q2 - y;
+        x = csub(lazy_mul(x + y, lo), Q);
+        y = csub(lazy_mul(d, hi), Q);
+    }
+    FHE_DEV uint32_t fwd_out(uint32_t x) const { return csub(csub(x, Q2), Q); }
 };
 
+// 64-bit path (Q < 2^62): fully reduced butterflies.
 template <>
 struct ModT<uint64_t> {
     using TW = ulonglong2;  // (w, w' = floor(w 2^64 / Q))
-    uint64_t Q;
-    FHE_DEV uint64_t mul(uint64_t x, TW w) const { return mul_shoup64(x, w.x, w.y, Q); }
-    FHE_DEV uint64_t add(uint64_t a, uint64_t b) const { return add_mod64(a, b, Q); }
-    FHE_DEV uint64_t sub(uint64_t a, uint64_t b) const { return sub_mod64(a, b, Q); }
+    uint64_t Q, Q2;
+    FHE_DEV void ct(uint64_t& x, uint64_t& y, TW w) const {
+        if (FHE_NTT_COPY) return;
+        const uint64_t t = mul_shoup64(y, w.x, w.y, Q);
+        y = sub_mod64(x, t, Q);
+        x = add_mod64(x, t, Q);
+    }
+    FHE_DEV void gs(uint64_t& x, uint64_t& y, TW w) const {
+        if (FHE_NTT_COPY) return;
+        const uint64_t t = sub_mod64(x, y, Q);
+        x = add_mod64(x, y, Q);
+        y = mul_shoup64(t, w.x, w.y, Q);
+    }
+    FHE_DEV void gs_last(uint64_t& x, uint64_t& y, TW lo, TW hi) const {
+        if (FHE_NTT_COPY) return;
+        const uint64_t s = add_mod64(x, y, Q), d = sub_mod64(x, y, Q);
+        x = mul_shoup64(s, lo.x, lo.y, Q);
+        y = mul_shoup64(d, hi.x, hi.y, Q);
+    }
+    FHE_DEV uint64_t fwd_out(uint64_t x) const { return x; }
 };
-
-template <typename M, typename T>
-FHE_DEV void bf_ct(T& x, T& y, typename M::TW w, const M& m) {
-    T t = m.mul(y, w);
-    y   = m.sub(x, t);
-    x   = m.add(x, t);
-}
-template <typename M, typename T>
-FHE_DEV void bf_gs(T& x, T& y, typename M::TW w, const M& m) {
-    T t = m.sub(x, y);
-    x   = m.add(x, y);
-    y   = m.mul(t, w);
-}
 
 // 32x32 transpose of one half-wave's registers through its private LDS tile
 // (row stride 33 words: conflict-free on both sides).
@@ -66,58 +101,29 @@ template <typename T>
 FHE_DEV void half_transpose(T (&v)[32], T* tile, int l) {
 #pragma unroll
     for (int r = 0; r < 32; ++r) tile[l * 33 + r] = v[r];
-    __syncthreads();
+    if (FHE_NTT_WAVESYNC) { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); }
+    else __syncthreads();
 #pragma unroll
     for (int r = 0; r < 32; ++r) v[r] = tile[r * 33 + l];
-    __syncthreads();
+    if (FHE_NTT_WAVESYNC) { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); }
+    else __syncthreads();
 }
 
-template <typename T>
-FHE_DEV void load_pair(const uint64_t* p, T& a, T& b) {
-    ulonglong2 t = *reinterpret_cast<const ulonglong2*>(p);
-    a = (T)t.x;
-    b = (T)t.y;
-}
-template <typename T>
-FHE_DEV void store_pair(uint64_t* p, T a, T b) {
-    ulonglong2 t;
-    t.x = (uint64_t)a;
-    t.y = (uint64_t)b;
-    *reinterpret_cast<ulonglong2*>(p) = t;
-}
-
-template <typename T, bool INV, int PPB>
-__global__ void __launch_bounds__(PPB * 32)
-    k_ntt1024(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
-              const typename ModT<T>::TW* __restrict__ tab, T Q, typename ModT<T>::TW last_lo,
-              typename ModT<T>::TW last_hi) {
-    using M  = ModT<T>;
-    using TW = typename M::TW;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    TW* s_tw = reinterpret_cast<TW*>(smem);                      // 1024 entries
-    T* tiles = reinterpret_cast<T*>(smem + 1024 * sizeof(TW));   // PPB x 32 x 33
-    const M m{Q};
-
-    for (int i = threadIdx.x; i < 1024; i += PPB * 32) s_tw[i] = tab[i];
-
-    const int l        = threadIdx.x & 31;
-    const int hp       = threadIdx.x >> 5;
-    const uint32_t ply = blockIdx.x * PPB + hp;
-    const bool valid   = ply < count;
-    T* tile            = tiles + hp * (32 * 33);
-    const uint64_t* src = in + (size_t)(valid ? ply : 0) * 1024;
-    uint64_t* dst       = out + (size_t)(valid ? ply : 0) * 1024;
-
-    T v[32];
+// Raw 16-byte coefficient-pair loads of one polynomial row for this lane (layout A).
+FHE_DEV void load_raw(ulonglong2 (&pre)[16], const uint64_t* src, int l) {
 #pragma unroll
-    for (int h = 0; h < 16; ++h) {
-        if (valid) load_pair(src + (h << 6) + (l << 1), v[2 * h], v[2 * h + 1]);
-        else v[2 * h] = v[2 * h + 1] = 0;
-    }
-    __syncthreads();  // s_tw ready
+    for (int h = 0; h < 16; ++h) pre[h] = *reinterpret_cast<const ulonglong2*>(src + (h << 6) + (l << 1));
+}
 
+// Forward (CT, Table) or inverse (GS, TableI, N^-1 folded into the last stage) transform of
+// the 32 coefficients a half-wave lane holds in layout A; returns them in layout A.
+template <typename T, bool INV>
+FHE_DEV void transform(T (&v)[32], const typename ModT<T>::TW* __restrict__ tab, const typename ModT<T>::TW* s_tw,
+                       T* tile, int l, const ModT<T>& m, typename ModT<T>::TW last_lo, typename ModT<T>::TW last_hi) {
+    using TW    = typename ModT<T>::TW;
+    const int hl = l >> 1;
     if (!INV) {
-        // stages on bits 9..6 (layout A): twiddle index depends on h only
+        // stages on bits 9..6 (layout A): twiddle index depends on h only (scalar loads)
 #pragma unroll
         for (int b = 9; b >= 6; --b) {
             const int hb = b - 6;
@@ -125,13 +131,12 @@ __global__ void __launch_bounds__(PPB * 32)
             for (int h = 0; h < 16; ++h) {
                 if (h & (1 << hb)) continue;
                 const TW w = tab[(1 << (9 - b)) + (h >> (hb + 1))];
-                bf_ct(v[(h << 1) | 0], v[((h | (1 << hb)) << 1) | 0], w, m);
-                bf_ct(v[(h << 1) | 1], v[((h | (1 << hb)) << 1) | 1], w, m);
+                m.ct(v[(h << 1) | 0], v[((h | (1 << hb)) << 1) | 0], w);
+                m.ct(v[(h << 1) | 1], v[((h | (1 << hb)) << 1) | 1], w);
             }
         }
         half_transpose(v, tile, l);
         // layout B: lane = (h << 1) | b0, register r = x bits 5..1
-        const int hl = l >> 1;
 #pragma unroll
         for (int b = 5; b >= 1; --b) {
             const int rb = b - 1;
@@ -139,25 +144,17 @@ __global__ void __launch_bounds__(PPB * 32)
             for (int r = 0; r < 32; ++r) {
                 if (r & (1 << rb)) continue;
                 const TW w = s_tw[(1 << (9 - b)) + ((hl << (5 - b)) | (r >> b))];
-                bf_ct(v[r], v[r | (1 << rb)], w, m);
+                m.ct(v[r], v[r | (1 << rb)], w);
             }
         }
         half_transpose(v, tile, l);
         // stage on bit 0 (layout A)
 #pragma unroll
-        for (int h = 0; h < 16; ++h) {
-            const TW w = s_tw[512 + (h << 5) + l];
-            bf_ct(v[2 * h], v[2 * h + 1], w, m);
-        }
+        for (int h = 0; h < 16; ++h) m.ct(v[2 * h], v[2 * h + 1], s_tw[512 + (h << 5) + l]);
     } else {
-        // stage on bit 0 (layout A), GS butterflies with the inverse table
 #pragma unroll
-        for (int h = 0; h < 16; ++h) {
-            const TW w = s_tw[512 + (h << 5) + l];
-            bf_gs(v[2 * h], v[2 * h + 1], w, m);
-        }
+        for (int h = 0; h < 16; ++h) m.gs(v[2 * h], v[2 * h + 1], s_tw[512 + (h << 5) + l]);
         half_transpose(v, tile, l);
-        const int hl = l >> 1;
 #pragma unroll
         for (int b = 1; b <= 5; ++b) {
             const int rb = b - 1;
@@ -165,7 +162,7 @@ __global__ void __launch_bounds__(PPB * 32)
             for (int r = 0; r < 32; ++r) {
                 if (r & (1 << rb)) continue;
                 const TW w = s_tw[(1 << (9 - b)) + ((hl << (5 - b)) | (r >> b))];
-                bf_gs(v[r], v[r | (1 << rb)], w, m);
+                m.gs(v[r], v[r | (1 << rb)], w);
             }
         }
         half_transpose(v, tile, l);
@@ -176,35 +173,106 @@ __global__ void __launch_bounds__(PPB * 32)
             for (int h = 0; h < 16; ++h) {
                 if (h & (1 << hb)) continue;
                 const TW w = tab[(1 << (9 - b)) + (h >> (hb + 1))];
-                bf_gs(v[(h << 1) | 0], v[((h | (1 << hb)) << 1) | 0], w, m);
-                bf_gs(v[(h << 1) | 1], v[((h | (1 << hb)) << 1) | 1], w, m);
+                m.gs(v[(h << 1) | 0], v[((h | (1 << hb)) << 1) | 0], w);
+                m.gs(v[(h << 1) | 1], v[((h | (1 << hb)) << 1) | 1], w);
             }
         }
         // bit 9: lo' = (lo + hi) N^-1, hi' = (lo - hi) w1 N^-1
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-#pragma unroll
-            for (int b0 = 0; b0 < 2; ++b0) {
-                T& x = v[(h << 1) | b0];
-                T& y = v[((h | 8) << 1) | b0];
-                T s = m.add(x, y), d = m.sub(x, y);
-                x   = m.mul(s, last_lo);
-                y   = m.mul(d, last_hi);
-            }
+            m.gs_last(v[(h << 1) | 0], v[((h | 8) << 1) | 0], last_lo, last_hi);
+            m.gs_last(v[(h << 1) | 1], v[((h | 8) << 1) | 1], last_lo, last_hi);
         }
-    }
-    if (valid) {
-#pragma unroll
-        for (int h = 0; h < 16; ++h) store_pair(dst + (h << 6) + (l << 1), v[2 * h], v[2 * h + 1]);
     }
 }
 
-template <typename T, int PPB>
+// Persistent, software-pipelined batch kernel.  A wave transforms a pair of
+// polynomials per iteration (one per half-wave) and walks pairs wave_id,
+// wave_id + W, ... (W = waves in the grid); the raw loads of its next pair are
+// issued before the current pair's arithmetic and stores, so HBM reads, the
+// butterflies and HBM writes of consecutive pairs overlap.  The LDS twiddle
+// table is filled once per workgroup; the transposes use half-wave-private LDS
+// tiles and need only wave-level ordering.
+template <typename T, bool INV>
+__global__ void __launch_bounds__(256)
+    k_ntt1024(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
+              const typename ModT<T>::TW* __restrict__ tab, T Q, typename ModT<T>::TW last_lo,
+              typename ModT<T>::TW last_hi) {
+    using M  = ModT<T>;
+    using TW = typename M::TW;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    TW* s_tw = reinterpret_cast<TW*>(smem);                      // 1024 entries
+    T* tiles = reinterpret_cast<T*>(smem + 1024 * sizeof(TW));   // 8 x 32 x 33
+    const M m{Q, (T)(2 * Q)};
+
+    for (int i = threadIdx.x; i < 1024; i += 256) s_tw[i] = tab[i];
+
+    const int l  = threadIdx.x & 31;
+    const int hp = threadIdx.x >> 5;                 // half-wave within the workgroup
+    T* tile      = tiles + hp * (32 * 33);
+    const uint32_t npairs = (count + 1) >> 1;
+    const uint32_t W      = gridDim.x * 4;
+    uint32_t pair         = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t half   = (threadIdx.x >> 5) & 1;
+
+    // Rows are clamped to count - 1, so every load and store is unconditional (the
+    // waitcnt before each unpack then covers just the prefetch, not the previous
+    // pair's stores).  The second half-wave of an odd tail pair transforms row
+    // count - 1 as well and rewrites the same values; prefetches past the last
+    // pair load row count - 1 and are never used.
+    auto row = [&](uint32_t pr) -> uint32_t {
+        const uint32_t ply = 2 * pr + half;
+        return ply < count ? ply : count - 1;
+    };
+    // one pair: unpack the raw words, transform, store (the register buffer is then free)
+    auto step = [&](ulonglong2 (&buf)[16], uint32_t pr) {
+        T v[32];
+#pragma unroll
+        for (int h = 0; h < 16; ++h) {
+            v[2 * h]     = (T)buf[h].x;
+            v[2 * h + 1] = (T)buf[h].y;
+        }
+        transform<T, INV>(v, tab, s_tw, tile, l, m, last_lo, last_hi);
+        uint64_t* dst = out + (size_t)row(pr) * 1024;
+#pragma unroll
+        for (int h = 0; h < 16; ++h) {
+            ulonglong2 t;
+            t.x = (uint64_t)(INV ? v[2 * h] : m.fwd_out(v[2 * h]));
+            t.y = (uint64_t)(INV ? v[2 * h + 1] : m.fwd_out(v[2 * h + 1]));
+            *reinterpret_cast<ulonglong2*>(dst + (h << 6) + (l << 1)) = t;
+        }
+    };
+    // two register buffers, alternated by a 2x unrolled loop: the next pair's loads are
+    // in flight while the current pair is transformed and stored, with no copies
+    ulonglong2 bufA[16], bufB[16];
+    if (pair < npairs) load_raw(bufA, in + (size_t)row(pair) * 1024, l);
+    __syncthreads();  // s_tw ready
+    for (; pair < npairs; pair += 2 * W) {
+        load_raw(bufB, in + (size_t)row(pair + W) * 1024, l);
+        __builtin_amdgcn_sched_barrier(0);
+        step(bufA, pair);
+        if (pair + W >= npairs) break;
+        load_raw(bufA, in + (size_t)row(pair + 2 * W) * 1024, l);
+        __builtin_amdgcn_sched_barrier(0);
+        step(bufB, pair + W);
+    }
+}
+
+#ifndef FHE_NTT_WPS
+#define FHE_NTT_WPS 2   // resident waves per SIMD the grid is sized for
+#endif
+
+template <typename T>
 static hipError_t launch(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                          hipStream_t s) {
     using TW        = typename ModT<T>::TW;
-    const size_t sm = 1024 * sizeof(TW) + (size_t)PPB * 32 * 33 * sizeof(T);
-    dim3 grid((count + PPB - 1) / PPB), block(PPB * 32);
+    const size_t sm = 1024 * sizeof(TW) + (size_t)8 * 32 * 33 * sizeof(T);
+    if (count == 0) return hipSuccess;
+    // one workgroup = 4 waves = 8 polynomials per iteration; cap the grid at the
+    // resident capacity so that every wave iterates (pipelining) on large batches
+    const uint32_t groups = (count + 7) / 8;
+    const uint32_t cap    = (uint32_t)p.cus * FHE_NTT_WPS;  // 4 waves/group, 4 SIMDs/CU
+    dim3 grid(groups < cap ? groups : cap), block(256);
     const TW* tab = reinterpret_cast<const TW*>(inverse ? p.d_tab_inv : p.d_tab_fwd);
     TW lo, hi;
     if constexpr (sizeof(T) == 4) {
@@ -214,18 +282,17 @@ static hipError_t launch(const NttPlan& p, const uint64_t* in, uint64_t* out, ui
         lo = TW{p.ninv, p.ninv_pre};
         hi = TW{p.w1ninv, p.w1ninv_pre};
     }
-    if (count == 0) return hipSuccess;
     if (inverse)
-        hipLaunchKernelGGL((k_ntt1024<T, true, PPB>), grid, block, sm, s, in, out, count, tab, (T)p.Q, lo, hi);
+        hipLaunchKernelGGL((k_ntt1024<T, true>), grid, block, sm, s, in, out, count, tab, (T)p.Q, lo, hi);
     else
-        hipLaunchKernelGGL((k_ntt1024<T, false, PPB>), grid, block, sm, s, in, out, count, tab, (T)p.Q, lo, hi);
+        hipLaunchKernelGGL((k_ntt1024<T, false>), grid, block, sm, s, in, out, count, tab, (T)p.Q, lo, hi);
     return hipGetLastError();
 }
 
 hipError_t ntt1024_launch(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                           hipStream_t s) {
-    if (p.wide) return launch<uint64_t, 4>(p, in, out, count, inverse, s);
-    return launch<uint32_t, 8>(p, in, out, count, inverse, s);
+    if (p.wide) return launch<uint64_t>(p, in, out, count, inverse, s);
+    return launch<uint32_t>(p, in, out, count, inverse, s);
 }
 
 }  // namespace fhe_amd

@@ -14,12 +14,13 @@ hipError_t ntt_plan_init(NttPlan& p, uint64_t Q, uint64_t psi, uint32_t N, int d
     HostNtt h;
     h.init(N, Q, psi);
     p.Q = Q; p.psi = psi; p.N = N; p.device = device;
-    p.wide = Q >= (1ull << 31);
+    p.wide = Q >= (1ull << 30);  // the 32-bit path keeps lazy values below 4Q < 2^32
     const uint64_t w1 = h.tabI[1];
     p.ninv = h.ninv;
     p.w1ninv = mulmod(w1, h.ninv, Q);
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&p.cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess) return e;
     if (!p.wide) {
         std::vector<uint32_t> f(2 * N), iv(2 * N);
         for (uint32_t i = 0; i < N; ++i) {

@@ -127,3 +127,54 @@ def test_gpu_ntt_empty_and_bad_params():
     assert plan.forward(np.zeros((0, 1024), np.uint64)).shape == (0, 1024)
     with pytest.raises(FheHipError):
         NttPlan(134215683)   # not prime
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Q", [1073707009, 2147473409])
+def test_gpu_ntt_lazy_bound_moduli(Q, restatement):
+    """moduli at the edge of the 32-bit lazy path (4Q < 2^32 needs Q < 2^30; larger Q
+    takes the 64-bit path), with all-(Q-1) rows as the worst case for lazy bounds."""
+    from fhe_amd import NttPlan
+    plan = NttPlan(Q)
+    rng = np.random.default_rng(17)
+    x = rng.integers(0, Q, size=(9, 1024), dtype=np.uint64)
+    x[0] = Q - 1
+    x[1, ::2] = Q - 1
+    f = plan.forward(x)
+    assert np.array_equal(f, restatement.ntt(Q, plan.psi, x))
+    assert np.array_equal(plan.inverse(x), restatement.ntt(Q, plan.psi, x, inverse=True))
+    assert np.array_equal(plan.inverse(f), x)
+
+
+@pytest.mark.gpu
+def test_gpu_ntt_multi_iteration_out_of_place(restatement):
+    """a batch larger than the persistent grid (every wave loops, odd tail pair),
+    out-of-place on device buffers == in-place host path; sampled rows vs the oracle."""
+    import ctypes
+    from fhe_amd import NttPlan
+    from fhe_amd._lib import check, lib, ptr, vp
+    Q = 134215681
+    plan = NttPlan(Q)
+    count = 20001
+    rng = np.random.default_rng(23)
+    x = rng.integers(0, Q, size=(count, 1024), dtype=np.uint64)
+    ref = plan.forward(x)
+    dx, dy = vp(), vp()
+    check(lib().fhe_hip_alloc(0, x.nbytes, ctypes.byref(dx)))
+    check(lib().fhe_hip_alloc(0, x.nbytes, ctypes.byref(dy)))
+    try:
+        check(lib().fhe_hip_copy_to_device(dx, ptr(x), x.nbytes))
+        plan.run_device(dx.value, dy.value, count, False)
+        check(lib().fhe_hip_synchronize(0))
+        y = np.zeros_like(x)
+        xin = np.zeros_like(x)
+        check(lib().fhe_hip_copy_to_host(ptr(y), dy, x.nbytes))
+        check(lib().fhe_hip_copy_to_host(ptr(xin), dx, x.nbytes))
+    finally:
+        lib().fhe_hip_free(dx)
+        lib().fhe_hip_free(dy)
+    assert np.array_equal(y, ref)
+    assert np.array_equal(xin, x)   # input untouched
+    rows = [0, 1, 4095, 4096, 12345, count - 2, count - 1]
+    assert np.array_equal(ref[rows], restatement.ntt(Q, plan.psi, x[rows]))
+    assert np.array_equal(plan.inverse(ref), x)
