@@ -563,16 +563,19 @@ namespace {
 // EVAL-domain automorphism X -> X^k (poly-impl.h:350-356 / PrecomputeAutoMap, nbtheory2.cpp:264-275):
 // out[slot brv(j)] = in[slot brv(((2j+1)k mod 2N) >> 1)].  Through the half-wave's LDS region
 // (row stride 33: conflict-free writes).
+// Output slot x = (l << 5) | r has j = brv10(x) = (brv5(r) << 5) | brv5(l), so
+// (2j+1) k = (2 brv5(l) + 1) k + 64 brv5(r) k: one per-lane term plus a wave-uniform
+// term per register (k is uniform), and no per-register index stays live across calls.
 FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint32_t k) {
 #pragma unroll
     for (int r = 0; r < 32; ++r) region[l * 33 + r] = v[r];
     wave_lds_sync();
+    const uint32_t cl = (2 * (__builtin_bitreverse32((uint32_t)l) >> 27) + 1) * k;
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
-        const uint32_t x  = (uint32_t)(l << 5) | r;            // output slot
-        const uint32_t j  = __builtin_bitreverse32(x) >> 22;   // brv10
-        const uint32_t t  = (((2 * j + 1) * k) & 2047) >> 1;
-        const uint32_t sx = __builtin_bitreverse32(t) >> 22;   // source slot
+        const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
+        const uint32_t t  = ((cl + sr) & 2047) >> 1;
+        const uint32_t sx = __builtin_bitreverse32(t) >> 22;   // source slot brv10(t)
         v[r]              = region[sx + (sx >> 5)];
     }
     wave_lds_sync();
