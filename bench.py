@@ -158,6 +158,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(f"k_blind_rotate_{args.method}", B),
             "launch_ms": round(br_ms, 4), "keyswitch_ms": round(ks_ms, 4),
             "alg_bytes_per_launch": alg_bytes,
+            "traffic_note": "2*FETCH_SIZE+WRITE_SIZE (profiles/*pmc_traffic.json); FETCH counts L2->fabric "
+                            "requests incl. Infinity-Cache hits: the BSK is streamed once per XCD per wave "
+                            "generation (8 XCDs x 4 generations at B=8192) from the 256 MiB cache",
             "valu_note": "integer-VALU bound: modmul rate below",
             "modmul_per_s": round(mm_per_gate * B / (br_ms * 1e-3) / 1e12, 3), "modmul_unit": "T/s",
         }
