@@ -25,7 +25,9 @@ from ._lib import FheHipError, check, lib, ptr, sz, u64, vp
 TOY, STD128, STD128_LMKCDEY = 0, 3, 21
 AP, GINX, LMKCDEY = 1, 2, 3
 OR, AND, NOR, NAND, XOR, XNOR, MAJORITY, AND3, OR3, AND4, OR4, XOR_FAST, XNOR_FAST, CMUX = range(14)
-GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR}
+GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR, "MAJORITY": MAJORITY,
+              "AND3": AND3, "OR3": OR3, "AND4": AND4, "OR4": OR4, "CMUX": CMUX}
+MULTI_GATES = (MAJORITY, AND3, OR3, AND4, OR4)
 
 
 class _Params(ctypes.Structure):
@@ -57,6 +59,15 @@ def _setup(L):
     L.fhe_hip_keygen.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp, vp, vp, vp]
     L.fhe_hip_encrypt.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, vp, vp]
     L.fhe_hip_decrypt.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, sz, ctypes.c_uint32, u64, vp]
+    L.fhe_hip_eval_gate_multi_batch.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, sz, vp, vp, vp,
+                                                vp, ctypes.c_int]
+    L.fhe_hip_eval_gate_multi_batch_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, sz, vp,
+                                                       vp, vp, vp, vp]
+    L.fhe_hip_eval_cmux_batch.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_eval_cmux_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_encrypt_ptmod.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, ctypes.c_uint32, vp, vp]
+    L.fhe_hip_decrypt_ptmod.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, sz, ctypes.c_uint32, u64,
+                                        ctypes.c_uint32, vp]
     L.fhe_hip_multi_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.fhe_hip_multi_destroy.argtypes = [vp]
     L.fhe_hip_multi_destroy.restype = None
@@ -119,23 +130,31 @@ def keygen(paramset, method, seed):
     return KeySet(sk, bsk, A, B)
 
 
-def encrypt(paramset, method, sk, bits, seed):
+def encrypt(paramset, method, sk, bits, seed, p=4):
+    """LWE encryptions of `bits` (messages mod p) under sk, mod q (lwe-pke.cpp:103-128)."""
     P = params(paramset, method)
     bits = np.ascontiguousarray(bits, dtype=np.int32)
     a = np.zeros((len(bits), P.n), np.uint64)
     b = np.zeros(len(bits), np.uint64)
-    check(L().fhe_hip_encrypt(paramset, method, ptr(_u64(sk)), ptr(bits), len(bits), seed, ptr(a), ptr(b)))
+    check(L().fhe_hip_encrypt_ptmod(paramset, method, ptr(_u64(sk)), ptr(bits), len(bits), seed, p, ptr(a), ptr(b)))
     return a, b
 
 
-def decrypt(paramset, method, sk, a, b, mod=None):
+def decrypt(paramset, method, sk, a, b, mod=None, p=4):
     P = params(paramset, method)
     a = _u64(np.atleast_2d(a))
     b = _u64(np.atleast_1d(b))
     out = np.zeros(len(b), np.int64)
-    check(L().fhe_hip_decrypt(paramset, method, ptr(_u64(sk)), ptr(a), ptr(b), len(b), a.shape[1],
-                              mod if mod is not None else P.q, ptr(out)))
+    check(L().fhe_hip_decrypt_ptmod(paramset, method, ptr(_u64(sk)), ptr(a), ptr(b), len(b), a.shape[1],
+                                    mod if mod is not None else P.q, p, ptr(out)))
     return out
+
+
+def _ptrs(arrs):
+    t = (vp * len(arrs))()
+    for j, x in enumerate(arrs):
+        t[j] = x.ctypes.data if isinstance(x, np.ndarray) else x
+    return t
 
 
 class GateEngine:
@@ -196,6 +215,37 @@ class GateEngine:
     def keyswitch_workspace_device(self, count, d_ao, d_bo, stream=None):
         check(L().fhe_hip_keyswitch_workspace_device(self._h, count, vp(d_ao), vp(d_bo),
                                                      vp(stream) if stream else None))
+
+    def eval_gate_multi(self, gate, a_list, b_list, p, extended=False):
+        """EvalBinGate(gate, ctvector) for MAJORITY/AND3/OR3/AND4/OR4 over a batch of k-tuples:
+        a_list[j] [count][n], b_list[j] [count]; p = plaintext modulus of the inputs."""
+        a_list = [_u64(a) for a in a_list]
+        b_list = [_u64(b) for b in b_list]
+        cnt = len(b_list[0])
+        ao = np.zeros((cnt, self.params.N if extended else self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_eval_gate_multi_batch(self._h, gate, len(a_list), p, cnt, _ptrs(a_list), _ptrs(b_list),
+                                                ptr(ao), ptr(bo), int(extended)))
+        return ao, bo
+
+    def eval_cmux(self, a0, b0, a1, b1, a2, b2):
+        """EvalBinGate(CMUX, {ct0, ct1, ct2}) = ct2 ? ct1 : ct0 over a batch."""
+        a0, b0, a1, b1, a2, b2 = (_u64(x) for x in (a0, b0, a1, b1, a2, b2))
+        cnt = len(b0)
+        ao = np.zeros((cnt, self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_eval_cmux_batch(self._h, cnt, ptr(a0), ptr(b0), ptr(a1), ptr(b1), ptr(a2), ptr(b2),
+                                          ptr(ao), ptr(bo)))
+        return ao, bo
+
+    def eval_gate_multi_device(self, gate, count, p, d_a_list, d_b_list, d_ao, d_bo, stream=None):
+        check(L().fhe_hip_eval_gate_multi_batch_device(self._h, gate, len(d_a_list), p, count, _ptrs(d_a_list),
+                                                       _ptrs(d_b_list), vp(d_ao), vp(d_bo),
+                                                       vp(stream) if stream else None))
+
+    def eval_cmux_device(self, count, d_a0, d_b0, d_a1, d_b1, d_a2, d_b2, d_ao, d_bo, stream=None):
+        check(L().fhe_hip_eval_cmux_batch_device(self._h, count, vp(d_a0), vp(d_b0), vp(d_a1), vp(d_b1), vp(d_a2),
+                                                 vp(d_b2), vp(d_ao), vp(d_bo), vp(stream) if stream else None))
 
     def keyswitch(self, a, b):
         a, b = _u64(a), _u64(b)
@@ -258,6 +308,7 @@ class LWECiphertext:
     a: np.ndarray
     b: int
     modulus: int
+    p: int = 4  # plaintext modulus (GetptModulus)
 
 
 @dataclass
@@ -293,17 +344,55 @@ class BinFHEContext:
     def BTKeyLoad(self, bsk, kskA, kskB):
         self.engine.load_keys(bsk, kskA, kskB)
 
-    def Encrypt(self, sk, m):
-        a, b = encrypt(self.paramset, self.method, sk.s, [int(m)], self._next_seed())
-        return LWECiphertext(a[0], int(b[0]), self.params.q)
+    def Encrypt(self, sk, m, output=None, p=4):
+        """Encrypt(sk, m, SMALL_DIM, p) (binfhecontext.cpp:220-234)"""
+        a, b = encrypt(self.paramset, self.method, sk.s, [int(m)], self._next_seed(), p)
+        return LWECiphertext(a[0], int(b[0]), self.params.q, p)
 
-    def Decrypt(self, sk, ct):
-        return int(decrypt(self.paramset, self.method, sk.s, ct.a[None, :], [ct.b], ct.modulus)[0])
+    def Decrypt(self, sk, ct, p=4):
+        return int(decrypt(self.paramset, self.method, sk.s, ct.a[None, :], [ct.b], ct.modulus, p)[0])
 
-    def EvalBinGate(self, gate, ct1, ct2):
+    def EvalNOT(self, ct):
+        """EvalNOT (binfhe-base-scheme.cpp:223-236): (q - a, q/4 - b) mod q"""
+        q = ct.modulus
+        a = np.where(ct.a == 0, 0, q - ct.a.astype(np.uint64)).astype(np.uint64)
+        return LWECiphertext(a, int(((q >> 2) - ct.b) % q), q, ct.p)
+
+    def EvalBinGate(self, gate, ct1, ct2=None):
+        """EvalBinGate(gate, ct1, ct2) or EvalBinGate(gate, ctvector) (binfhecontext.h:305-315)"""
+        if ct2 is None:
+            return self._eval_vector(gate, list(ct1))
         if ct1 is ct2:
             raise FheHipError(-8, "Input ciphertexts should be independant")
         return self.EvalBinGateBatch(gate, [ct1], [ct2])[0]
+
+    def _eval_vector(self, gate, cts):
+        for i in range(len(cts)):
+            for j in range(i + 1, len(cts)):
+                if cts[i] is cts[j]:
+                    raise FheHipError(-8, "Input ciphertexts should be independent")
+        if gate in MULTI_GATES:
+            p = cts[0].p
+            ao, bo = self.engine.eval_gate_multi(gate, [c.a[None, :] for c in cts],
+                                                 [np.array([c.b], np.uint64) for c in cts], p)
+            return LWECiphertext(ao[0], int(bo[0]), self.params.q, p)
+        if gate == CMUX:
+            if len(cts) != 3:
+                raise FheHipError(-8, "CMUX gate implemented for ciphertext vectors of size 3")
+            return self.EvalCMUXBatch([cts[0]], [cts[1]], [cts[2]])[0]
+        raise FheHipError(-8, "This gate is not implemented for vector of ciphertexts at this time")
+
+    def EvalCMUXBatch(self, ct_sel, ct_true, ct_false):
+        """EvalCMUXBatch (batch.cpp:212-249): EvalBinGate(CMUX, {sel, true, false}) per element,
+        which the reference evaluates as ctvector[2] ? ctvector[1] : ctvector[0]."""
+        if not (len(ct_sel) == len(ct_true) == len(ct_false)):
+            raise FheHipError(-2, "Input size mismatch")
+        if not ct_sel:
+            return []
+        st = lambda cs: (np.stack([c.a for c in cs]), np.array([c.b for c in cs], np.uint64))  # noqa: E731
+        (a0, b0), (a1, b1), (a2, b2) = st(ct_sel), st(ct_true), st(ct_false)
+        ao, bo = self.engine.eval_cmux(a0, b0, a1, b1, a2, b2)
+        return [LWECiphertext(ao[i], int(bo[i]), self.params.q) for i in range(len(bo))]
 
     def EvalBinGateBatch(self, gate, ct1, ct2):
         """EvalBinGateBatch (src/binfhe/lib/batch/batch.cpp:176-210) on the GPU."""

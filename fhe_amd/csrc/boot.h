@@ -21,22 +21,33 @@ struct BootTables {
 struct GateArgs {
     uint32_t count, n, N, q, qKS;
     uint32_t lb, ub, lv, uv, factor;  // BootstrapGateCore test-vector window (binfhe-base-scheme.cpp:535-567)
-    uint32_t b_const;                 // (Q >> 3) + 1 (binfhe-base-scheme.cpp:118-120)
+    uint32_t b_const;                 // Q/(2p) + 1 (binfhe-base-scheme.cpp:118-120, :162-163)
     uint32_t xor_double;              // XOR/XNOR: 2 (ct1 + ct2)
     uint32_t msb_out;                 // 1: write ctExt mod-switched to qKS; 0: raw ctExt mod Q
     uint32_t gbits;                   // log2(baseG)
 };
 
-// GINX/CGGI: inputs (u64, mod q) -> monomial exponents + test-vector b
-hipError_t launch_prep_ginx(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
-                            const uint64_t* b2, uint16_t* idx, uint32_t* tvb, hipStream_t s);
+// The LWE ciphertext a gate bootstraps: ct = sum_j (-1)^{neg_j} ct_j + (0, boff) mod q, then
+// doubled for XOR/XNOR.  2-input gates: k = 2 (binfhe-base-scheme.cpp:95-107); AND3/OR3/AND4/
+// OR4/MAJORITY: k = 3..4 (:146-150); CMUX's NAND(ct0, NOT ct2): neg = {ct2}, boff = q/4
+// (EvalNOT :223-236 folded into the sum).  Inputs are u64 [count][n] / [count], mod q.
+struct GateInputs {
+    const uint64_t* a[4];
+    const uint64_t* b[4];
+    uint32_t k;         // 1..4
+    uint32_t neg_mask;  // bit j: subtract input j
+    uint32_t boff;      // added to b
+};
+
+// GINX/CGGI: inputs -> monomial exponents + test-vector b
+hipError_t launch_prep_ginx(const GateArgs& g, const GateInputs& in, uint16_t* idx, uint32_t* tvb, hipStream_t s);
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 // LMKCDEY: per-gate op schedule (EXT(i) / AUTO(t)), then the fused accumulator
-hipError_t launch_prep_lmk(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
-                           const uint64_t* b2, const int16_t* logGen, uint16_t* scratch, uint16_t* ops,
-                           uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys, hipStream_t s);
+hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen, uint16_t* scratch,
+                           uint16_t* ops, uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys,
+                           hipStream_t s);
 hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const void* bsk, const void* autok,
                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
                                    uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);

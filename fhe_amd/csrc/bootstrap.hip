@@ -244,24 +244,35 @@ FHE_DEV uint32_t mod_switch(uint64_t v, uint64_t from, uint64_t to) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// prep: ct = ct1 + ct2 (XOR/XNOR: 2(ct1 + ct2)) mod q (binfhe-base-scheme.cpp:95-107);
-// monomial exponent per i: ((q - a_i) mod q) * (2N / q) (rgsw-acc-cggi.cpp:62-66)
+// prep: ct = combination of the inputs (GateInputs, boot.h) mod q, doubled for XOR/XNOR
+// (binfhe-base-scheme.cpp:95-107, :146-150, :180-182); monomial exponent per i:
+// ((q - a_i) mod q) * (2N / q) (rgsw-acc-cggi.cpp:62-66)
 // ---------------------------------------------------------------------------
-__global__ void k_prep_ginx(const uint64_t* __restrict__ a1, const uint64_t* __restrict__ b1,
-                            const uint64_t* __restrict__ a2, const uint64_t* __restrict__ b2, GateArgs g,
-                            uint16_t* __restrict__ idx, uint32_t* __restrict__ tvb) {
+namespace {
+FHE_DEV uint32_t combine(const GateInputs& in, const uint64_t* const* v, size_t t, uint32_t boff, uint32_t qm,
+                         uint32_t dbl) {
+    uint32_t s = boff;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j < (int)in.k) {
+            const uint32_t x = (uint32_t)v[j][t];
+            s += ((in.neg_mask >> j) & 1) ? 0u - x : x;
+        }
+    }
+    s &= qm;
+    return dbl ? (2 * s) & qm : s;
+}
+}  // namespace
+
+__global__ void k_prep_ginx(GateInputs in, GateArgs g, uint16_t* __restrict__ idx, uint32_t* __restrict__ tvb) {
     const uint64_t total = (uint64_t)g.count * g.n;
     const uint32_t qm = g.q - 1, mbymod = 2 * g.N / g.q;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t a = (uint32_t)((a1[t] + a2[t]) & qm);
-        if (g.xor_double) a = (2 * a) & qm;
+        const uint32_t a = combine(in, in.a, t, 0, qm, g.xor_double);
         idx[t] = (uint16_t)(((g.q - a) & qm) * mbymod);
     }
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < g.count; t += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t b = (uint32_t)((b1[t] + b2[t]) & qm);
-        if (g.xor_double) b = (2 * b) & qm;
-        tvb[t] = b;
-    }
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < g.count; t += (uint64_t)gridDim.x * blockDim.x)
+        tvb[t] = combine(in, in.b, t, in.boff, qm, g.xor_double);
 }
 
 // ---------------------------------------------------------------------------
@@ -461,12 +472,12 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     }
 }
 
-hipError_t launch_prep_ginx(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
-                            const uint64_t* b2, uint16_t* idx, uint32_t* tvb, hipStream_t s) {
+hipError_t launch_prep_ginx(const GateArgs& g, const GateInputs& in, uint16_t* idx, uint32_t* tvb, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
+    if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
     const uint64_t total = (uint64_t)g.count * g.n;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_prep_ginx, dim3(blocks), dim3(256), 0, s, a1, b1, a2, b2, g, idx, tvb);
+    hipLaunchKernelGGL(k_prep_ginx, dim3(blocks), dim3(256), 0, s, in, g, idx, tvb);
     return hipGetLastError();
 }
 
@@ -489,9 +500,7 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
 //                         with (*ek)[0][1][t]                              (:257-287)
 // k_prep_lmk builds them with a stable counting sort of the a_i into the
 // logGen groups (permuteMap, :83-94) and replays the nSkips logic (:99-157).
-__global__ void k_prep_lmk(const uint64_t* __restrict__ a1, const uint64_t* __restrict__ b1,
-                           const uint64_t* __restrict__ a2, const uint64_t* __restrict__ b2, GateArgs g,
-                           const int16_t* __restrict__ logGen, uint16_t* __restrict__ scratch,
+__global__ void k_prep_lmk(GateInputs in, GateArgs g, const int16_t* __restrict__ logGen, uint16_t* __restrict__ scratch,
                            uint16_t* __restrict__ ops, uint32_t* __restrict__ nops, uint32_t* __restrict__ tvb,
                            uint32_t maxops, uint32_t numAutoKeys) {
     const uint32_t gate = blockIdx.x * blockDim.x + threadIdx.x;
@@ -500,11 +509,8 @@ __global__ void k_prep_lmk(const uint64_t* __restrict__ a1, const uint64_t* __re
     uint16_t* end    = scratch + (size_t)gate * (N + n);  // per position: counts -> bucket ends
     uint16_t* sorted = end + N;
     for (uint32_t p = 0; p < N; ++p) end[p] = 0;
-    const uint64_t* A1 = a1 + (size_t)gate * n;
-    const uint64_t* A2 = a2 + (size_t)gate * n;
     auto pos_of = [&](uint32_t i) -> uint32_t {
-        uint32_t a = (uint32_t)((A1[i] + A2[i]) & qm);
-        if (g.xor_double) a = (2 * a) & qm;
+        const uint32_t a = combine(in, in.a, (size_t)gate * n + i, 0, qm, g.xor_double);
         const uint32_t aodd = ((M - a) & (M - 1)) | 1u;  // (0 - a_i) mod 2N, made odd
         const int32_t v     = logGen[aodd];
         if (v == (int32_t)M) return Nh - 1;                          // -1
@@ -554,9 +560,7 @@ __global__ void k_prep_lmk(const uint64_t* __restrict__ a1, const uint64_t* __re
         }
     }
     nops[gate] = k;
-    uint32_t b = (uint32_t)((b1[gate] + b2[gate]) & qm);
-    if (g.xor_double) b = (2 * b) & qm;
-    tvb[gate] = b;
+    tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
 }
 
 namespace {
@@ -746,12 +750,13 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     }
 }
 
-hipError_t launch_prep_lmk(const GateArgs& g, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
-                           const uint64_t* b2, const int16_t* logGen, uint16_t* scratch, uint16_t* ops,
-                           uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys, hipStream_t s) {
+hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen, uint16_t* scratch,
+                           uint16_t* ops, uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys,
+                           hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prep_lmk, dim3((g.count + 63) / 64), dim3(64), 0, s, a1, b1, a2, b2, g, logGen, scratch, ops,
-                       nops, tvb, maxops, numAutoKeys);
+    if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_prep_lmk, dim3((g.count + 63) / 64), dim3(64), 0, s, in, g, logGen, scratch, ops, nops, tvb,
+                       maxops, numAutoKeys);
     return hipGetLastError();
 }
 

@@ -274,6 +274,53 @@ int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, cons
     });
 }
 
+int fhe_hip_eval_gate_multi_batch(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32_t ptmod, size_t count,
+                                  const uint64_t* const* a_in, const uint64_t* const* b_in, uint64_t* a_out,
+                                  uint64_t* b_out, int extended) {
+    if (!ctx || (count && (!a_in || !b_in || !a_out || !b_out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (k < 2 || k > 4) return fail(FHE_HIP_ERR_INVALID_PARAM, "k must be 2..4");
+    return guarded([&]() -> int {
+        ctx->eng.eval_gate_multi_host(gate, count, k, a_in, b_in, ptmod, a_out, b_out, extended != 0);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_gate_multi_batch_device(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32_t ptmod, size_t count,
+                                         const uint64_t* const* d_a_in, const uint64_t* const* d_b_in,
+                                         uint64_t* d_a_out, uint64_t* d_b_out, void* stream) {
+    if (!ctx || (count && (!d_a_in || !d_b_in || !d_a_out || !d_b_out)))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (k < 2 || k > 4) return fail(FHE_HIP_ERR_INVALID_PARAM, "k must be 2..4");
+    return guarded([&]() -> int {
+        ctx->eng.eval_gate_multi_device(gate, count, k, d_a_in, d_b_in, ptmod, d_a_out, d_b_out,
+                                        stream ? (hipStream_t)stream : ctx->eng.stream());
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_cmux_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a0, const uint64_t* b0,
+                            const uint64_t* a1, const uint64_t* b1, const uint64_t* a2, const uint64_t* b2,
+                            uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a0, b0, a1, b1, a_out, b_out) || (count && (!a2 || !b2)))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.eval_cmux_host(count, a0, b0, a1, b1, a2, b2, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a0, const uint64_t* d_b0,
+                                   const uint64_t* d_a1, const uint64_t* d_b1, const uint64_t* d_a2,
+                                   const uint64_t* d_b2, uint64_t* d_a_out, uint64_t* d_b_out, void* stream) {
+    if (!ctx || !io_ok(count, d_a0, d_b0, d_a1, d_b1, d_a_out, d_b_out) || (count && (!d_a2 || !d_b2)))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.eval_cmux_device(count, d_a0, d_b0, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
+                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+        return FHE_HIP_OK;
+    });
+}
+
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
                             uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
@@ -375,6 +422,27 @@ int fhe_hip_decrypt(int paramset, int method, const uint64_t* sk, const uint64_t
         Params p = make_params(paramset, method);
         if (len != p.n && len != p.N) return fail(FHE_HIP_ERR_INVALID_PARAM, "len must be n or N");
         for (size_t i = 0; i < count; ++i) out[i] = decrypt(p, sk, a + i * len, b[i], len, mod);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_encrypt_ptmod(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
+                          uint32_t ptmod, uint64_t* a, uint64_t* b) {
+    if (!sk || (count && (!bits || !a || !b))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        encrypt(make_params(paramset, method), sk, bits, count, seed, a, b, ptmod);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_decrypt_ptmod(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b,
+                          size_t count, uint32_t len, uint64_t mod, uint32_t ptmod, int64_t* out) {
+    if (!sk || (count && (!a || !b || !out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (ptmod < 2 || ptmod > mod) return fail(FHE_HIP_ERR_INVALID_PARAM, "plaintext modulus out of range");
+    return guarded([&]() -> int {
+        Params p = make_params(paramset, method);
+        if (len != p.n && len != p.N) return fail(FHE_HIP_ERR_INVALID_PARAM, "len must be n or N");
+        for (size_t i = 0; i < count; ++i) out[i] = decrypt(p, sk, a + i * len, b[i], len, mod, ptmod);
         return FHE_HIP_OK;
     });
 }

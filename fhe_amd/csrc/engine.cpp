@@ -34,7 +34,7 @@ Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       (void*)d_scratch_})
         if (ptr) (void)hipFree(ptr);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -168,31 +168,37 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
     FHE_HIP_CHECK(hipMemcpy(d_ksk_, dev.data(), dev.size() * 2, hipMemcpyHostToDevice));
 }
 
-GateArgs Engine::gate_args(int gate, size_t count) const {
+GateArgs Engine::gate_args(int gate, size_t count, uint32_t p, bool multi) const {
     switch (gate) {
         case G_OR: case G_AND: case G_NOR: case G_NAND: case G_XOR: case G_XNOR: case G_XOR_FAST: case G_XNOR_FAST:
+            if (multi) throw std::invalid_argument("EvalBinGate(ctvector): AND3, OR3, AND4, OR4, MAJORITY or CMUX only");
+            break;
+        case G_MAJORITY: case G_AND3: case G_OR3: case G_AND4: case G_OR4:
+            if (!multi) throw std::invalid_argument("EvalBinGate: multi-input gates take a ciphertext vector");
             break;
         default:
-            throw std::invalid_argument("EvalBinGate: only 2-input gates (OR AND NOR NAND XOR XNOR) are supported");
+            throw std::invalid_argument("EvalBinGate: unsupported gate");
     }
     if (count > 0x7fffffffull) throw std::invalid_argument("batch too large");
+    if (p < 2 || 2 * p > p_.q) throw std::invalid_argument("plaintext modulus out of range");
     GateArgs g{};
     g.count = (uint32_t)count;
     g.n = p_.n;
     g.N = p_.N;
     g.q = p_.q;
     g.qKS = p_.qKS;
-    // BootstrapGateCore window (binfhe-base-scheme.cpp:535-553), p = 4
+    // BootstrapGateCore window (binfhe-base-scheme.cpp:535-553); Q2p = Q/(2p) + 1 (:555-556)
     const uint64_t q = p_.q, qHalf = q >> 1, Q = p_.Q;
     const uint64_t q1 = p_.gate_const(gate), q2 = (q1 + qHalf) % q;
     const bool swap = q1 >= q2;
     g.lb = (uint32_t)(swap ? q2 : q1);
     g.ub = (uint32_t)(swap ? q1 : q2);
-    const uint64_t Q2p = Q / 8 + 1, Q2pNeg = Q - Q2p;
+    const uint64_t Q2p = Q / (2 * p) + 1, Q2pNeg = Q - Q2p;
     g.lv = (uint32_t)(swap ? Q2p : Q2pNeg);
     g.uv = (uint32_t)(swap ? Q2pNeg : Q2p);
     g.factor = (uint32_t)(p_.N / qHalf);
-    g.b_const = (uint32_t)((Q >> 3) + 1);
+    // b = Q/8 + 1 for 2-input gates (:118, hardcoded p = 4), Q/(2p) + 1 for ctvector gates (:162)
+    g.b_const = (uint32_t)(multi ? Q / (2 * p) + 1 : (Q >> 3) + 1);
     g.xor_double = (gate == G_XOR || gate == G_XNOR || gate == G_XOR_FAST || gate == G_XNOR_FAST) ? 1 : 0;
     g.msb_out = 1;
     g.gbits = p_.gBits;
@@ -228,9 +234,27 @@ void Engine::ensure_host_stage(size_t count) {
     if (d_io_) FHE_HIP_CHECK(hipFree(d_io_));
     d_io_ = nullptr;
     hcap_ = 0;
-    const size_t words = count * (2 * (size_t)p_.n + 2 + p_.N + 1);
+    const size_t words = count * (4 * ((size_t)p_.n + 1) + p_.N + 1);
     FHE_HIP_CHECK(hipMalloc(&d_io_, words * 8));
     hcap_ = count;
+}
+
+void Engine::prep_device(const GateArgs& g, const GateInputs& in, size_t offset, hipStream_t s) {
+    if (p_.method == M_GINX) {
+        FHE_HIP_CHECK(launch_prep_ginx(g, in, d_idx_ + offset * p_.n, d_tvb_ + offset, s));
+    } else {
+        FHE_HIP_CHECK(launch_prep_lmk(g, in, d_logGen_, d_scratch_ + offset * (p_.N + p_.n), d_ops_ + offset * maxops_,
+                                      d_nops_ + offset, d_tvb_ + offset, maxops_, p_.numAutoKeys, s));
+    }
+}
+
+void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
+    if (p_.method == M_GINX) {
+        FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+    } else {
+        FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_bsk_, d_autok_, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
+                                              d_ext_b_, s));
+    }
 }
 
 void Engine::bootstrap_device(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
@@ -241,15 +265,63 @@ void Engine::bootstrap_device(int gate, size_t count, const uint64_t* a1, const 
     if (count == 0) return;
     ensure_work(count);
     FHE_HIP_CHECK(hipSetDevice(device_));
-    if (p_.method == M_GINX) {
-        FHE_HIP_CHECK(launch_prep_ginx(g, a1, b1, a2, b2, d_idx_, d_tvb_, s));
-        FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
-    } else {
-        FHE_HIP_CHECK(launch_prep_lmk(g, a1, b1, a2, b2, d_logGen_, d_scratch_, d_ops_, d_nops_, d_tvb_, maxops_,
-                                      p_.numAutoKeys, s));
-        FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_bsk_, d_autok_, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
-                                              d_ext_b_, s));
+    GateInputs in{{a1, a2, nullptr, nullptr}, {b1, b2, nullptr, nullptr}, 2, 0, 0};
+    prep_device(g, in, 0, s);
+    rotate_device(g, s);
+}
+
+void Engine::eval_gate_multi_device(int gate, size_t count, uint32_t k, const uint64_t* const* a,
+                                    const uint64_t* const* b, uint32_t p, uint64_t* a_out, uint64_t* b_out,
+                                    hipStream_t s) {
+    if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
+    if (k < 2 || k > 4) throw std::invalid_argument("EvalBinGate(ctvector): 2 to 4 ciphertexts");
+    GateArgs g = gate_args(gate, count, p, true);
+    if (count == 0) return;
+    ensure_work(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    GateInputs in{};
+    for (uint32_t j = 0; j < k; ++j) {
+        if (!a[j] || !b[j]) throw std::invalid_argument("null ciphertext array");
+        in.a[j] = a[j];
+        in.b[j] = b[j];
     }
+    in.k = k;
+    g.msb_out = a_out ? 1 : 0;
+    prep_device(g, in, 0, s);
+    rotate_device(g, s);
+    if (a_out) keyswitch_workspace_device(count, a_out, b_out, s);
+}
+
+void Engine::eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1,
+                              const uint64_t* b1, const uint64_t* a2, const uint64_t* b2, uint64_t* a_out,
+                              uint64_t* b_out, hipStream_t s) {
+    if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
+    if (count == 0) return;
+    if (2 * count > 0x7fffffffull) throw std::invalid_argument("batch too large");
+    ensure_work(2 * count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    if (count > ccap_) {
+        FHE_HIP_CHECK(hipStreamSynchronize(s));
+        if (d_l1_) FHE_HIP_CHECK(hipFree(d_l1_));
+        d_l1_ = nullptr;
+        ccap_ = 0;
+        FHE_HIP_CHECK(hipMalloc(&d_l1_, 2 * count * ((size_t)p_.n + 1) * 8));
+        ccap_ = count;
+    }
+    const size_t n = p_.n;
+    uint64_t* l1a = d_l1_;                 // [2 count][n]: NAND(ct0, NOT ct2) | NAND(ct1, ct2)
+    uint64_t* l1b = d_l1_ + 2 * count * n; // [2 count]
+    const GateArgs gh = gate_args(G_NAND, count);
+    GateInputs lo{{a0, a2, nullptr, nullptr}, {b0, b2, nullptr, nullptr}, 2, 2u, p_.q >> 2};  // ct0 + NOT ct2
+    GateInputs hi{{a1, a2, nullptr, nullptr}, {b1, b2, nullptr, nullptr}, 2, 0u, 0u};
+    prep_device(gh, lo, 0, s);
+    prep_device(gh, hi, count, s);
+    rotate_device(gate_args(G_NAND, 2 * count), s);
+    keyswitch_workspace_device(2 * count, l1a, l1b, s);
+    GateInputs top{{l1a, l1a + count * n, nullptr, nullptr}, {l1b, l1b + count, nullptr, nullptr}, 2, 0u, 0u};
+    prep_device(gh, top, 0, s);
+    rotate_device(gh, s);
+    keyswitch_workspace_device(count, a_out, b_out, s);
 }
 
 void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
@@ -337,6 +409,71 @@ void Engine::keyswitch_host(size_t count, const uint64_t* a, const uint64_t* b, 
     GateArgs g = gate_args(G_AND, count);
     FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, 0, dao, dbo, stream_));
     FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * p_.n * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void Engine::stage_inputs(size_t count, uint32_t k, const uint64_t* const* a, const uint64_t* const* b,
+                          const uint64_t** da, const uint64_t** db) {
+    const size_t n = p_.n;
+    uint64_t* cur = d_io_;
+    for (uint32_t j = 0; j < k; ++j) {
+        if (!a[j] || !b[j]) throw std::invalid_argument("null ciphertext array");
+        FHE_HIP_CHECK(hipMemcpyAsync(cur, a[j], count * n * 8, hipMemcpyHostToDevice, stream_));
+        da[j] = cur;
+        cur += count * n;
+        FHE_HIP_CHECK(hipMemcpyAsync(cur, b[j], count * 8, hipMemcpyHostToDevice, stream_));
+        db[j] = cur;
+        cur += count;
+    }
+}
+
+void Engine::eval_gate_multi_host(int gate, size_t count, uint32_t k, const uint64_t* const* a,
+                                  const uint64_t* const* b, uint32_t p, uint64_t* a_out, uint64_t* b_out,
+                                  bool extended) {
+    if (k < 2 || k > 4) throw std::invalid_argument("EvalBinGate(ctvector): 2 to 4 ciphertexts");
+    gate_args(gate, count, p, true);  // validate before any transfer
+    if (count == 0) return;
+    ensure_host_stage(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    const uint64_t* da[4] = {};
+    const uint64_t* db[4] = {};
+    stage_inputs(count, k, a, b, da, db);
+    const size_t n = p_.n, N = p_.N;
+    uint64_t* dao = d_io_ + count * 4 * (n + 1);
+    uint64_t* dbo = dao + count * n;
+    if (!extended) {
+        eval_gate_multi_device(gate, count, k, da, db, p, dao, dbo, stream_);
+        FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * n * 8, hipMemcpyDeviceToHost, stream_));
+        FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+        FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+        return;
+    }
+    eval_gate_multi_device(gate, count, k, da, db, p, nullptr, nullptr, stream_);
+    std::vector<uint32_t> ha(count * N), hb(count);
+    FHE_HIP_CHECK(hipMemcpyAsync(ha.data(), d_ext_a_, count * N * 4, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(hb.data(), d_ext_b_, count * 4, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (size_t i = 0; i < count * N; ++i) a_out[i] = ha[i];
+    for (size_t i = 0; i < count; ++i) b_out[i] = hb[i];
+}
+
+void Engine::eval_cmux_host(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1,
+                            const uint64_t* b1, const uint64_t* a2, const uint64_t* b2, uint64_t* a_out,
+                            uint64_t* b_out) {
+    if (count == 0) return;
+    ensure_host_stage(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    const uint64_t* ha[3] = {a0, a1, a2};
+    const uint64_t* hb[3] = {b0, b1, b2};
+    const uint64_t* da[4] = {};
+    const uint64_t* db[4] = {};
+    stage_inputs(count, 3, ha, hb, da, db);
+    const size_t n = p_.n;
+    uint64_t* dao = d_io_ + count * 4 * (n + 1);
+    uint64_t* dbo = dao + count * n;
+    eval_cmux_device(count, da[0], db[0], da[1], db[1], da[2], db[2], dao, dbo, stream_);
+    FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * n * 8, hipMemcpyDeviceToHost, stream_));
     FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
     FHE_HIP_CHECK(hipStreamSynchronize(stream_));
 }

@@ -59,15 +59,36 @@ public:
     const uint32_t* ext_a() const { return d_ext_a_; }
     const uint32_t* ext_b() const { return d_ext_b_; }
 
+    // EvalBinGate(gate, ctvector) for AND3 / OR3 / AND4 / OR4 / MAJORITY (binfhe-base-scheme.cpp:129-171):
+    // k inputs a[j] [count][n], b[j] [count] (mod q), plaintext modulus p of the inputs
+    void eval_gate_multi_device(int gate, size_t count, uint32_t k, const uint64_t* const* a,
+                                const uint64_t* const* b, uint32_t p, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // EvalBinGate(CMUX, {ct0, ct1, ct2}) = NAND(NAND(ct0, NOT ct2), NAND(ct1, ct2)) (:172-182):
+    // one 2*count-gate NAND level, then one count-gate NAND level
+    void eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
+                          const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+
     // host-buffer convenience entry points (synchronous)
     void eval_gate_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
                         const uint64_t* b2, uint64_t* a_out, uint64_t* b_out);
     void bootstrap_extended_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
                                  const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b);
     void keyswitch_host(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
+    // extended = true returns ctExt ([count][N] mod Q) instead of the switched output
+    void eval_gate_multi_host(int gate, size_t count, uint32_t k, const uint64_t* const* a, const uint64_t* const* b,
+                              uint32_t p, uint64_t* a_out, uint64_t* b_out, bool extended);
+    void eval_cmux_host(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
+                        const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out);
 
 private:
-    GateArgs gate_args(int gate, size_t count) const;
+    // p: plaintext modulus of the bootstrapped ciphertext; multi: AND3..OR4/MAJORITY allowed
+    GateArgs gate_args(int gate, size_t count, uint32_t p = 4, bool multi = false) const;
+    // prep of g.count gates into the workspace slots [offset, offset + g.count)
+    void prep_device(const GateArgs& g, const GateInputs& in, size_t offset, hipStream_t s);
+    // blind rotation of workspace slots [0, g.count)
+    void rotate_device(const GateArgs& g, hipStream_t s);
+    void stage_inputs(size_t count, uint32_t k, const uint64_t* const* a, const uint64_t* const* b,
+                      const uint64_t** da, const uint64_t** db);
     void ensure_work(size_t count);
     void ensure_host_stage(size_t count);
     void build_tables();
@@ -91,7 +112,10 @@ private:
     uint32_t* d_tvb_ = nullptr;
     uint32_t* d_ext_a_ = nullptr;
     uint32_t* d_ext_b_ = nullptr;
-    // staging for host entry points
+    // CMUX: first-level NAND outputs [2 count][n] + [2 count]
+    size_t ccap_ = 0;
+    uint64_t* d_l1_ = nullptr;
+    // staging for host entry points: up to 4 inputs + one ctExt-sized output
     size_t hcap_ = 0;
     uint64_t* d_io_ = nullptr;
 };

@@ -182,8 +182,9 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
 }
 
 void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
-             uint64_t* b) {
+             uint64_t* b, uint32_t ptmod) {
     const uint64_t q = p.q;
+    if (ptmod < 2 || ptmod > q) throw std::invalid_argument("plaintext modulus out of range");
 #pragma omp parallel for schedule(static) if (count > 64)
     for (int64_t g = 0; g < (int64_t)count; ++g) {
         Rng r(seed, T_ENC, (uint64_t)g);
@@ -193,18 +194,21 @@ void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count,
             ag[i] = r.uniform(q);
             acc += (u128)ag[i] * lift(signed_of(sk[i], p.qKS), q);
         }
-        uint64_t m = (uint64_t)(bits[g] & 3) * (q / 4);  // p = 4
+        // b = (m mod p) (q / p) + e + <a, s>   (lwe-pke.cpp:103-128)
+        uint64_t m = ((uint64_t)(uint32_t)bits[g] % ptmod) * (q / ptmod);
         b[g] = (m + lift(r.cbd(), q) + (uint64_t)(acc % q)) % q;
     }
 }
 
-int64_t decrypt(const Params& p, const uint64_t* sk, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod) {
+int64_t decrypt(const Params& p, const uint64_t* sk, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod,
+                uint32_t ptmod) {
     u128 acc = 0;
     for (uint32_t i = 0; i < len; ++i) acc += (u128)(a[i] % mod) * lift(signed_of(sk[i], p.qKS), mod);
     uint64_t inner = (uint64_t)(acc % mod);
     uint64_t r = submod(b % mod, inner, mod);
-    r = addmod(r, mod / 8, mod);  // Round(4/q x) = q/8 + Floor(4/q x)   (lwe-pke.cpp:214-219)
-    return (int64_t)((4 * r) / mod);
+    // Round(p/q x) = Floor(p/q (x + q/(2p)))   (lwe-pke.cpp:209-215)
+    r = addmod(r, mod / (2 * (uint64_t)ptmod), mod);
+    return (int64_t)(((u128)ptmod * r) / mod);
 }
 
 }  // namespace fhe_amd

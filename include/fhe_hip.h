@@ -69,7 +69,8 @@ void* fhe_hip_ntt_plan_stream(fhe_hip_ntt_plan* plan);
 /* Parameter sets / methods / gates use the reference's enum values         */
 /*   (src/binfhe/include/binfhe-constants.h:49-126):                         */
 /*   paramset TOY=0, STD128=3, STD128_LMKCDEY=21; method GINX=2, LMKCDEY=3;   */
-/*   gate OR=0 AND=1 NOR=2 NAND=3 XOR=4 XNOR=5 XOR_FAST=11 XNOR_FAST=12.      */
+/*   gate OR=0 AND=1 NOR=2 NAND=3 XOR=4 XNOR=5 MAJORITY=6 AND3=7 OR3=8       */
+/*   AND4=9 OR4=10 XOR_FAST=11 XNOR_FAST=12 CMUX=13.                        */
 /* Raw key layouts (u64 words, the reference's values):                     */
 /*   GINX bsk    [n][2 (s=+1, s=-1)][digitsG2][2][N]  EVAL (bit-reversed)   */
 /*               = (*BSkey)[0][0..1][i] (rgsw-acc-cggi.cpp:39-57)           */
@@ -116,6 +117,25 @@ int fhe_hip_keyswitch_workspace_device(fhe_hip_ctx* ctx, size_t count, uint64_t*
 /* EvalBinGate(..., extended = true): ctExt before SwitchCTtoqn, dimension N, mod Q */
 int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
                                   const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b);
+/* EvalBinGate(gate, ctvector, extended) for gate in {MAJORITY, AND3, OR3, AND4, OR4}
+ * (binfhe-base-scheme.cpp:129-171): k (2..4) inputs a_in[j] [count][n], b_in[j] [count]
+ * mod q, summed; ptmod = the inputs' plaintext modulus (GetptModulus of ctvector[0]:
+ * 6 for AND3/OR3, 8 for AND4/OR4, 4 for MAJORITY in the reference's tests).
+ * extended = 0: outputs [count][n] mod q; extended = 1: ctExt [count][N] mod Q. */
+int fhe_hip_eval_gate_multi_batch(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32_t ptmod, size_t count,
+                                  const uint64_t* const* a_in, const uint64_t* const* b_in, uint64_t* a_out,
+                                  uint64_t* b_out, int extended);
+int fhe_hip_eval_gate_multi_batch_device(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32_t ptmod, size_t count,
+                                         const uint64_t* const* d_a_in, const uint64_t* const* d_b_in,
+                                         uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* EvalBinGate(CMUX, {ct0, ct1, ct2}) = NAND(NAND(ct0, NOT ct2), NAND(ct1, ct2)), i.e. ct2 ? ct1 : ct0
+ * (binfhe-base-scheme.cpp:172-182; EvalCMUXBatch, batch.cpp:212-249, passes {sel, true, false}). */
+int fhe_hip_eval_cmux_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a0, const uint64_t* b0,
+                            const uint64_t* a1, const uint64_t* b1, const uint64_t* a2, const uint64_t* b2,
+                            uint64_t* a_out, uint64_t* b_out);
+int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a0, const uint64_t* d_b0,
+                                   const uint64_t* d_a1, const uint64_t* d_b1, const uint64_t* d_a2,
+                                   const uint64_t* d_b2, uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
 /* LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372): (N, qKS) -> (n, qKS) */
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
                             uint64_t* b_out);
@@ -146,6 +166,11 @@ int fhe_hip_encrypt(int paramset, int method, const uint64_t* sk, const int* bit
                     uint64_t* a, uint64_t* b);
 int fhe_hip_decrypt(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b, size_t count,
                     uint32_t len, uint64_t mod, int64_t* out);
+/* the same with an explicit plaintext modulus (Encrypt/Decrypt(..., p), lwe-pke.cpp:103-128, 181-226) */
+int fhe_hip_encrypt_ptmod(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
+                          uint32_t ptmod, uint64_t* a, uint64_t* b);
+int fhe_hip_decrypt_ptmod(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b,
+                          size_t count, uint32_t len, uint64_t mod, uint32_t ptmod, int64_t* out);
 
 /* ------------------------------------------------------------------------ */
 /* Device memory (Backend::Allocate/Free/CopyToDevice/CopyToHost/Synchronize, */

@@ -445,25 +445,19 @@ static void eval_acc_lmk(const boot_ctx* c, const uint64_t* bsk, const uint64_t*
     free(idx);
 }
 
-/* EvalBinGate (binfhe-base-scheme.cpp:76-126) + BootstrapGateCore (:525-583) +
- * SwitchCTtoqn (lwe-pke.cpp:170-178) for one gate. */
-static void eval_gate1(const boot_ctx* c, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB, int gate,
-                       const uint64_t* a1, uint64_t b1, const uint64_t* a2, uint64_t b2, uint64_t* a_out,
-                       uint64_t* b_out, int stage, uint64_t* work) {
+/* BootstrapGateCore (binfhe-base-scheme.cpp:525-583) on the combined ciphertext (a, b) mod q,
+ * then Transpose/iNTT/b fix-up (:110-121 / :155-163) and SwitchCTtoqn (lwe-pke.cpp:170-178).
+ * tv_p: plaintext modulus of the bootstrapped ct (test vector Q/(2p)+1, :555-556);
+ * b_p: the b constant Q/(2 b_p)+1 (b_p = 4 for 2-input gates, :118; the ctvector p, :162). */
+static void eval_core(const boot_ctx* c, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB, int gate,
+                      const uint64_t* a, uint64_t b, uint64_t tv_p, uint64_t b_p, uint64_t* a_out, uint64_t* b_out,
+                      int stage, uint64_t* work) {
     const tfo_params* p = c->p; const uint32_t n = p->n, N = p->N; const uint64_t q = p->q, Q = p->Q;
-    uint64_t* a = work; work += N;
-    uint64_t b = (b1 + b2) % q;
-    for (uint32_t i = 0; i < n; ++i) a[i] = (a1[i] + a2[i]) % q;
-    if (gate == 4 || gate == 5 || gate == 11 || gate == 12) {  /* XOR/XNOR: 2(ct1+ct2) */
-        for (uint32_t i = 0; i < n; ++i) a[i] = (2 * a[i]) % q;
-        b = (2 * b) % q;
-    }
-    /* BootstrapGateCore */
     const uint64_t qHalf = q >> 1;
     uint64_t q1 = gate_const((uint32_t)q, gate), q2 = (q1 + qHalf) % q;
     int swap = q1 >= q2;
     uint64_t lb = swap ? q2 : q1, ub = swap ? q1 : q2;
-    uint64_t Q2p = Q / (4 * 2) + 1, Q2pNeg = Q - Q2p;  /* p = 4 */
+    uint64_t Q2p = Q / (tv_p * 2) + 1, Q2pNeg = Q - Q2p;
     uint64_t lv = swap ? Q2p : Q2pNeg, uv = swap ? Q2pNeg : Q2p;
     uint64_t* acc = work; work += 2 * N;
     memset(acc, 0, 2 * N * sizeof(uint64_t));
@@ -481,7 +475,7 @@ static void eval_gate1(const boot_ctx* c, const uint64_t* bsk, const uint64_t* k
     automorphism(p, 2 * N - 1, acc, t0);
     memcpy(acc, t0, N * sizeof(uint64_t));
     ntt_inv(&c->T, acc); ntt_inv(&c->T, acc + N);
-    uint64_t bext = addmod((Q >> 3) + 1, acc[N], Q);
+    uint64_t bext = addmod(Q / (2 * b_p) + 1, acc[N], Q);
     if (stage == 1) {
         memcpy(a_out, acc, N * sizeof(uint64_t));
         *b_out = bext;
@@ -493,6 +487,22 @@ static void eval_gate1(const boot_ctx* c, const uint64_t* bsk, const uint64_t* k
     uint64_t* ks = work + N; uint64_t bks;
     keyswitch1(p, kskA, kskB, ms, bms, ks, &bks);
     tfo_modswitch(p->qKS, q, n, 1, ks, &bks, a_out, b_out);
+    (void)n;
+}
+
+/* EvalBinGate (binfhe-base-scheme.cpp:76-126) for one 2-input gate (inputs with p = 4). */
+static void eval_gate1(const boot_ctx* c, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB, int gate,
+                       const uint64_t* a1, uint64_t b1, const uint64_t* a2, uint64_t b2, uint64_t* a_out,
+                       uint64_t* b_out, int stage, uint64_t* work) {
+    const tfo_params* p = c->p; const uint32_t n = p->n, N = p->N; const uint64_t q = p->q;
+    uint64_t* a = work; work += N;
+    uint64_t b = (b1 + b2) % q;
+    for (uint32_t i = 0; i < n; ++i) a[i] = (a1[i] + a2[i]) % q;
+    if (gate == 4 || gate == 5 || gate == 11 || gate == 12) {  /* XOR/XNOR: 2(ct1+ct2) */
+        for (uint32_t i = 0; i < n; ++i) a[i] = (2 * a[i]) % q;
+        b = (2 * b) % q;
+    }
+    eval_core(c, bsk, kskA, kskB, gate, a, b, 4, 4, a_out, b_out, stage, work);
 }
 
 int tfo_eval_gate_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB, int gate,
@@ -513,8 +523,59 @@ int tfo_eval_gate_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t
     return 0;
 }
 
-/* Decrypt: lwe-pke.cpp:181-226 (p = 4); SwitchModulus: mubintvecnat.cpp:109-122 */
-int64_t tfo_decrypt(const uint64_t* sk, uint64_t skmod, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod) {
+/* EvalBinGate(gate, ctvector) for MAJORITY/AND3/OR3/AND4/OR4 (binfhe-base-scheme.cpp:129-171):
+ * ct = sum of the k inputs mod q, bootstrapped with the inputs' plaintext modulus ptmod. */
+int tfo_eval_gate_multi_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                              int gate, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a_in,
+                              const uint64_t* const* b_in, uint64_t* a_out, uint64_t* b_out, int stage, int nthreads) {
+    if (k < 2 || k > 4 || gate < 6 || gate > 10) return -2;
+    boot_ctx c; boot_ctx_init(&c, p);
+    const uint32_t n = p->n, N = p->N, outLen = stage == 1 ? N : n;
+    const uint64_t q = p->q;
+    const size_t wlen = (size_t)N * (5 + 3 + 2 * c.dG2 + 4);
+    long long g;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(dynamic, 1)
+    for (g = 0; g < (long long)count; ++g) {
+        uint64_t* work = (uint64_t*)malloc(wlen * sizeof(uint64_t));
+        uint64_t* a = work;
+        uint64_t b = 0;
+        for (uint32_t i = 0; i < n; ++i) a[i] = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            for (uint32_t i = 0; i < n; ++i) a[i] = (a[i] + a_in[j][(size_t)g * n + i]) % q;
+            b = (b + b_in[j][g]) % q;
+        }
+        eval_core(&c, bsk, kskA, kskB, gate, a, b, ptmod, ptmod, a_out + (size_t)g * outLen, b_out + g, stage,
+                  work + N);
+        free(work);
+    }
+    boot_ctx_free(&c);
+    return 0;
+}
+
+/* EvalBinGate(CMUX, {ct0, ct1, ct2}) = NAND(NAND(ct0, EvalNOT(ct2)), NAND(ct1, ct2))
+ * (binfhe-base-scheme.cpp:172-182); EvalNOT: (q - a, q/4 - b) (:223-236). */
+int tfo_eval_cmux_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                        size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
+                        const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, int nthreads) {
+    const uint32_t n = p->n;
+    const uint64_t q = p->q;
+    uint64_t* na = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* nb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    uint64_t* l1a = (uint64_t*)malloc(2 * count * n * sizeof(uint64_t));
+    uint64_t* l1b = (uint64_t*)malloc(2 * count * sizeof(uint64_t));
+    for (size_t i = 0; i < count * n; ++i) na[i] = a2[i] == 0 ? 0 : q - a2[i];
+    for (size_t g = 0; g < count; ++g) nb[g] = ((q >> 2) + q - b2[g] % q) % q;
+    tfo_eval_gate_batch(p, bsk, kskA, kskB, 3, count, a0, b0, na, nb, l1a, l1b, 0, nthreads);
+    tfo_eval_gate_batch(p, bsk, kskA, kskB, 3, count, a1, b1, a2, b2, l1a + count * n, l1b + count, 0, nthreads);
+    tfo_eval_gate_batch(p, bsk, kskA, kskB, 3, count, l1a, l1b, l1a + count * n, l1b + count, a_out, b_out, 0,
+                        nthreads);
+    free(na); free(nb); free(l1a); free(l1b);
+    return 0;
+}
+
+/* Decrypt: lwe-pke.cpp:181-226 with plaintext modulus ptmod; SwitchModulus: mubintvecnat.cpp:109-122 */
+int64_t tfo_decrypt_p(const uint64_t* sk, uint64_t skmod, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod,
+                      uint32_t ptmod) {
     uint64_t inner = 0;
     for (uint32_t i = 0; i < len; ++i) {
         uint64_t s = sk[i], sm;
@@ -527,6 +588,10 @@ int64_t tfo_decrypt(const uint64_t* sk, uint64_t skmod, const uint64_t* a, uint6
         inner = addmod(inner, mulmod(a[i], sm, mod), mod);
     }
     uint64_t r = submod(b % mod, inner, mod);
-    r = addmod(r, mod / 8, mod);
-    return (int64_t)((4 * r) / mod);
+    r = addmod(r, mod / (2 * (uint64_t)ptmod), mod);
+    return (int64_t)(((unsigned __int128)ptmod * r) / mod);
+}
+
+int64_t tfo_decrypt(const uint64_t* sk, uint64_t skmod, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod) {
+    return tfo_decrypt_p(sk, skmod, a, b, len, mod, 4);
 }

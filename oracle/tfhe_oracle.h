@@ -58,6 +58,16 @@ int tfo_eval_gate_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t
                         int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
                         const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, int stage, int nthreads);
 
+/* EvalBinGate(gate, ctvector) for MAJORITY=6/AND3=7/OR3=8/AND4=9/OR4=10 (binfhe-base-scheme.cpp:129-171):
+ * k inputs a_in[j][count][n], b_in[j][count] summed mod q; ptmod = their plaintext modulus. */
+int tfo_eval_gate_multi_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                              int gate, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a_in,
+                              const uint64_t* const* b_in, uint64_t* a_out, uint64_t* b_out, int stage, int nthreads);
+/* EvalBinGate(CMUX, {ct0, ct1, ct2}) (binfhe-base-scheme.cpp:172-182) */
+int tfo_eval_cmux_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                        size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
+                        const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, int nthreads);
+
 /* LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:41-46, 254-261) */
 void tfo_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, size_t count, const uint64_t* a, const uint64_t* b,
                    uint64_t* a_out, uint64_t* b_out);
@@ -66,6 +76,9 @@ void tfo_keyswitch(const tfo_params* p, const uint64_t* kskA, const uint64_t* ks
                    const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
 /* LWEEncryptionScheme::Decrypt (lwe-pke.cpp:181-226) with p = 4; sk stored mod qKS */
 int64_t tfo_decrypt(const uint64_t* sk, uint64_t skmod, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod);
+/* the same with plaintext modulus ptmod */
+int64_t tfo_decrypt_p(const uint64_t* sk, uint64_t skmod, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod,
+                      uint32_t ptmod);
 
 #ifdef __cplusplus
 }

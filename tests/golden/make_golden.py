@@ -88,9 +88,54 @@ def make_gates(names=("std128", "lmkcdey")):
         print(name, "ok", outs.shape)
 
 
+# multi-input gates (binfhe-base-scheme.cpp:129-187): (gate, k, plaintext modulus) as the
+# reference's UnitTestFHEW.cpp:202-224 uses them; every input combination once
+MULTI = {"MAJORITY": (6, 3, 4), "AND3": (7, 3, 6), "OR3": (8, 3, 6), "AND4": (9, 4, 8), "OR4": (10, 4, 8),
+         "CMUX": (13, 3, 4)}
+
+
+def multi_inputs(ps, m, key_seed):
+    """keys + per gate: bits [2^k][k] (all combinations) and k encrypted input arrays."""
+    from fhe_amd import binfhe as bf
+    keys = bf.keygen(ps, m, key_seed)
+    cases = {}
+    for gi, (gname, (g, k, p)) in enumerate(MULTI.items()):
+        bits = np.array([[(c >> j) & 1 for j in range(k)] for c in range(1 << k)])
+        ins = [bf.encrypt(ps, m, keys.sk, bits[:, j], key_seed + 100 + 8 * gi + j, p) for j in range(k)]
+        cases[gname] = (g, k, p, bits, [x[0] for x in ins], [x[1] for x in ins])
+    return keys, cases
+
+
+def make_multi(names=("std128", "lmkcdey")):
+    for name in names:
+        ps, m = GATE_SETS[name]
+        key_seed = 0xB0070000 + ps
+        keys, cases = multi_inputs(ps, m, key_seed)
+        ref = Ref(ps, m)
+        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        out = {"paramset": ps, "method": m, "key_seed": np.uint64(key_seed),
+               "keys_sha": np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB))}
+        for gname, (g, k, p, bits, A, B) in cases.items():
+            ao, bo = ref.eval_gate_multi(g, A, B, p)
+            out[f"{gname}_out_a"] = ao.astype(np.uint16)
+            out[f"{gname}_out_b"] = bo.astype(np.uint16)
+            out[f"{gname}_bits"] = bits
+            out[f"{gname}_in_sha"] = np.array("".join(sha(x) for x in A + B))
+            if g != 13:   # CMUX ignores `extended` in the reference (it returns the final NAND)
+                ea, eb = ref.eval_gate_multi(g, A, B, p, extended=True)
+                out[f"{gname}_ext_sha"] = np.array(sha(ea) + sha(eb))
+            dec = [ref.decrypt(keys.sk, ao[i], bo[i], ref.q, p) for i in range(len(bo))]
+            out[f"{gname}_dec"] = np.array(dec)
+            print(name, gname, "decrypts:", dec)
+        np.savez_compressed(os.path.join(HERE, f"gates_multi_{name}.npz"), **out)
+        print(name, "multi ok")
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("ntt", "all"):
         make_ntt()
     if what in ("gates", "all"):
         make_gates(sys.argv[2:] or ("std128",))
+    if what in ("multi", "all"):
+        make_multi(sys.argv[2:] or ("std128", "lmkcdey"))

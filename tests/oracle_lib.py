@@ -21,6 +21,15 @@ vp = ctypes.c_void_p
 TOY, STD128, STD128_LMKCDEY = 0, 3, 21
 GINX, LMKCDEY = 2, 3
 GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}
+MAJORITY, AND3, OR3, AND4, OR4, CMUX = 6, 7, 8, 9, 10, 13
+
+
+def _ptrs(arrs):
+    """array of k uint64 pointers (const uint64_t* const*) to the given arrays"""
+    t = (vp * len(arrs))()
+    for j, a in enumerate(arrs):
+        t[j] = _p(a)
+    return t
 
 
 def _p(a):
@@ -113,6 +122,26 @@ class Ref:
                                        _p(b2), _p(ao), _p(bo), ctypes.c_int(int(extended)), ctypes.c_int(nthreads)))
         return ao, bo
 
+    def eval_gate_multi(self, gate, a_list, b_list, ptmod, extended=False, nthreads=0):
+        """EvalBinGate(gate, ctvector, extended) per k-tuple (gate = MAJORITY..OR4 or CMUX)."""
+        cnt = a_list[0].shape[0]
+        L = self.N if extended else self.n
+        ao = np.zeros((cnt, L), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        self._chk(self.L.ref_eval_gate_multi(self.h, ctypes.c_int(gate), ctypes.c_uint32(len(a_list)),
+                                             ctypes.c_uint32(ptmod), ctypes.c_size_t(cnt), _ptrs(a_list),
+                                             _ptrs(b_list), _p(ao), _p(bo), ctypes.c_int(int(extended)),
+                                             ctypes.c_int(nthreads)))
+        return ao, bo
+
+    def decrypt(self, sk, a, b, mod, ptmod=4):
+        r = ctypes.c_int64()
+        self._chk(self.L.ref_decrypt_p(self.h, _p(np.ascontiguousarray(sk, np.uint64)),
+                                       _p(np.ascontiguousarray(a, np.uint64)), ctypes.c_uint64(int(b)),
+                                       ctypes.c_uint32(len(a)), ctypes.c_uint64(mod), ctypes.c_uint32(ptmod),
+                                       ctypes.byref(r)))
+        return r.value
+
     def time_gates(self, gate, a1, b1, a2, b2, nthreads=0):
         cnt = a1.shape[0]
         ao = np.zeros((cnt, self.n), np.uint64)
@@ -137,13 +166,6 @@ class Ref:
         self._chk(self.L.ref_keyswitch(self.h, ctypes.c_size_t(cnt), _p(a), _p(b), _p(ao), _p(bo)))
         return ao, bo
 
-    def decrypt(self, sk, a, b, mod):
-        r = ctypes.c_int64()
-        self._chk(self.L.ref_decrypt(self.h, _p(np.ascontiguousarray(sk, np.uint64)),
-                                     _p(np.ascontiguousarray(a, np.uint64)), ctypes.c_uint64(int(b)),
-                                     ctypes.c_uint32(len(a)), ctypes.c_uint64(mod), ctypes.byref(r)))
-        return r.value
-
 
 class _Params(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint32) for f in
@@ -161,6 +183,9 @@ class Restatement:
         self.L.tfo_root_of_unity.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         self.L.tfo_decrypt.restype = ctypes.c_int64
         self.L.tfo_decrypt.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64]
+        self.L.tfo_decrypt_p.restype = ctypes.c_int64
+        self.L.tfo_decrypt_p.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                         ctypes.c_uint32]
         self.p = None
         if paramset is not None:
             self.p = _Params()
@@ -187,6 +212,27 @@ class Restatement:
                                    ctypes.c_int(stage), ctypes.c_int(nthreads))
         return ao, bo
 
+    def eval_gate_multi(self, bsk, A, B, gate, a_list, b_list, ptmod, stage=0, nthreads=8):
+        cnt = a_list[0].shape[0]
+        L = self.N if stage == 1 else self.n
+        ao = np.zeros((cnt, L), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        rc = self.L.tfo_eval_gate_multi_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_int(gate),
+                                              ctypes.c_uint32(len(a_list)), ctypes.c_uint32(ptmod),
+                                              ctypes.c_size_t(cnt), _ptrs(a_list), _ptrs(b_list), _p(ao), _p(bo),
+                                              ctypes.c_int(stage), ctypes.c_int(nthreads))
+        if rc != 0:
+            raise ValueError("tfo_eval_gate_multi_batch: bad arguments")
+        return ao, bo
+
+    def eval_cmux(self, bsk, A, B, a0, b0, a1, b1, a2, b2, nthreads=8):
+        cnt = a0.shape[0]
+        ao = np.zeros((cnt, self.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        self.L.tfo_eval_cmux_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(cnt), _p(a0), _p(b0),
+                                   _p(a1), _p(b1), _p(a2), _p(b2), _p(ao), _p(bo), ctypes.c_int(nthreads))
+        return ao, bo
+
     def modswitch(self, q_from, q_to, a, b):
         cnt, L = a.shape
         ao = np.zeros_like(a)
@@ -202,7 +248,8 @@ class Restatement:
         self.L.tfo_keyswitch(ctypes.byref(self.p), _p(A), _p(B), ctypes.c_size_t(cnt), _p(a), _p(b), _p(ao), _p(bo))
         return ao, bo
 
-    def decrypt(self, sk, skmod, a, b, mod):
+    def decrypt(self, sk, skmod, a, b, mod, ptmod=4):
         a = np.ascontiguousarray(a, np.uint64)
-        return int(self.L.tfo_decrypt(_p(np.ascontiguousarray(sk, np.uint64)), ctypes.c_uint64(skmod), _p(a),
-                                      ctypes.c_uint64(int(b)), ctypes.c_uint32(len(a)), ctypes.c_uint64(mod)))
+        return int(self.L.tfo_decrypt_p(_p(np.ascontiguousarray(sk, np.uint64)), ctypes.c_uint64(skmod), _p(a),
+                                        ctypes.c_uint64(int(b)), ctypes.c_uint32(len(a)), ctypes.c_uint64(mod),
+                                        ctypes.c_uint32(ptmod)))
