@@ -56,8 +56,10 @@ __global__ void __launch_bounds__(256)
 // staged in LDS once and every gate (one thread) subtracts the slice its digit
 // selects.  KSK gather traffic drops from 3 MB per gate to 12.6 MB per 256
 // gates; accumulation is packed u16 (v_pk_sub_u16: mod 2^16, hence exact mod
-// qKS = 2^14) with two columns per VGPR.  The kernel is bound by the LDS reads
-// (128 B per gate per step); prefetch depth beyond 2 steps measured no gain.
+// qKS = 2^14) with two columns per VGPR.  baseKS = 32 and digitsKS = 3 are
+// compile-time (both STD128 sets); a round covers 4 values of i (12 steps), so
+// the gate's a_i come as one 16-byte load per round, prefetched two rounds
+// ahead (a dependent a_i load per i was the kernel's critical path).
 // Below 4096 gates the per-gate kernel above fills the chip better.
 // ---------------------------------------------------------------------------
 // two independent u16 subtractions (mod 2^16) in one VALU op
@@ -67,40 +69,39 @@ __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
     return r;
 }
 
-constexpr int kKsCols  = 64;         // columns per workgroup (32 packed u32)
-constexpr int kKsRowB  = 144;        // LDS bytes per staged slice (128 + 16 pad: conflict-light b128 reads)
-#ifndef FHE_KS_STEPS
-#define FHE_KS_STEPS 2
-#endif
-constexpr int kKsStep  = FHE_KS_STEPS;  // (i, j) steps per LDS buffer / barrier (= prefetch depth)
-constexpr int kKsParts = 32 * kKsCols * 2 / 16;  // uint4 parts staged per step (32 slices x 128 B)
+constexpr int kKsCols  = 64;                    // columns per workgroup (32 packed u32)
+constexpr int kKsRowB  = kKsCols * 2 + 16;      // LDS bytes per staged slice (+16 pad: conflict-light b128 reads)
+constexpr int kKsParts = 32 * kKsCols * 2 / 16; // 16-byte parts staged per step (32 slices x 128 B)
+constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
+constexpr int kKsDigits = 3, kKsLogBase = 5;    // digitsKS, log2(baseKS)
+constexpr int kKsIPR   = 4;                     // values of i per round
+constexpr int kKsStep  = kKsIPR * kKsDigits;    // (i, j) steps per round / LDS buffer / barrier
 
-// G gates (threads) per workgroup; each thread stages kKsParts / G parts per step
 template <int G>
 __global__ void __launch_bounds__(G)
-    k_keyswitch_tiled(GateArgs g, uint32_t logBase, uint32_t digitsKS, const uint16_t* __restrict__ ksk,
-                      const uint32_t* __restrict__ ms_a, const uint32_t* __restrict__ ms_b, uint32_t q_out,
-                      uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
-    constexpr int P = kKsParts / G;
+    k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
+                      const uint32_t* __restrict__ ms_b, uint32_t q_out, uint64_t* __restrict__ a_out,
+                      uint64_t* __restrict__ b_out) {
+    static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
+    constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
     __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][32 * kKsRowB];
     const uint32_t t = threadIdx.x;
     const uint32_t gate = blockIdx.x * G + t;
     const bool valid = gate < g.count;
     const uint32_t col0 = blockIdx.y * kKsCols;
-    const uint32_t base = 1u << logBase, mask = base - 1;
-    const uint32_t steps = g.N * digitsKS;                 // (i, j) pairs, i-major
-    const uint32_t* ga = ms_a + (size_t)(valid ? gate : 0) * g.N;
+    const uint32_t rounds = g.N / kKsIPR;
+    const uint4* ga4 = reinterpret_cast<const uint4*>(ms_a + (size_t)(valid ? gate : 0) * g.N);
 
-    // staging role: part index x = t + G*r -> slice x / 8, 16-byte part x % 8
-    auto slice_src = [&](uint32_t step, int r) -> const uint4* {
-        const uint32_t x = t + G * r, sd = x >> 3, sp = x & 7;
-        const uint32_t i = step / digitsKS, j = step - i * digitsKS;
-        const size_t row = ((size_t)i * base + sd) * digitsKS + j;
+    // staging role: part x = t + G*r -> slice x / kKsPartsPerSlice, 16-byte part x % kKsPartsPerSlice
+    auto slice_src = [&](uint32_t round, int q, int r) -> const uint4* {
+        const uint32_t x = t + G * r, sd = x / kKsPartsPerSlice, sp = x % kKsPartsPerSlice;
+        const uint32_t i = round * kKsIPR + q / kKsDigits, j = q % kKsDigits;
+        const size_t row = ((size_t)i * (1u << kKsLogBase) + sd) * kKsDigits + j;
         return reinterpret_cast<const uint4*>(ksk + row * 512 + col0) + sp;
     };
     auto slice_dst = [&](unsigned char* sb, int r) -> uint4* {
         const uint32_t x = t + G * r;
-        return reinterpret_cast<uint4*>(sb + (x >> 3) * kKsRowB + (x & 7) * 16);
+        return reinterpret_cast<uint4*>(sb + (x / kKsPartsPerSlice) * kKsRowB + (x % kKsPartsPerSlice) * 16);
     };
 
     uint32_t acc[kKsCols / 2];
@@ -111,40 +112,42 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
     for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
-        for (int r = 0; r < P; ++r) st[q][r] = *slice_src(q, r);
-    uint32_t aval = valid ? ga[0] : 0;
-
-    auto consume = [&](const unsigned char* sb, uint32_t step) {
-        const uint32_t i = step / digitsKS, j = step - i * digitsKS;
-        if (j == 0 && valid) aval = ga[i];
-        const uint32_t dig = (aval >> (logBase * j)) & mask;
-        const uint4* src = reinterpret_cast<const uint4*>(sb + dig * kKsRowB);
-#pragma unroll
-        for (int k = 0; k < kKsCols / 8; ++k) {
-            const uint4 w = src[k];
-            acc[4 * k + 0] = pk_sub_u16(acc[4 * k + 0], w.x);
-            acc[4 * k + 1] = pk_sub_u16(acc[4 * k + 1], w.y);
-            acc[4 * k + 2] = pk_sub_u16(acc[4 * k + 2], w.z);
-            acc[4 * k + 3] = pk_sub_u16(acc[4 * k + 3], w.w);
-        }
-    };
+        for (int r = 0; r < P; ++r) st[q][r] = *slice_src(0, q, r);
+    uint4 a0 = ga4[0], a1 = ga4[rounds > 1 ? 1 : 0], a2 = ga4[rounds > 2 ? 2 : 0];
 
     // one barrier per round: buffer buf is rewritten two rounds later, after every thread
     // has passed the next round's barrier (and so finished consuming it)
-    for (uint32_t s0 = 0, buf = 0; s0 < steps; s0 += kKsStep, buf ^= 1) {
+    for (uint32_t rd = 0, buf = 0; rd < rounds; ++rd, buf ^= 1) {
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
-            for (int r = 0; r < P; ++r) *slice_dst(s_buf[buf][q], r) = st[q][r];
+            for (int r = 0; r < P; ++r)
+                if (kKsParts >= G || (int)t < kKsParts) *slice_dst(s_buf[buf][q], r) = st[q][r];
         __syncthreads();
-        if (s0 + kKsStep < steps) {
+        if (rd + 1 < rounds) {
 #pragma unroll
             for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
-                for (int r = 0; r < P; ++r) st[q][r] = *slice_src(s0 + kKsStep + q, r);
+                for (int r = 0; r < P; ++r) st[q][r] = *slice_src(rd + 1, q, r);
         }
+        const uint4 av = a0;
+        a0 = a1;
+        a1 = a2;
+        if (rd + 3 < rounds) a2 = ga4[rd + 3];
+        const uint32_t as[kKsIPR] = {av.x, av.y, av.z, av.w};
 #pragma unroll
-        for (int q = 0; q < kKsStep; ++q) consume(s_buf[buf][q], s0 + q);
+        for (int q = 0; q < kKsStep; ++q) {
+            const uint32_t dig = (as[q / kKsDigits] >> (kKsLogBase * (q % kKsDigits))) & ((1u << kKsLogBase) - 1);
+            const uint4* src = reinterpret_cast<const uint4*>(s_buf[buf][q] + dig * kKsRowB);
+#pragma unroll
+            for (int k = 0; k < kKsCols / 8; ++k) {
+                const uint4 w = src[k];
+                acc[4 * k + 0] = pk_sub_u16(acc[4 * k + 0], w.x);
+                acc[4 * k + 1] = pk_sub_u16(acc[4 * k + 1], w.y);
+                acc[4 * k + 2] = pk_sub_u16(acc[4 * k + 2], w.z);
+                acc[4 * k + 3] = pk_sub_u16(acc[4 * k + 3], w.w);
+            }
+        }
     }
     if (!valid) return;
     const uint32_t qm = g.qKS - 1;
@@ -176,17 +179,15 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
 #endif
     int tile = FHE_KS_TILE;
     if (tile == 0) tile = g.count >= 4096 ? 256 : 1;  // tiles need >= 16 x 8 workgroups to pay
-    if (tile > 1 && (baseKS != 32 || (g.N * digitsKS) % kKsStep)) tile = 1;
-    const uint32_t ytiles = 512 / kKsCols;
-    switch (tile) {
-        case 256:
-            hipLaunchKernelGGL(k_keyswitch_tiled<256>, dim3((g.count + 255) / 256, ytiles), dim3(256), 0, s, g,
-                               logBase, digitsKS, ksk, ms_a, ms_b, q_out, a_out, b_out);
-            break;
-        default:
-            hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(256), 0, s, g, logBase, digitsKS,
-                               reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
-    }    return hipGetLastError();
+    if (tile > 1 && (logBase != (uint32_t)kKsLogBase || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
+    if (tile > 1) {
+        hipLaunchKernelGGL(k_keyswitch_tiled<256>, dim3((g.count + 255) / 256, 512 / kKsCols), dim3(256), 0, s, g,
+                           ksk, ms_a, ms_b, q_out, a_out, b_out);
+    } else {
+        hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(256), 0, s, g, logBase, digitsKS,
+                           reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
+    }
+    return hipGetLastError();
 }
 
 }  // namespace fhe_amd
