@@ -11,6 +11,8 @@
 #include "arith.h"
 #include "boot.h"
 
+#include <type_traits>
+
 namespace fhe_amd {
 
 __global__ void __launch_bounds__(256)
@@ -74,7 +76,13 @@ constexpr int kKsRowB  = kKsCols * 2 + 16;      // LDS bytes per staged slice (+
 constexpr int kKsParts = 32 * kKsCols * 2 / 16; // 16-byte parts staged per step (32 slices x 128 B)
 constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
 constexpr int kKsDigits = 3, kKsLogBase = 5;    // digitsKS, log2(baseKS)
-constexpr int kKsIPR   = 4;                     // values of i per round
+#ifndef FHE_KS_IPR
+#define FHE_KS_IPR 4
+#endif
+#ifndef FHE_KS_G
+#define FHE_KS_G 256
+#endif
+constexpr int kKsIPR   = FHE_KS_IPR;            // values of i per round (4: one uint4 of a_i)
 constexpr int kKsStep  = kKsIPR * kKsDigits;    // (i, j) steps per round / LDS buffer / barrier
 
 template <int G>
@@ -90,7 +98,9 @@ __global__ void __launch_bounds__(G)
     const bool valid = gate < g.count;
     const uint32_t col0 = blockIdx.y * kKsCols;
     const uint32_t rounds = g.N / kKsIPR;
-    const uint4* ga4 = reinterpret_cast<const uint4*>(ms_a + (size_t)(valid ? gate : 0) * g.N);
+    using AV = typename std::conditional<kKsIPR == 4, uint4, uint2>::type;
+    static_assert(kKsIPR == 4 || kKsIPR == 2, "a_i vector width");
+    const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N);
 
     // staging role: part x = t + G*r -> slice x / kKsPartsPerSlice, 16-byte part x % kKsPartsPerSlice
     auto slice_src = [&](uint32_t round, int q, int r) -> const uint4* {
@@ -113,7 +123,7 @@ __global__ void __launch_bounds__(G)
     for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
         for (int r = 0; r < P; ++r) st[q][r] = *slice_src(0, q, r);
-    uint4 a0 = ga4[0], a1 = ga4[rounds > 1 ? 1 : 0], a2 = ga4[rounds > 2 ? 2 : 0];
+    AV a0 = ga4[0], a1 = ga4[rounds > 1 ? 1 : 0], a2 = ga4[rounds > 2 ? 2 : 0];
 
     // one barrier per round: buffer buf is rewritten two rounds later, after every thread
     // has passed the next round's barrier (and so finished consuming it)
@@ -130,11 +140,11 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
                 for (int r = 0; r < P; ++r) st[q][r] = *slice_src(rd + 1, q, r);
         }
-        const uint4 av = a0;
+        const AV av = a0;
         a0 = a1;
         a1 = a2;
         if (rd + 3 < rounds) a2 = ga4[rd + 3];
-        const uint32_t as[kKsIPR] = {av.x, av.y, av.z, av.w};
+        const uint32_t* as = reinterpret_cast<const uint32_t*>(&av);
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q) {
             const uint32_t dig = (as[q / kKsDigits] >> (kKsLogBase * (q % kKsDigits))) & ((1u << kKsLogBase) - 1);
@@ -181,8 +191,8 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     if (tile == 0) tile = g.count >= 4096 ? 256 : 1;  // tiles need >= 16 x 8 workgroups to pay
     if (tile > 1 && (logBase != (uint32_t)kKsLogBase || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
     if (tile > 1) {
-        hipLaunchKernelGGL(k_keyswitch_tiled<256>, dim3((g.count + 255) / 256, 512 / kKsCols), dim3(256), 0, s, g,
-                           ksk, ms_a, ms_b, q_out, a_out, b_out);
+        hipLaunchKernelGGL(k_keyswitch_tiled<FHE_KS_G>, dim3((g.count + FHE_KS_G - 1) / FHE_KS_G, 512 / kKsCols),
+                           dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, a_out, b_out);
     } else {
         hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(256), 0, s, g, logBase, digitsKS,
                            reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
