@@ -8,19 +8,29 @@ namespace fhe_amd {
 
 // Twiddle/monomial tables for the fused accumulator kernels (all u32,
 // Montgomery form x * 2^32 mod Q).
+// monomial tables (N = 1024, entries padded by one word per 32, 16-byte rounded):
+//   half resolution: psi^(2f) - 1 for f in [0, 2N] at f + (f >> 5)  (exponents a * 2N/ctmod even)
+//   full resolution: psi^e - 1 for e in [0, 4N] at e + (e >> 5)     (ctmod = 2N: any exponent)
+constexpr int kMonoHalfWords = 2176;
+constexpr int kMonoTableWords = 4228;
+
 struct BootTables {
     const uint32_t* twA_fwd;  // Table[0..31]   (uniform stages on bits 9..5)
     const uint32_t* twA_inv;  // TableI[0..31]
     const uint32_t* twB_fwd;  // 992 words: lane-major Table entries of the stages on bits 4..0
     const uint32_t* twB_inv;  // 992 words: same for TableI
-    const uint32_t* mono;     // [2N]: (psi^e - 1) -> EVAL(X^m - 1) = omega_j^m - 1
+    const uint32_t* mono;     // kMonoHalfWords: psi^(2f) - 1 -> EVAL(X^m - 1) = omega_j^m - 1, m even
+    const uint32_t* mono_full;  // kMonoTableWords: psi^e - 1, any m
     uint32_t Q, Q2, qinv;     // qinv = -Q^-1 mod 2^32
     uint32_t ninvR, w1ninvR;  // N^-1 and TableI[1] * N^-1 (Montgomery) for the last iNTT stage
 };
 
 struct GateArgs {
     uint32_t count, n, N, q, qKS;
+    uint32_t ctmod;                   // modulus of the bootstrapped ct's a (q; 2q for BootstrapFunc), power of 2
     uint32_t lb, ub, lv, uv, factor;  // BootstrapGateCore test-vector window (binfhe-base-scheme.cpp:535-567)
+    const uint32_t* tv;               // BootstrapFuncCore test vector (binfhe-base-scheme.cpp:596-608): tv[x] =
+                                      // (Q / fmod) f(x) for x < ctmod; null: gate window lb/ub/lv/uv
     uint32_t b_const;                 // Q/(2p) + 1 (binfhe-base-scheme.cpp:118-120, :162-163)
     uint32_t xor_double;              // XOR/XNOR: 2 (ct1 + ct2)
     uint32_t msb_out;                 // 1: write ctExt mod-switched to qKS; 0: raw ctExt mod Q

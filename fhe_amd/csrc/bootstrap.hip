@@ -266,10 +266,10 @@ FHE_DEV uint32_t combine(const GateInputs& in, const uint64_t* const* v, size_t 
 
 __global__ void k_prep_ginx(GateInputs in, GateArgs g, uint16_t* __restrict__ idx, uint32_t* __restrict__ tvb) {
     const uint64_t total = (uint64_t)g.count * g.n;
-    const uint32_t qm = g.q - 1, mbymod = 2 * g.N / g.q;
+    const uint32_t qm = g.ctmod - 1, mbymod = 2 * g.N / g.ctmod;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t a = combine(in, in.a, t, 0, qm, g.xor_double);
-        idx[t] = (uint16_t)(((g.q - a) & qm) * mbymod);
+        idx[t] = (uint16_t)(((g.ctmod - a) & qm) * mbymod);
     }
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < g.count; t += (uint64_t)gridDim.x * blockDim.x)
         tvb[t] = combine(in, in.b, t, in.boff, qm, g.xor_double);
@@ -279,22 +279,35 @@ __global__ void k_prep_ginx(GateInputs in, GateArgs g, uint16_t* __restrict__ id
 // fused blind rotation, 4 gates (waves) per 256-thread workgroup
 // ---------------------------------------------------------------------------
 constexpr int kWaves = 4;
-constexpr int kMonoWords = 2176;  // 2N+1 entries padded by one word per 32, rounded to 16 B
-constexpr size_t kBootLds = (size_t)(992 * 2 + kMonoWords + kWaves * 2 * kTile) * 4;
+constexpr size_t boot_lds(bool full) {
+    return (size_t)(992 * 2 + (full ? kMonoTableWords : kMonoHalfWords) + kWaves * 2 * kTile) * 4;
+}
 
+// MFULL: full-resolution monomial table (ciphertext modulus 2N, any exponent); otherwise the
+// half-resolution table (even exponents: every gate), where slots r and r ^ 1 share a monomial
+// and the compiler drops half of the table reads.
+template <bool MFULL>
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
                         const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_twBf = sm;
     uint32_t* s_twBi = sm + 992;
+    // the dynamic LDS size and the tile region follow the table (launch_blind_rotate_ginx)
+    constexpr bool mfull = MFULL;
     uint32_t* s_mono = sm + 1984;
-    uint32_t* s_tile = sm + 1984 + kMonoWords;
+    uint32_t* s_tile = sm + 1984 + (mfull ? kMonoTableWords : kMonoHalfWords);
     for (int i = threadIdx.x; i < 992; i += 256) {
         s_twBf[i] = T.twB_fwd[i];
         s_twBi[i] = T.twB_inv[i];
     }
-    for (int i = threadIdx.x; i < kMonoWords; i += 256) s_mono[i] = T.mono[i];
+    {
+        const uint32_t* src = mfull ? T.mono_full : T.mono;
+        const int words     = mfull ? kMonoTableWords : kMonoHalfWords;
+        for (int i = threadIdx.x; i < words; i += 256) s_mono[i] = src[i];
+    }
+    constexpr uint32_t msh = mfull ? 0u : 1u, emask = mfull ? 2047u : 1023u, umask = mfull ? 31u : 15u;
+    constexpr uint32_t eper = mfull ? 4096u : 2048u;
     __syncthreads();
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
@@ -307,14 +320,14 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[32];
     {
-        const uint32_t b = tvb[gate], qm = g.q - 1;
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             const uint32_t x = (uint32_t)(r << 5) | l;
             uint32_t v       = 0;
             if (h == 1 && x % g.factor == 0) {
-                const uint32_t bx = (b - x / g.factor) & qm;
-                v                 = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v                 = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             acc[r] = v;
         }
@@ -374,14 +387,16 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
         //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
         //     out so that each load instruction reads 1 KiB contiguous.
-        // monomial addressing: a = 2a' (factor 2N/q = 2), slot exponent e = a (2 brv(x) + 1) mod 2N
-        // = 2 f with f = a'(2 brv5(l) + 1) + 64 ((a' brv5(r)) mod 16): lane part fl + uniform part.
-        // s_mono holds M[2f mod 2N] at f + (f >> 5) for f in [0, 2N] (padded: few bank conflicts).
-        const uint32_t ah = a >> 1;
-        const uint32_t fl = (ah * lbase) & 1023;
-        const uint32_t Pp = fl + (fl >> 5);                    // f1 = fl + 64u  -> pos = Pp + 66u
-        const uint32_t gl = 2048 - fl;
-        const uint32_t Pn = gl + (gl >> 5);                    // f2 = gl - 64u  -> pos = Pn - 66u
+        // monomial addressing: slot x = (l << 5) | r evaluates at psi^(2 brv(x) + 1), so X^a maps to
+        // psi^e with e = a (2 brv(x) + 1) = a (2 brv5(l) + 1) + 64 (a brv5(r) mod 32)  (mod 2N):
+        // a per-lane part plus a wave-uniform multiple of 64.  Half-resolution table (a = 2a'):
+        // f = e / 2 = a' (2 brv5(l) + 1) + 64 ((a' brv5(r)) mod 16) (mod N), entry f at f + (f >> 5);
+        // full table: e itself.  64 k in (half or full) index space moves a position by 66 k.
+        const uint32_t as = a >> msh;
+        const uint32_t el = (as * lbase) & emask;
+        const uint32_t Pp = el + (el >> 5);                    // index el + 64k       -> Pp + 66k
+        const uint32_t gl = eper - el;
+        const uint32_t Pn = gl + (gl >> 5);                    // index eper - el - 64k -> Pn - 66k
 #if FHE_KEY_PF > 0
 #pragma unroll
         for (int k = 0; k < FHE_KEY_PF; ++k)
@@ -430,7 +445,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                               (uint64_t)D2 * (e ? KN(2).y : KN(2).x) + (uint64_t)D3 * (e ? KN(3).y : KN(3).x);
                 const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
-                const uint32_t u  = __builtin_amdgcn_readfirstlane((ah * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & 15) * 66;
+                const uint32_t u  = __builtin_amdgcn_readfirstlane((as * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & umask) * 66;
 #if defined(FHE_ABL) && (FHE_ABL & 2)
                 const uint64_t S  = (uint64_t)t1 * (Pp + u) + (uint64_t)t2 * (Pn - u);  // ablation: no monomial reads
 #else
@@ -485,8 +500,12 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
-    hipLaunchKernelGGL(k_blind_rotate_ginx, dim3(blocks), dim3(256), kBootLds, s, g, t,
-                       reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
+    if (g.ctmod == 2 * g.N)
+        hipLaunchKernelGGL(k_blind_rotate_ginx<true>, dim3(blocks), dim3(256), boot_lds(true), s, g, t,
+                           reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_ginx<false>, dim3(blocks), dim3(256), boot_lds(false), s, g, t,
+                           reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
     return hipGetLastError();
 }
 
@@ -505,7 +524,7 @@ __global__ void k_prep_lmk(GateInputs in, GateArgs g, const int16_t* __restrict_
                            uint32_t maxops, uint32_t numAutoKeys) {
     const uint32_t gate = blockIdx.x * blockDim.x + threadIdx.x;
     if (gate >= g.count) return;
-    const uint32_t N = g.N, M = 2 * N, Nh = N / 2, n = g.n, qm = g.q - 1;
+    const uint32_t N = g.N, M = 2 * N, Nh = N / 2, n = g.n, qm = g.ctmod - 1;
     uint16_t* end    = scratch + (size_t)gate * (N + n);  // per position: counts -> bucket ends
     uint16_t* sorted = end + N;
     for (uint32_t p = 0; p < N; ++p) end[p] = 0;
@@ -609,14 +628,14 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 
     uint32_t acc[32];
     {
-        const uint32_t b = tvb[gate], qm = g.q - 1;
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             const uint32_t x = (uint32_t)(r << 5) | l;
             uint32_t v       = 0;
             if (h == 1 && x % g.factor == 0) {
-                const uint32_t bx = (b - x / g.factor) & qm;
-                v                 = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v                 = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             acc[r] = v;
         }

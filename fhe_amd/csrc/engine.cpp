@@ -22,8 +22,6 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
     if (p_.q & (p_.q - 1)) throw std::invalid_argument("device path needs a power-of-two q");
     if (p_.digitsG != 3) throw std::invalid_argument("device path expects digitsG = 3");
-    if (p_.method == M_GINX && ((2 * p_.N / p_.q) & 1))
-        throw std::invalid_argument("GINX device path needs an even 2N/q (monomial table)");
     FHE_HIP_CHECK(hipSetDevice(device_));
     FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     build_tables();
@@ -44,12 +42,13 @@ void Engine::build_tables() {
     const uint64_t Q = p_.Q;
     HostNtt h;
     h.init(p_.N, Q, p_.psi);
-    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2176, 0);
+    std::vector<uint32_t> t(32 + 32 + 992 + 992 + kMonoHalfWords + kMonoTableWords, 0);
     uint32_t* twAf = t.data();
     uint32_t* twAi = twAf + 32;
     uint32_t* twBf = twAi + 32;
     uint32_t* twBi = twBf + 992;
     uint32_t* mono = twBi + 992;
+    uint32_t* monoF = mono + kMonoHalfWords;
     for (int i = 0; i < 32; ++i) {
         twAf[i] = to_mont(h.tab[i], Q);
         twAi[i] = to_mont(h.tabI[i], Q);
@@ -64,15 +63,21 @@ void Engine::build_tables() {
                 twBi[off + k * 32 + l] = to_mont(h.tabI[idx], Q);
             }
     }
-    // EVAL(X^m - 1) at slot j = omega_j^m - 1 with omega_j = psi^(2 brv(j) + 1).  GINX exponents
-    // are even (m = a_i * 2N/q), so the table holds psi^(2f) - 1 for f in [0, 2N], entry f at
-    // f + (f >> 5) (bootstrap.hip, monomial addressing).
+    // EVAL(X^m - 1) at slot j = omega_j^m - 1 with omega_j = psi^(2 brv(j) + 1) (bootstrap.hip,
+    // monomial addressing).  Gates (m = a_i * 2N/q, 2N/q = 2) have even exponents: the
+    // half-resolution table psi^(2f) - 1, f in [0, 2N].  BootstrapFunc with ciphertext modulus
+    // 2N has any exponent: the full table psi^e - 1, e in [0, 4N].  Entry k at k + (k >> 5).
     {
         const uint64_t psi2 = mulmod(p_.psi, p_.psi, Q);
         uint64_t x = 1;
         for (uint32_t f = 0; f <= 2 * p_.N; ++f) {
             mono[f + (f >> 5)] = to_mont(submod(x, 1, Q), Q);
             x = mulmod(x, psi2, Q);
+        }
+        x = 1;
+        for (uint32_t e = 0; e <= 4 * p_.N; ++e) {
+            monoF[e + (e >> 5)] = to_mont(submod(x, 1, Q), Q);
+            x = mulmod(x, p_.psi, Q);
         }
     }
     if (p_.method == M_LMKCDEY) {  // rgsw-cryptoparameters.cpp:115-127
@@ -95,7 +100,8 @@ void Engine::build_tables() {
     tabs_.twA_inv = d + 32;
     tabs_.twB_fwd = d + 64;
     tabs_.twB_inv = d + 64 + 992;
-    tabs_.mono = d + 64 + 1984;  // 2176 words
+    tabs_.mono = d + 64 + 1984;                     // kMonoHalfWords words
+    tabs_.mono_full = tabs_.mono + kMonoHalfWords;  // kMonoTableWords words
     tabs_.Q = (uint32_t)Q;
     tabs_.Q2 = (uint32_t)(2 * Q);
     tabs_.qinv = neg_inv32((uint32_t)Q);
@@ -187,6 +193,8 @@ GateArgs Engine::gate_args(int gate, size_t count, uint32_t p, bool multi) const
     g.N = p_.N;
     g.q = p_.q;
     g.qKS = p_.qKS;
+    g.ctmod = p_.q;
+    g.tv = nullptr;
     // BootstrapGateCore window (binfhe-base-scheme.cpp:535-553); Q2p = Q/(2p) + 1 (:555-556)
     const uint64_t q = p_.q, qHalf = q >> 1, Q = p_.Q;
     const uint64_t q1 = p_.gate_const(gate), q2 = (q1 + qHalf) % q;
