@@ -66,8 +66,16 @@ def _setup(L):
     L.fhe_hip_eval_cmux_batch.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]
     L.fhe_hip_eval_cmux_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.fhe_hip_encrypt_ptmod.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, ctypes.c_uint32, vp, vp]
+    L.fhe_hip_encrypt_mod.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, ctypes.c_uint32, u64, vp, vp]
     L.fhe_hip_decrypt_ptmod.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, sz, ctypes.c_uint32, u64,
                                         ctypes.c_uint32, vp]
+    L.fhe_hip_eval_func_batch.argtypes = [vp, sz, vp, vp, u64, vp, sz, vp, vp]
+    L.fhe_hip_eval_func_batch_device.argtypes = [vp, sz, vp, vp, u64, vp, sz, vp, vp, vp]
+    L.fhe_hip_eval_floor_batch.argtypes = [vp, sz, vp, vp, u64, ctypes.c_uint32, vp, vp]
+    L.fhe_hip_eval_sign_batch.argtypes = [vp, sz, vp, vp, u64, ctypes.c_int, vp, vp]
+    L.fhe_hip_eval_decomp_parts.argtypes = [vp, u64, vp]
+    L.fhe_hip_eval_decomp_batch.argtypes = [vp, sz, vp, vp, u64, vp, vp]
+    L.fhe_hip_bootstrap_func_batch.argtypes = [vp, sz, vp, vp, ctypes.c_uint32, vp, u64, vp, vp]
     L.fhe_hip_multi_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.fhe_hip_multi_destroy.argtypes = [vp]
     L.fhe_hip_multi_destroy.restype = None
@@ -130,13 +138,14 @@ def keygen(paramset, method, seed):
     return KeySet(sk, bsk, A, B)
 
 
-def encrypt(paramset, method, sk, bits, seed, p=4):
-    """LWE encryptions of `bits` (messages mod p) under sk, mod q (lwe-pke.cpp:103-128)."""
+def encrypt(paramset, method, sk, bits, seed, p=4, mod=0):
+    """LWE encryptions of `bits` (messages mod p) under sk, modulo `mod` (0: q) (lwe-pke.cpp:103-128)."""
     P = params(paramset, method)
     bits = np.ascontiguousarray(bits, dtype=np.int32)
     a = np.zeros((len(bits), P.n), np.uint64)
     b = np.zeros(len(bits), np.uint64)
-    check(L().fhe_hip_encrypt_ptmod(paramset, method, ptr(_u64(sk)), ptr(bits), len(bits), seed, p, ptr(a), ptr(b)))
+    check(L().fhe_hip_encrypt_mod(paramset, method, ptr(_u64(sk)), ptr(bits), len(bits), seed, p, mod, ptr(a),
+                                  ptr(b)))
     return a, b
 
 
@@ -247,6 +256,44 @@ class GateEngine:
         check(L().fhe_hip_eval_cmux_batch_device(self._h, count, vp(d_a0), vp(d_b0), vp(d_a1), vp(d_b1), vp(d_a2),
                                                  vp(d_b2), vp(d_ao), vp(d_bo), vp(stream) if stream else None))
 
+    # ---- functional bootstrapping (binfhe-base-scheme.cpp:241-521) ----
+    def _fb_out(self, b, parts=1):
+        cnt = len(b)
+        return np.zeros((parts, cnt, self.params.n), np.uint64), np.zeros((parts, cnt), np.uint64)
+
+    def eval_func(self, a, b, q_in, lut):
+        a, b, lut = _u64(a), _u64(b), _u64(lut)
+        ao, bo = self._fb_out(b)
+        check(L().fhe_hip_eval_func_batch(self._h, len(b), ptr(a), ptr(b), q_in, ptr(lut), len(lut), ptr(ao), ptr(bo)))
+        return ao[0], bo[0]
+
+    def eval_floor(self, a, b, mod, roundbits=0):
+        a, b = _u64(a), _u64(b)
+        ao, bo = self._fb_out(b)
+        check(L().fhe_hip_eval_floor_batch(self._h, len(b), ptr(a), ptr(b), mod, roundbits, ptr(ao), ptr(bo)))
+        return ao[0], bo[0]
+
+    def eval_sign(self, a, b, mod, scheme_switch=False):
+        a, b = _u64(a), _u64(b)
+        ao, bo = self._fb_out(b)
+        check(L().fhe_hip_eval_sign_batch(self._h, len(b), ptr(a), ptr(b), mod, int(scheme_switch), ptr(ao), ptr(bo)))
+        return ao[0], bo[0]
+
+    def eval_decomp(self, a, b, mod):
+        a, b = _u64(a), _u64(b)
+        k = ctypes.c_uint32()
+        check(L().fhe_hip_eval_decomp_parts(self._h, mod, ctypes.byref(k)))
+        ao, bo = self._fb_out(b, k.value)
+        check(L().fhe_hip_eval_decomp_batch(self._h, len(b), ptr(a), ptr(b), mod, ptr(ao), ptr(bo)))
+        return ao, bo
+
+    def bootstrap_func(self, a, b, ctmod, f, fmod):
+        a, b, f = _u64(a), _u64(b), _u64(f)
+        ao, bo = self._fb_out(b)
+        check(L().fhe_hip_bootstrap_func_batch(self._h, len(b), ptr(a), ptr(b), ctmod, ptr(f), fmod, ptr(ao),
+                                               ptr(bo)))
+        return ao[0], bo[0]
+
     def keyswitch(self, a, b):
         a, b = _u64(a), _u64(b)
         cnt = len(b)
@@ -344,13 +391,57 @@ class BinFHEContext:
     def BTKeyLoad(self, bsk, kskA, kskB):
         self.engine.load_keys(bsk, kskA, kskB)
 
-    def Encrypt(self, sk, m, output=None, p=4):
-        """Encrypt(sk, m, SMALL_DIM, p) (binfhecontext.cpp:220-234)"""
-        a, b = encrypt(self.paramset, self.method, sk.s, [int(m)], self._next_seed(), p)
-        return LWECiphertext(a[0], int(b[0]), self.params.q, p)
+    def Encrypt(self, sk, m, output=None, p=4, mod=0):
+        """Encrypt(sk, m, SMALL_DIM, p, mod) (binfhecontext.cpp:220-234)"""
+        a, b = encrypt(self.paramset, self.method, sk.s, [int(m)], self._next_seed(), p, mod)
+        return LWECiphertext(a[0], int(b[0]), mod or self.params.q, p)
 
     def Decrypt(self, sk, ct, p=4):
         return int(decrypt(self.paramset, self.method, sk.s, ct.a[None, :], [ct.b], ct.modulus, p)[0])
+
+    # ---- functional bootstrapping (binfhecontext.cpp:340-392) ----
+    def GetBeta(self):
+        return 128
+
+    def GetMaxPlaintextSpace(self):
+        return self.params.q // (2 * self.GetBeta())
+
+    def GenerateLUTviaFunction(self, f, p):
+        """GenerateLUTviaFunction (binfhecontext.cpp:372-390): lut[i] = (q/p) f(i p / q, p)"""
+        if p & (p - 1):
+            raise FheHipError(-2, "plaintext p not power of two")
+        q = self.params.q
+        lut = []
+        for i in range(q):
+            v = (q // p) * int(f((i * p) // q, p))
+            if v >= q:
+                raise FheHipError(-2, "input function should output in Z_{p_output}")
+            lut.append(v)
+        return np.array(lut, np.uint64)
+
+    def _one(self, ct):
+        return ct.a[None, :], np.array([ct.b], np.uint64)
+
+    def EvalFunc(self, ct, lut):
+        ao, bo = self.engine.eval_func(*self._one(ct), ct.modulus, lut)
+        return LWECiphertext(ao[0], int(bo[0]), ct.modulus, ct.p)
+
+    def EvalFloor(self, ct, roundbits=0):
+        ao, bo = self.engine.eval_floor(*self._one(ct), ct.modulus, roundbits)
+        return LWECiphertext(ao[0], int(bo[0]), ct.modulus, ct.p)
+
+    def EvalSign(self, ct, schemeSwitch=False):
+        ao, bo = self.engine.eval_sign(*self._one(ct), ct.modulus, schemeSwitch)
+        return LWECiphertext(ao[0], int(bo[0]), self.params.q)
+
+    def EvalDecomp(self, ct):
+        ao, bo = self.engine.eval_decomp(*self._one(ct), ct.modulus)
+        mods, mod, q = [], ct.modulus, self.params.q
+        while mod > q:
+            mods.append(q)
+            mod = mod // q * 2 * self.GetBeta()
+        mods.append(mod)
+        return [LWECiphertext(ao[k][0], int(bo[k][0]), mods[k]) for k in range(len(mods))]
 
     def EvalNOT(self, ct):
         """EvalNOT (binfhe-base-scheme.cpp:223-236): (q - a, q/4 - b) mod q"""

@@ -61,10 +61,20 @@ hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_
 hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const void* bsk, const void* autok,
                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
                                    uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
-// KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q) (:254-261), KSK as u16 rows of 512
+// KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out) (:254-261), KSK as u16 rows of 512;
+// q_out = 0: no final switch (output mod qKS)
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
-                            const uint32_t* ms_a, const uint32_t* ms_b, uint32_t q_out, uint64_t* a_out,
+                            const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
                             uint64_t* b_out, hipStream_t s);
+// LWE element-wise operations on [count][len] / [count] u64 arrays (lwe.hip):
+//   reduce: (a, b) mod m (LWECiphertextImpl::SetModulus, lwe-ciphertext.h:116-120)
+//   sub:    x - y mod m, inputs < m (EvalSubEq / EvalSubEq2, lwe-pke.cpp:234-242); outputs may alias
+//   addb:   b = (b + c) mod m, c < m (EvalAddConstEq / EvalSubConstEq as m - c, :230-246)
+hipError_t launch_lwe_reduce(const uint64_t* a, const uint64_t* b, uint64_t* ao, uint64_t* bo, uint64_t m,
+                             uint32_t len, size_t count, hipStream_t s);
+hipError_t launch_lwe_sub(const uint64_t* xa, const uint64_t* xb, const uint64_t* ya, const uint64_t* yb, uint64_t* oa,
+                          uint64_t* ob, uint64_t m, uint32_t len, size_t count, hipStream_t s);
+hipError_t launch_lwe_addb(uint64_t* b, uint64_t c, uint64_t m, size_t count, hipStream_t s);
 // ModSwitch on u64 vectors (lwe-pke.cpp:41-46, 254-261)
 hipError_t launch_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, uint32_t count, const uint64_t* a,
                             const uint64_t* b, uint64_t* a_out, uint64_t* b_out, hipStream_t s);

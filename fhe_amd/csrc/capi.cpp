@@ -321,6 +321,74 @@ int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
     });
 }
 
+// ---- functional bootstrapping ----
+int fhe_hip_eval_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in,
+                            const uint64_t* lut, size_t lut_len, uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !lut || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
+    return guarded([&]() -> int {
+        ctx->eng.fb_host(0, count, a, b, q_in, 0, 0, lut, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_func_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                   uint64_t q_in, const uint64_t* lut, size_t lut_len, uint64_t* d_a_out,
+                                   uint64_t* d_b_out, void* stream) {
+    if (!ctx || !lut || !io_ok(count, d_a, d_b, d_a_out, d_b_out, d_a, d_b))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
+    return guarded([&]() -> int {
+        ctx->eng.eval_func_device(count, d_a, d_b, q_in, lut, d_a_out, d_b_out,
+                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_floor_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
+                             uint32_t roundbits, uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.fb_host(1, count, a, b, mod, 0, roundbits, nullptr, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_sign_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
+                            int scheme_switch, uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.fb_host(2, count, a, b, mod, 0, scheme_switch ? 1u : 0u, nullptr, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_decomp_parts(fhe_hip_ctx* ctx, uint64_t mod, uint32_t* parts) {
+    if (!ctx || !parts) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        *parts = ctx->eng.eval_decomp_parts(mod);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_decomp_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
+                              uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.fb_host(3, count, a, b, mod, 0, 0, nullptr, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_bootstrap_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b,
+                                 uint32_t ctmod, const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out) {
+    if (!ctx || !f || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx->eng.fb_host(4, count, a, b, ctmod, fmod, 0, f, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
                             uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
@@ -431,6 +499,15 @@ int fhe_hip_encrypt_ptmod(int paramset, int method, const uint64_t* sk, const in
     if (!sk || (count && (!bits || !a || !b))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
         encrypt(make_params(paramset, method), sk, bits, count, seed, a, b, ptmod);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_encrypt_mod(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
+                        uint32_t ptmod, uint64_t mod, uint64_t* a, uint64_t* b) {
+    if (!sk || (count && (!bits || !a || !b))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        encrypt(make_params(paramset, method), sk, bits, count, seed, a, b, ptmod, mod);
         return FHE_HIP_OK;
     });
 }

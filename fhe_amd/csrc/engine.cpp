@@ -32,7 +32,7 @@ Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       (void*)d_scratch_})
         if (ptr) (void)hipFree(ptr);
     if (stream_) (void)hipStreamDestroy(stream_);

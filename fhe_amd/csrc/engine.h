@@ -68,6 +68,30 @@ public:
     void eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
                           const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
 
+    // ---- functional bootstrapping (binfhe-base-scheme.cpp:241-521, 589-648); fb.cpp ----
+    // BootstrapFunc: a [count][n] mod ctmod (power of two <= 2N), f[x] = f(x) < fmod for x < ctmod;
+    // output [count][n] mod fmod
+    void bootstrap_func_device(size_t count, const uint64_t* a, const uint64_t* b, uint32_t ctmod,
+                               const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // EvalFunc: inputs / outputs mod q_in (= lut length, power of two)
+    void eval_func_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in, const uint64_t* lut,
+                          uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // EvalFloor: inputs / outputs mod `mod`
+    void eval_floor_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint32_t roundbits,
+                           uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // EvalSign: inputs mod `mod` > q, outputs mod q
+    void eval_sign_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, bool scheme_switch,
+                          uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // EvalDecomp: a_out [parts][count][n], b_out [parts][count]
+    uint32_t eval_decomp_parts(uint64_t mod) const;
+    void eval_decomp_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint64_t* a_out,
+                            uint64_t* b_out, hipStream_t s);
+    // host-buffer versions (synchronous); op: 0 func (arg = q_in, lut), 1 floor (arg = mod, iarg =
+    // roundbits), 2 sign (arg = mod, iarg = scheme_switch), 3 decomp (arg = mod), 4 bootstrap_func
+    // (arg = ctmod, lut = f table, arg2 = fmod)
+    void fb_host(int op, size_t count, const uint64_t* a, const uint64_t* b, uint64_t arg, uint64_t arg2,
+                 uint32_t iarg, const uint64_t* lut, uint64_t* a_out, uint64_t* b_out);
+
     // host-buffer convenience entry points (synchronous)
     void eval_gate_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
                         const uint64_t* b2, uint64_t* a_out, uint64_t* b_out);
@@ -87,6 +111,9 @@ private:
     void prep_device(const GateArgs& g, const GateInputs& in, size_t offset, hipStream_t s);
     // blind rotation of workspace slots [0, g.count)
     void rotate_device(const GateArgs& g, hipStream_t s);
+    void fb_floor(size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint32_t roundbits, uint64_t* a_out,
+                  uint64_t* b_out, uint64_t* w, hipStream_t s);
+    uint64_t* fb_work(size_t count, int cts);
     void stage_inputs(size_t count, uint32_t k, const uint64_t* const* a, const uint64_t* const* b,
                       const uint64_t** da, const uint64_t** db);
     void ensure_work(size_t count);
@@ -115,6 +142,10 @@ private:
     // CMUX: first-level NAND outputs [2 count][n] + [2 count]
     size_t ccap_ = 0;
     uint64_t* d_l1_ = nullptr;
+    // functional bootstrapping: test-vector table [2N] u32 and ciphertext temporaries
+    uint32_t* d_tv_ = nullptr;
+    size_t fbcap_ = 0;
+    uint64_t* d_fb_ = nullptr;
     // staging for host entry points: up to 4 inputs + one ctExt-sized output
     size_t hcap_ = 0;
     uint64_t* d_io_ = nullptr;

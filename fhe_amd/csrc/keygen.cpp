@@ -182,8 +182,8 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
 }
 
 void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
-             uint64_t* b, uint32_t ptmod) {
-    const uint64_t q = p.q;
+             uint64_t* b, uint32_t ptmod, uint64_t mod) {
+    const uint64_t q = mod ? mod : p.q;
     if (ptmod < 2 || ptmod > q) throw std::invalid_argument("plaintext modulus out of range");
 #pragma omp parallel for schedule(static) if (count > 64)
     for (int64_t g = 0; g < (int64_t)count; ++g) {

@@ -35,9 +35,10 @@ struct KeySet {
 
 void keygen_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& sk);
 void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed, KeySet& out);
-// LWEEncryptionScheme::Encrypt / Decrypt (lwe-pke.cpp:103-128, 181-226) with plaintext modulus ptmod
+// LWEEncryptionScheme::Encrypt / Decrypt (lwe-pke.cpp:103-128, 181-226) with plaintext modulus
+// ptmod and ciphertext modulus mod (0: q)
 void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
-             uint64_t* b, uint32_t ptmod = 4);
+             uint64_t* b, uint32_t ptmod = 4, uint64_t mod = 0);
 int64_t decrypt(const Params& p, const uint64_t* sk, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod,
                 uint32_t ptmod = 4);
 

@@ -15,9 +15,18 @@
 
 namespace fhe_amd {
 
+namespace {
+// RoundqQ(v, q_out, qKS) = floor(0.5 + v q_out / qKS) mod q_out (lwe-pke.cpp:41-46) as the exact
+// integer floor((2 v q_out + qKS) / (2 qKS)) mod q_out: qKS is a power of two, so the double
+// expression is exact (v q_out < 2^14 2^32 < 2^53) and so is this one.
+FHE_DEV uint64_t mod_switch_up(uint64_t v, uint32_t qKS, uint64_t q_out) {
+    return ((2 * v * q_out + qKS) / (2 * (uint64_t)qKS)) % q_out;
+}
+}  // namespace
+
 __global__ void __launch_bounds__(256)
     k_keyswitch(GateArgs g, uint32_t logBase, uint32_t digitsKS, const uint32_t* __restrict__ ksk,
-                const uint32_t* __restrict__ ms_a, const uint32_t* __restrict__ ms_b, uint32_t q_out,
+                const uint32_t* __restrict__ ms_a, const uint32_t* __restrict__ ms_b, uint64_t q_out,
                 uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
     __shared__ uint32_t s_a[1024];
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
@@ -39,11 +48,11 @@ __global__ void __launch_bounds__(256)
     const uint32_t qm = g.qKS - 1;
     const uint32_t c0 = 2 * t, c1 = 2 * t + 1;
     const uint32_t b  = ms_b[gate];
-    uint32_t v0 = ((c0 == g.n ? b : 0u) - lo) & qm;
-    uint32_t v1 = ((c1 == g.n ? b : 0u) - hi) & qm;
-    if (q_out) {  // ModSwitch qKS -> q: floor((2 v q + qKS) / (2 qKS)) mod q (exact, see bootstrap.hip)
-        v0 = ((2 * v0 * q_out + g.qKS) / (2 * g.qKS)) % q_out;
-        v1 = ((2 * v1 * q_out + g.qKS) / (2 * g.qKS)) % q_out;
+    uint64_t v0 = ((c0 == g.n ? b : 0u) - lo) & qm;
+    uint64_t v1 = ((c1 == g.n ? b : 0u) - hi) & qm;
+    if (q_out) {  // ModSwitch qKS -> q_out
+        v0 = mod_switch_up(v0, g.qKS, q_out);
+        v1 = mod_switch_up(v1, g.qKS, q_out);
     }
     uint64_t* oa = a_out + (size_t)gate * g.n;
     if (c0 < g.n) oa[c0] = v0;
@@ -88,7 +97,7 @@ constexpr int kKsStep  = kKsIPR * kKsDigits;    // (i, j) steps per round / LDS 
 template <int G>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
-                      const uint32_t* __restrict__ ms_b, uint32_t q_out, uint64_t* __restrict__ a_out,
+                      const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                       uint64_t* __restrict__ b_out) {
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
@@ -169,8 +178,8 @@ __global__ void __launch_bounds__(G)
         for (int h = 0; h < 2; ++h) {
             const uint32_t c = col0 + 2 * k + h;
             const uint32_t neg = h ? (acc[k] >> 16) : (acc[k] & 0xffffu);  // -sum mod 2^16
-            uint32_t v = ((c == g.n ? b : 0u) + neg) & qm;
-            if (q_out) v = ((2 * v * q_out + g.qKS) / (2 * g.qKS)) % q_out;  // ModSwitch qKS -> q
+            uint64_t v = ((c == g.n ? b : 0u) + neg) & qm;
+            if (q_out) v = mod_switch_up(v, g.qKS, q_out);  // ModSwitch qKS -> q_out
             if (c < g.n) oa[c] = v;
             else if (c == g.n) b_out[gate] = v;
         }
@@ -178,7 +187,7 @@ __global__ void __launch_bounds__(G)
 }
 
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
-                            const uint32_t* ms_a, const uint32_t* ms_b, uint32_t q_out, uint64_t* a_out,
+                            const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
                             uint64_t* b_out, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (baseKS & (baseKS - 1)) return hipErrorInvalidValue;

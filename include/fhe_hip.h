@@ -136,6 +136,33 @@ int fhe_hip_eval_cmux_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a0, 
 int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a0, const uint64_t* d_b0,
                                    const uint64_t* d_a1, const uint64_t* d_b1, const uint64_t* d_a2,
                                    const uint64_t* d_b2, uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* ---- functional bootstrapping (binfhe-base-scheme.cpp:241-521, 589-648) ----
+ * Batches of `count` LWE ciphertexts a[count][n], b[count] under the context's keys; beta = 128
+ * (BinFHEContext::GetBeta).  Moduli are powers of two.
+ * EvalFunc (binfhecontext.cpp:340-344): inputs/outputs mod q_in; lut[lut_len = q_in] as from
+ *   GenerateLUTviaFunction; negacyclic / periodic / arbitrary LUTs as checkInputFunction
+ *   classifies them (arbitrary needs q_in <= N). */
+int fhe_hip_eval_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in,
+                            const uint64_t* lut, size_t lut_len, uint64_t* a_out, uint64_t* b_out);
+int fhe_hip_eval_func_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                   uint64_t q_in, const uint64_t* lut, size_t lut_len, uint64_t* d_a_out,
+                                   uint64_t* d_b_out, void* stream);
+/* EvalFloor (binfhecontext.cpp:346-357): inputs/outputs mod `mod` (<= 2^31) */
+int fhe_hip_eval_floor_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
+                             uint32_t roundbits, uint64_t* a_out, uint64_t* b_out);
+/* EvalSign (binfhecontext.cpp:359-364): inputs mod `mod` (q < mod <= 2^31), outputs mod q */
+int fhe_hip_eval_sign_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
+                            int scheme_switch, uint64_t* a_out, uint64_t* b_out);
+/* EvalDecomp (binfhecontext.cpp:366-370): *parts ciphertexts per input; a_out [parts][count][n],
+ * b_out [parts][count]; parts - 1 of them mod q, the last one mod its own reduced modulus */
+int fhe_hip_eval_decomp_parts(fhe_hip_ctx* ctx, uint64_t mod, uint32_t* parts);
+int fhe_hip_eval_decomp_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
+                              uint64_t* a_out, uint64_t* b_out);
+/* BootstrapFunc (binfhe-base-scheme.cpp:617-642): a mod ctmod (<= 2N), f[ctmod] with f(x) <= fmod,
+ * outputs mod fmod (<= 2^40) */
+int fhe_hip_bootstrap_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b,
+                                 uint32_t ctmod, const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out);
+
 /* LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372): (N, qKS) -> (n, qKS) */
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
                             uint64_t* b_out);
@@ -169,6 +196,9 @@ int fhe_hip_decrypt(int paramset, int method, const uint64_t* sk, const uint64_t
 /* the same with an explicit plaintext modulus (Encrypt/Decrypt(..., p), lwe-pke.cpp:103-128, 181-226) */
 int fhe_hip_encrypt_ptmod(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
                           uint32_t ptmod, uint64_t* a, uint64_t* b);
+/* ... and an explicit ciphertext modulus mod (Encrypt(sk, m, SMALL_DIM, p, mod), binfhecontext.cpp:220-234) */
+int fhe_hip_encrypt_mod(int paramset, int method, const uint64_t* sk, const int* bits, size_t count, uint64_t seed,
+                        uint32_t ptmod, uint64_t mod, uint64_t* a, uint64_t* b);
 int fhe_hip_decrypt_ptmod(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b,
                           size_t count, uint32_t len, uint64_t mod, uint32_t ptmod, int64_t* out);
 

@@ -378,12 +378,14 @@ void tfo_keyswitch(const tfo_params* p, const uint64_t* kskA, const uint64_t* ks
 }
 
 /* EvalAcc GINX: rgsw-acc-cggi.cpp:59-68 */
-static void eval_acc_cggi(const boot_ctx* c, const uint64_t* bsk, const uint64_t* a, uint64_t* acc, uint64_t* work) {
+/* ctmod: modulus of a (q for gates; BootstrapFunc may use 2q), rgsw-acc-cggi.cpp:61-66 */
+static void eval_acc_cggi(const boot_ctx* c, const uint64_t* bsk, const uint64_t* a, uint64_t ctmod, uint64_t* acc,
+                          uint64_t* work) {
     const tfo_params* p = c->p; const uint32_t N = p->N;
     const size_t rg = (size_t)c->dG2 * 2 * N;    /* one RGSW */
-    const uint64_t MbyMod = 2 * N / p->q;
+    const uint64_t MbyMod = 2 * N / ctmod;
     for (uint32_t i = 0; i < p->n; ++i) {
-        uint64_t ai = (p->q - a[i] % p->q) % p->q;
+        uint64_t ai = (ctmod - a[i] % ctmod) % ctmod;
         add_to_acc_cggi(c, bsk + (size_t)i * 2 * rg, bsk + ((size_t)i * 2 + 1) * rg, (uint32_t)(ai * MbyMod), acc, work);
     }
 }
@@ -468,7 +470,7 @@ static void eval_core(const boot_ctx* c, const uint64_t* bsk, const uint64_t* ks
         bb = submod(bb, 1, q);
     }
     ntt_fwd(&c->T, acc + N);
-    if (p->method == TFO_GINX) eval_acc_cggi(c, bsk, a, acc, work);
+    if (p->method == TFO_GINX) eval_acc_cggi(c, bsk, a, q, acc, work);
     else eval_acc_lmk(c, bsk, a, acc, work);
     /* Transpose acc0 (automorphism 2N-1), iNTT both */
     uint64_t* t0 = work;
@@ -570,6 +572,256 @@ int tfo_eval_cmux_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t
     tfo_eval_gate_batch(p, bsk, kskA, kskB, 3, count, l1a, l1b, l1a + count * n, l1b + count, a_out, b_out, 0,
                         nthreads);
     free(na); free(nb); free(l1a); free(l1b);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Functional bootstrapping (binfhe-base-scheme.cpp:241-521, 589-648)                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* BootstrapFunc for one ciphertext (a mod ctmod, b): BootstrapFuncCore (:592-614) with the test
+ * vector m[j * 2N/ctmod] = tv[(b - j) mod ctmod] (tv[x] = (Q / fmod) f(x, ctmod, fmod)), EvalAcc,
+ * Transpose / iNTT, ctExt = (acc0, acc1[0]), ModSwitch(qKS), KeySwitch, ModSwitch(fmod) (:617-642). */
+static void bootstrap_func1(const boot_ctx* c, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                            const uint64_t* a, uint64_t b, uint64_t ctmod, const uint64_t* tv, uint64_t fmod,
+                            uint64_t* a_out, uint64_t* b_out, uint64_t* work) {
+    const tfo_params* p = c->p; const uint32_t n = p->n, N = p->N; const uint64_t Q = p->Q;
+    uint64_t* acc = work; work += 2 * N;
+    memset(acc, 0, 2 * N * sizeof(uint64_t));
+    const uint64_t factor = 2 * N / ctmod;
+    b %= ctmod;
+    for (uint64_t j = 0; j < (ctmod >> 1); ++j) acc[N + j * factor] = tv[(b + ctmod - j) % ctmod];
+    ntt_fwd(&c->T, acc + N);
+    if (p->method == TFO_GINX) eval_acc_cggi(c, bsk, a, ctmod, acc, work);
+    else eval_acc_lmk(c, bsk, a, acc, work);
+    uint64_t* t0 = work;
+    automorphism(p, 2 * N - 1, acc, t0);
+    memcpy(acc, t0, N * sizeof(uint64_t));
+    ntt_inv(&c->T, acc); ntt_inv(&c->T, acc + N);
+    uint64_t bext = acc[N];
+    uint64_t* ms = work; uint64_t bms;
+    tfo_modswitch(Q, p->qKS, N, 1, acc, &bext, ms, &bms);
+    uint64_t* ks = work + N; uint64_t bks;
+    keyswitch1(p, kskA, kskB, ms, bms, ks, &bks);
+    tfo_modswitch(p->qKS, fmod, n, 1, ks, &bks, a_out, b_out);
+    (void)Q;
+}
+
+int tfo_bootstrap_func_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                             size_t count, const uint64_t* a, const uint64_t* b, uint64_t ctmod, const uint64_t* tv,
+                             uint64_t fmod, uint64_t* a_out, uint64_t* b_out, int nthreads) {
+    if (ctmod < 2 || (ctmod & (ctmod - 1)) || ctmod > 2ull * p->N) return -2;
+    boot_ctx c; boot_ctx_init(&c, p);
+    const uint32_t n = p->n, N = p->N;
+    const size_t wlen = (size_t)N * (4 + 3 + 2 * c.dG2 + 4);
+    long long g;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(dynamic, 1)
+    for (g = 0; g < (long long)count; ++g) {
+        uint64_t* work = (uint64_t*)malloc(wlen * sizeof(uint64_t));
+        bootstrap_func1(&c, bsk, kskA, kskB, a + (size_t)g * n, b[g], ctmod, tv, fmod, a_out + (size_t)g * n,
+                        b_out + g, work);
+        free(work);
+    }
+    boot_ctx_free(&c);
+    return 0;
+}
+
+/* test-vector functions f(x, q = ctmod, Q = fmod) of the reference's lambdas */
+enum { TV_LUT, TV_LUT_ANTI, TV_HALF, TV_FLOOR2, TV_SIGN, TV_SIGN_SS };
+static void make_tv(const tfo_params* p, int kind, const uint64_t* lut, uint64_t lutlen, uint64_t q, uint64_t fmod,
+                    uint64_t* tv) {
+    const uint64_t scale = p->Q / fmod;
+    for (uint64_t x = 0; x < q; ++x) {
+        uint64_t f = 0;
+        switch (kind) {
+            case TV_LUT: f = lut[x]; break;                                             /* :254-256 */
+            case TV_LUT_ANTI: f = x < (q >> 1) ? lut[x % lutlen] : fmod - lut[(x - q / 2) % lutlen]; break; /* :302-307, 324-329 */
+            case TV_HALF: f = x < (q >> 1) ? fmod - (q >> 2) : (q >> 2); break;         /* f0 / f1 :285-290 */
+            case TV_FLOOR2:                                                             /* f2 :361-368 */
+                f = x < (q >> 2) ? fmod - (q >> 1) - x : (x < 3 * (q >> 2) ? x : fmod + (q >> 1) - x); break;
+            case TV_SIGN: f = x < q / 2 ? fmod / 4 : fmod - fmod / 4; break;            /* f3 :413-416 */
+            case TV_SIGN_SS: f = x < q / 2 ? fmod - fmod / 4 : fmod / 4; break;         /* :421-424 */
+        }
+        tv[x] = scale * f;
+    }
+}
+
+static void lwe_addb(uint64_t* b, size_t count, uint64_t c, uint64_t m) {   /* EvalAddConstEq :230-232 */
+    for (size_t g = 0; g < count; ++g) b[g] = (b[g] + c % m) % m;
+}
+static void lwe_subb(uint64_t* b, size_t count, uint64_t c, uint64_t m) {   /* EvalSubConstEq :244-246 */
+    for (size_t g = 0; g < count; ++g) b[g] = (b[g] % m + m - c % m) % m;
+}
+static void lwe_reduce(const uint64_t* a, const uint64_t* b, uint64_t* ao, uint64_t* bo, size_t count, uint32_t n,
+                       uint64_t m) {                                          /* SetModulus, lwe-ciphertext.h:116-120 */
+    for (size_t i = 0; i < count * n; ++i) ao[i] = a[i] % m;
+    for (size_t g = 0; g < count; ++g) bo[g] = b[g] % m;
+}
+/* out = x - y mod m (EvalSubEq :234-237 / EvalSubEq2 :239-242); out may alias x or y */
+static void lwe_sub(const uint64_t* xa, const uint64_t* xb, const uint64_t* ya, const uint64_t* yb, uint64_t* oa,
+                    uint64_t* ob, size_t count, uint32_t n, uint64_t m) {
+    for (size_t i = 0; i < count * n; ++i) oa[i] = (xa[i] % m + m - ya[i] % m) % m;
+    for (size_t g = 0; g < count; ++g) ob[g] = (xb[g] % m + m - yb[g] % m) % m;
+}
+
+static int lut_property(const uint64_t* lut, uint64_t len, uint64_t mod) {  /* checkInputFunction, binfhe-base-scheme.h:245-260 */
+    uint64_t mid = len / 2;
+    if (lut[0] == mod - lut[mid]) {
+        for (uint64_t i = 1; i < mid; ++i) if (lut[i] != mod - lut[mid + i]) return 2;
+        return 0;
+    }
+    if (lut[0] == lut[mid]) {
+        for (uint64_t i = 1; i < mid; ++i) if (lut[i] != lut[mid + i]) return 2;
+        return 1;
+    }
+    return 2;
+}
+
+#define BETA 128u  /* BinFHEContext::GetBeta, binfhecontext.h:445-447 */
+
+/* EvalFunc (binfhe-base-scheme.cpp:241-337): inputs mod q_in (= LUT length), outputs mod q_in */
+int tfo_eval_func_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                        size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in, const uint64_t* lut,
+                        uint64_t* a_out, uint64_t* b_out, int nthreads) {
+    const uint32_t n = p->n;
+    const int prop = lut_property(lut, q_in, q_in);
+    uint64_t* tv = (uint64_t*)malloc(4 * (size_t)p->N * sizeof(uint64_t));
+    uint64_t* ta = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* tb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    uint64_t* ua = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* ub = (uint64_t*)malloc(count * sizeof(uint64_t));
+    int rc = 0;
+    memcpy(ta, a, count * n * sizeof(uint64_t));
+    memcpy(tb, b, count * sizeof(uint64_t));
+    if (prop == 0) {                                   /* negacyclic: one bootstrap :253-259 */
+        lwe_addb(tb, count, BETA, q_in);
+        make_tv(p, TV_LUT, lut, q_in, q_in, q_in, tv);
+        tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ta, tb, q_in, tv, q_in, a_out, b_out, nthreads);
+    } else if (prop == 2) {                            /* arbitrary :261-312 */
+        if (q_in > p->N) { rc = -2; goto done; }
+        const uint64_t dq = q_in << 1;
+        /* ct1 = ct with a's modulus raised to dq (values unchanged); ct2 = ct1 + beta (mod dq) */
+        memcpy(ua, ta, count * n * sizeof(uint64_t));
+        memcpy(ub, tb, count * sizeof(uint64_t));
+        lwe_addb(ub, count, BETA, dq);
+        make_tv(p, TV_HALF, NULL, 0, dq, dq, tv);
+        uint64_t* ca = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+        uint64_t* cb = (uint64_t*)malloc(count * sizeof(uint64_t));
+        tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ua, ub, dq, tv, dq, ca, cb, nthreads);  /* ct3 */
+        lwe_sub(ta, tb, ca, cb, ca, cb, count, n, dq);  /* EvalSubEq2(ct1, ct3): ct3 = ct1 - ct3 */
+        lwe_addb(cb, count, BETA, dq);
+        lwe_subb(cb, count, q_in >> 1, dq);
+        make_tv(p, TV_LUT_ANTI, lut, q_in, dq, dq, tv);   /* LUT2 = LUT || LUT */
+        tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ca, cb, dq, tv, dq, ua, ub, nthreads);  /* ct4 */
+        lwe_reduce(ua, ub, a_out, b_out, count, n, q_in);   /* ct4->SetModulus(q) */
+        free(ca); free(cb);
+    } else {                                           /* periodic :315-337 */
+        lwe_addb(tb, count, BETA, q_in);
+        make_tv(p, TV_HALF, NULL, 0, q_in, q_in, tv);
+        tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ta, tb, q_in, tv, q_in, ua, ub, nthreads);  /* ct2 */
+        lwe_sub(a, b, ua, ub, ua, ub, count, n, q_in);    /* EvalSubEq2(ct, ct2) */
+        lwe_addb(ub, count, BETA, q_in);
+        lwe_subb(ub, count, q_in >> 2, q_in);
+        make_tv(p, TV_LUT_ANTI, lut, q_in, q_in, q_in, tv);
+        tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ua, ub, q_in, tv, q_in, a_out, b_out, nthreads);
+    }
+done:
+    free(tv); free(ta); free(tb); free(ua); free(ub);
+    return rc;
+}
+
+/* EvalFloor (:340-378): ct mod `mod` in and out; q' = q (roundbits = 0) or beta 2^(roundbits+1) */
+static void eval_floor(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                       size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint32_t roundbits,
+                       uint64_t* a_out, uint64_t* b_out, int nthreads) {
+    const uint32_t n = p->n;
+    const uint64_t qq = roundbits == 0 ? p->q : (uint64_t)BETA << (roundbits + 1);
+    uint64_t* tv = (uint64_t*)malloc(4 * (size_t)p->N * sizeof(uint64_t));
+    uint64_t* ra = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* rb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    uint64_t* sa = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* sb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    memcpy(a_out, a, count * n * sizeof(uint64_t));   /* ct1 = ct + beta */
+    memcpy(b_out, b, count * sizeof(uint64_t));
+    lwe_addb(b_out, count, BETA, mod);
+    lwe_reduce(a_out, b_out, ra, rb, count, n, qq);    /* ct1Modq */
+    make_tv(p, TV_HALF, NULL, 0, qq, mod, tv);
+    tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ra, rb, qq, tv, mod, sa, sb, nthreads);   /* ct2 */
+    lwe_sub(a_out, b_out, sa, sb, a_out, b_out, count, n, mod);                                   /* ct1 -= ct2 */
+    lwe_reduce(a_out, b_out, ra, rb, count, n, qq);    /* ct2Modq */
+    make_tv(p, TV_FLOOR2, NULL, 0, qq, mod, tv);
+    tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ra, rb, qq, tv, mod, sa, sb, nthreads);   /* ct3 */
+    lwe_sub(a_out, b_out, sa, sb, a_out, b_out, count, n, mod);                                   /* ct1 -= ct3 */
+    free(tv); free(ra); free(rb); free(sa); free(sb);
+}
+
+int tfo_eval_floor_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                         size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint32_t roundbits,
+                         uint64_t* a_out, uint64_t* b_out, int nthreads) {
+    eval_floor(p, bsk, kskA, kskB, count, a, b, mod, roundbits, a_out, b_out, nthreads);
+    return 0;
+}
+
+/* EvalSign (:381-449) with one bootstrapping key (no dynamic base change): outputs mod q */
+int tfo_eval_sign_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                        size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, int scheme_switch,
+                        uint64_t* a_out, uint64_t* b_out, int nthreads) {
+    const uint32_t n = p->n;
+    const uint64_t q = p->q;
+    if (mod <= q) return -2;
+    uint64_t* ta = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* tb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    uint64_t* fa = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* fb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    uint64_t* tv = (uint64_t*)malloc(4 * (size_t)p->N * sizeof(uint64_t));
+    memcpy(ta, a, count * n * sizeof(uint64_t));
+    memcpy(tb, b, count * sizeof(uint64_t));
+    while (mod > q) {
+        eval_floor(p, bsk, kskA, kskB, count, ta, tb, mod, 0, fa, fb, nthreads);
+        const uint64_t nmod = (mod << 1) * BETA / q;
+        tfo_modswitch(mod, nmod, n, count, fa, fb, ta, tb);
+        mod = nmod;
+    }
+    lwe_addb(tb, count, BETA, mod);
+    make_tv(p, scheme_switch ? TV_SIGN_SS : TV_SIGN, NULL, 0, mod, q, tv);
+    tfo_bootstrap_func_batch(p, bsk, kskA, kskB, count, ta, tb, mod, tv, q, a_out, b_out, nthreads);
+    if (!scheme_switch) lwe_subb(b_out, count, q >> 2, q);
+    free(ta); free(tb); free(fa); free(fb); free(tv);
+    return 0;
+}
+
+/* number of ciphertexts EvalDecomp returns for an input modulus */
+uint32_t tfo_eval_decomp_parts(const tfo_params* p, uint64_t mod) {
+    uint32_t k = 1;
+    while (mod > p->q) { ++k; mod = mod / p->q * 2 * BETA; }
+    return k;
+}
+
+/* EvalDecomp (:452-518): parts k -> a_out [k][count][n], b_out [k][count]; part i < k-1 is mod q */
+int tfo_eval_decomp_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                          size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint64_t* a_out,
+                          uint64_t* b_out, int nthreads) {
+    const uint32_t n = p->n;
+    const uint64_t q = p->q;
+    if (mod <= q) return -2;
+    uint64_t* ta = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* tb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    uint64_t* fa = (uint64_t*)malloc(count * n * sizeof(uint64_t));
+    uint64_t* fb = (uint64_t*)malloc(count * sizeof(uint64_t));
+    memcpy(ta, a, count * n * sizeof(uint64_t));
+    memcpy(tb, b, count * sizeof(uint64_t));
+    size_t part = 0;
+    while (mod > q) {
+        lwe_reduce(ta, tb, a_out + part * count * n, b_out + part * count, count, n, q);
+        ++part;
+        eval_floor(p, bsk, kskA, kskB, count, ta, tb, mod, 0, fa, fb, nthreads);
+        const uint64_t nmod = mod / q * 2 * BETA;
+        tfo_modswitch(mod, nmod, n, count, fa, fb, ta, tb);
+        mod = nmod;
+    }
+    memcpy(a_out + part * count * n, ta, count * n * sizeof(uint64_t));
+    memcpy(b_out + part * count, tb, count * sizeof(uint64_t));
+    free(ta); free(tb); free(fa); free(fb);
     return 0;
 }
 

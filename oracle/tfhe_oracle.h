@@ -68,6 +68,30 @@ int tfo_eval_cmux_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t
                         size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
                         const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, int nthreads);
 
+/* Functional bootstrapping (binfhe-base-scheme.cpp:241-521, 589-648).
+ * BootstrapFunc: a [count][n] mod ctmod (power of 2, <= 2N), test vector tv[x] = (Q/fmod) f(x) for
+ * x < ctmod, output [count][n] mod fmod. */
+int tfo_bootstrap_func_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                             size_t count, const uint64_t* a, const uint64_t* b, uint64_t ctmod, const uint64_t* tv,
+                             uint64_t fmod, uint64_t* a_out, uint64_t* b_out, int nthreads);
+/* EvalFunc: inputs and outputs mod q_in, lut[q_in] */
+int tfo_eval_func_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                        size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in, const uint64_t* lut,
+                        uint64_t* a_out, uint64_t* b_out, int nthreads);
+/* EvalFloor: inputs and outputs mod `mod` */
+int tfo_eval_floor_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                         size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint32_t roundbits,
+                         uint64_t* a_out, uint64_t* b_out, int nthreads);
+/* EvalSign: inputs mod `mod` > q, outputs mod q */
+int tfo_eval_sign_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                        size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, int scheme_switch,
+                        uint64_t* a_out, uint64_t* b_out, int nthreads);
+/* EvalDecomp: a_out [parts][count][n], b_out [parts][count] */
+uint32_t tfo_eval_decomp_parts(const tfo_params* p, uint64_t mod);
+int tfo_eval_decomp_batch(const tfo_params* p, const uint64_t* bsk, const uint64_t* kskA, const uint64_t* kskB,
+                          size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint64_t* a_out,
+                          uint64_t* b_out, int nthreads);
+
 /* LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:41-46, 254-261) */
 void tfo_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, size_t count, const uint64_t* a, const uint64_t* b,
                    uint64_t* a_out, uint64_t* b_out);

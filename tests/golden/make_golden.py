@@ -131,6 +131,63 @@ def make_multi(names=("std128", "lmkcdey")):
         print(name, "multi ok")
 
 
+# functional bootstrapping (binfhe-base-scheme.cpp:241-521): beta = 128, p = q / 256
+FB_LARGE_MOD = 1 << 14
+
+
+def fb_luts(q, p, N):
+    """LUTs as GenerateLUTviaFunction builds them (binfhecontext.cpp:372-390)"""
+    def lut_of(f):
+        return np.array([(q // p) * f((i * p) // q, p) for i in range(q)], np.uint64)
+    luts = {"neg": lut_of(lambda x, p: 1 if x < p // 2 else p - 1),   # negacyclic
+            "per": lut_of(lambda x, p: x % 2)}                          # periodic
+    if q <= N:
+        luts["cube"] = lut_of(lambda x, p: (x ** 3) % p)                # arbitrary (eval-function.cpp)
+    return luts
+
+
+def fb_inputs(ps, m, key_seed):
+    """keys; small-precision inputs (every m < p twice, mod q, plaintext modulus p) and
+    large-precision inputs (mod 2^14, plaintext modulus P = p 2^14 / q, values around P/2)."""
+    from fhe_amd import binfhe as bf
+    keys = bf.keygen(ps, m, key_seed)
+    P = bf.params(ps, m)
+    q = P.q
+    p = q // 256
+    ms = np.arange(2 * p) % p
+    sa, sb = bf.encrypt(ps, m, keys.sk, ms, key_seed + 300, p)
+    PL = p * (FB_LARGE_MOD // q)
+    xs = np.array([PL // 2 + i - 4 for i in range(8)] + [3, PL - 3, 0, PL // 4])
+    la, lb = bf.encrypt(ps, m, keys.sk, xs, key_seed + 301, PL, FB_LARGE_MOD)
+    return keys, q, p, ms, sa, sb, PL, xs, la, lb
+
+
+def make_fb(names=("std128", "lmkcdey")):
+    for name in names:
+        ps, m = GATE_SETS[name]
+        key_seed = 0xB0070000 + ps
+        keys, q, p, ms, sa, sb, PL, xs, la, lb = fb_inputs(ps, m, key_seed)
+        ref = Ref(ps, m)
+        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        out = {"paramset": ps, "method": m, "key_seed": np.uint64(key_seed), "ms": ms, "xs": xs,
+               "in_sha": np.array(sha(sa) + sha(sb) + sha(la) + sha(lb))}
+        for lname, lut in fb_luts(q, p, ref.N).items():
+            ao, bo = ref.eval_func(sa, sb, q, lut)
+            out[f"func_{lname}_a"], out[f"func_{lname}_b"] = ao.astype(np.uint16), bo.astype(np.uint16)
+        for rb in (0, 1):
+            ao, bo = ref.eval_floor(sa, sb, q, rb)
+            out[f"floor{rb}_a"], out[f"floor{rb}_b"] = ao.astype(np.uint16), bo.astype(np.uint16)
+        ao, bo = ref.eval_floor(la, lb, FB_LARGE_MOD, 0)
+        out["floorL_a"], out["floorL_b"] = ao.astype(np.uint16), bo.astype(np.uint16)
+        for ss in (0, 1):
+            ao, bo = ref.eval_sign(la, lb, FB_LARGE_MOD, bool(ss))
+            out[f"sign{ss}_a"], out[f"sign{ss}_b"] = ao.astype(np.uint16), bo.astype(np.uint16)
+        ao, bo = ref.eval_decomp(la, lb, FB_LARGE_MOD)
+        out["decomp_a"], out["decomp_b"] = ao.astype(np.uint16), bo.astype(np.uint16)
+        np.savez_compressed(os.path.join(HERE, f"fb_{name}.npz"), **out)
+        print(name, "fb ok", sorted(k for k in out if k.endswith("_a")))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("ntt", "all"):
@@ -139,3 +196,7 @@ if __name__ == "__main__":
         make_gates(sys.argv[2:] or ("std128",))
     if what in ("multi", "all"):
         make_multi(sys.argv[2:] or ("std128", "lmkcdey"))
+    if what == "fb":   # one parameter set per process (see tests/test_fb.py)
+        make_fb(sys.argv[2:] or ("std128",))
+    sys.stdout.flush()
+    os._exit(0)   # skip interpreter teardown: two OpenMP runtimes (reference + fhe_amd) in one process

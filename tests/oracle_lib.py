@@ -142,6 +142,37 @@ class Ref:
                                        ctypes.byref(r)))
         return r.value
 
+    # functional bootstrapping through BinFHEContext (binfhecontext.cpp:340-370)
+    def eval_func(self, a, b, ct_mod, lut, nthreads=0):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        lut = np.ascontiguousarray(lut, np.uint64)
+        self._chk(self.L.ref_eval_func(self.h, ctypes.c_size_t(len(b)), _p(a), _p(b), ctypes.c_uint64(ct_mod), _p(lut),
+                                       ctypes.c_size_t(len(lut)), _p(ao), _p(bo), ctypes.c_int(nthreads)))
+        return ao, bo
+
+    def eval_floor(self, a, b, ct_mod, roundbits=0, nthreads=0):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        self._chk(self.L.ref_eval_floor(self.h, ctypes.c_size_t(len(b)), _p(a), _p(b), ctypes.c_uint64(ct_mod),
+                                        ctypes.c_uint32(roundbits), _p(ao), _p(bo), ctypes.c_int(nthreads)))
+        return ao, bo
+
+    def eval_sign(self, a, b, ct_mod, scheme_switch=False):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        self._chk(self.L.ref_eval_sign(self.h, ctypes.c_size_t(len(b)), _p(a), _p(b), ctypes.c_uint64(ct_mod),
+                                       ctypes.c_int(int(scheme_switch)), _p(ao), _p(bo)))
+        return ao, bo
+
+    def eval_decomp(self, a, b, ct_mod, max_parts=16):
+        cnt, n = a.shape
+        ao = np.zeros((max_parts, cnt, n), np.uint64)
+        bo = np.zeros((max_parts, cnt), np.uint64)
+        parts = ctypes.c_size_t()
+        self._chk(self.L.ref_eval_decomp(self.h, ctypes.c_size_t(cnt), _p(a), _p(b), ctypes.c_uint64(ct_mod),
+                                         ctypes.c_size_t(max_parts), _p(ao), _p(bo), ctypes.byref(parts)))
+        k = parts.value
+        return np.ascontiguousarray(ao.reshape(-1)[:k * cnt * n].reshape(k, cnt, n)), np.ascontiguousarray(
+            bo.reshape(-1)[:k * cnt].reshape(k, cnt))
+
     def time_gates(self, gate, a1, b1, a2, b2, nthreads=0):
         cnt = a1.shape[0]
         ao = np.zeros((cnt, self.n), np.uint64)
@@ -231,6 +262,54 @@ class Restatement:
         bo = np.zeros(cnt, np.uint64)
         self.L.tfo_eval_cmux_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(cnt), _p(a0), _p(b0),
                                    _p(a1), _p(b1), _p(a2), _p(b2), _p(ao), _p(bo), ctypes.c_int(nthreads))
+        return ao, bo
+
+    # functional bootstrapping restatement (oracle/tfhe_oracle.c)
+    def bootstrap_func(self, bsk, A, B, a, b, ctmod, tv, fmod, nthreads=8):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        tv = np.ascontiguousarray(tv, np.uint64)
+        rc = self.L.tfo_bootstrap_func_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(len(b)),
+                                             _p(a), _p(b), ctypes.c_uint64(ctmod), _p(tv), ctypes.c_uint64(fmod),
+                                             _p(ao), _p(bo), ctypes.c_int(nthreads))
+        if rc:
+            raise ValueError("tfo_bootstrap_func_batch")
+        return ao, bo
+
+    def eval_func(self, bsk, A, B, a, b, ct_mod, lut, nthreads=8):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        lut = np.ascontiguousarray(lut, np.uint64)
+        rc = self.L.tfo_eval_func_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(len(b)), _p(a),
+                                        _p(b), ctypes.c_uint64(ct_mod), _p(lut), _p(ao), _p(bo), ctypes.c_int(nthreads))
+        if rc:
+            raise ValueError("tfo_eval_func_batch")
+        return ao, bo
+
+    def eval_floor(self, bsk, A, B, a, b, ct_mod, roundbits=0, nthreads=8):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        self.L.tfo_eval_floor_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(len(b)), _p(a),
+                                    _p(b), ctypes.c_uint64(ct_mod), ctypes.c_uint32(roundbits), _p(ao), _p(bo),
+                                    ctypes.c_int(nthreads))
+        return ao, bo
+
+    def eval_sign(self, bsk, A, B, a, b, ct_mod, scheme_switch=False, nthreads=8):
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        rc = self.L.tfo_eval_sign_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(len(b)), _p(a),
+                                        _p(b), ctypes.c_uint64(ct_mod), ctypes.c_int(int(scheme_switch)), _p(ao),
+                                        _p(bo), ctypes.c_int(nthreads))
+        if rc:
+            raise ValueError("tfo_eval_sign_batch")
+        return ao, bo
+
+    def eval_decomp(self, bsk, A, B, a, b, ct_mod, nthreads=8):
+        cnt, n = a.shape
+        self.L.tfo_eval_decomp_parts.restype = ctypes.c_uint32
+        k = self.L.tfo_eval_decomp_parts(ctypes.byref(self.p), ctypes.c_uint64(ct_mod))
+        ao = np.zeros((k, cnt, n), np.uint64)
+        bo = np.zeros((k, cnt), np.uint64)
+        rc = self.L.tfo_eval_decomp_batch(ctypes.byref(self.p), _p(bsk), _p(A), _p(B), ctypes.c_size_t(cnt), _p(a),
+                                          _p(b), ctypes.c_uint64(ct_mod), _p(ao), _p(bo), ctypes.c_int(nthreads))
+        if rc:
+            raise ValueError("tfo_eval_decomp_batch")
         return ao, bo
 
     def modswitch(self, q_from, q_to, a, b):
