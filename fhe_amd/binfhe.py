@@ -22,7 +22,7 @@ import numpy as np
 from ._lib import FheHipError, check, lib, ptr, sz, u64, vp
 
 # reference enum values (src/binfhe/include/binfhe-constants.h:49-126)
-TOY, STD128, STD128_LMKCDEY = 0, 3, 21
+TOY, STD128_AP, STD128, STD128_LMKCDEY = 0, 2, 3, 21
 AP, GINX, LMKCDEY = 1, 2, 3
 OR, AND, NOR, NAND, XOR, XNOR, MAJORITY, AND3, OR3, AND4, OR4, XOR_FAST, XNOR_FAST, CMUX = range(14)
 GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR, "MAJORITY": MAJORITY,

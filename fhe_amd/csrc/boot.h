@@ -58,9 +58,14 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
 hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen, uint16_t* scratch,
                            uint16_t* ops, uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys,
                            hipStream_t s);
+// dm = true: the AP/DM accumulator (rgsw-acc-dm.cpp:62-77) -- an op list of external products only
 hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const void* bsk, const void* autok,
                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
-                                   uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
+                                   uint32_t* ext_a, uint32_t* ext_b, bool dm, hipStream_t s);
+// AP/DM: per-gate op list EXT((i baseR + a0) digitsR + k) over the nonzero base-baseR digits a0 of
+// (q - a_i) mod q (rgsw-acc-dm.cpp:62-77), + test-vector b
+hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops, uint32_t* nops, uint32_t* tvb,
+                          uint32_t maxops, uint32_t baseR, uint32_t digitsR, hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out) (:254-261), KSK as u16 rows of 512;
 // q_out = 0: no final switch (output mod qKS)
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,

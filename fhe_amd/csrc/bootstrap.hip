@@ -605,6 +605,9 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
 }
 }  // namespace
 
+// DM: the AP/DM accumulator runs the same op loop with external products only (AddToAccDM ==
+// AddToAccLMKCDEY, rgsw-acc-dm.cpp:119-145) and no initial automorphism of acc1.
+template <bool DM>
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
@@ -643,7 +646,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #pragma unroll
         for (int r = 0; r < 32; ++r) acc[r] = csub(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), m.Q);
         // acc1 <- acc1(X^(2N-5))   (:99); applied to both halves, acc0 = 0 is invariant
-        automorphism_eval(acc, tile, l, M - 5);
+        if (!DM) automorphism_eval(acc, tile, l, M - 5);
     }
 
     const int32_t sh  = 32 - (int32_t)g.gbits;
@@ -654,8 +657,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     for (uint32_t it = 0; it < cnt; ++it) {
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
         uint32_t dA[32], dB[32];
-        if (!(op & 0x8000u)) {
-            // ---- AddToAccLMKCDEY: acc <- sum_d D_d * ek[i][d]   (acc replaced)
+        if (DM || !(op & 0x8000u)) {
+            // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
             inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
@@ -781,12 +784,49 @@ hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_
 
 hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const void* bsk, const void* autok,
                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
-                                   uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+                                   uint32_t* ext_a, uint32_t* ext_b, bool dm, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
     const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile) * 4;
-    hipLaunchKernelGGL(k_blind_rotate_lmk, dim3(blocks), dim3(256), lds, s, g, t, reinterpret_cast<const uint2*>(bsk),
-                       reinterpret_cast<const uint2*>(autok), ops, nops, maxops, tvb, ext_a, ext_b);
+    if (dm)
+        hipLaunchKernelGGL(k_blind_rotate_lmk<true>, dim3(blocks), dim3(256), lds, s, g, t,
+                           reinterpret_cast<const uint2*>(bsk), reinterpret_cast<const uint2*>(autok), ops, nops,
+                           maxops, tvb, ext_a, ext_b);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_lmk<false>, dim3(blocks), dim3(256), lds, s, g, t,
+                           reinterpret_cast<const uint2*>(bsk), reinterpret_cast<const uint2*>(autok), ops, nops,
+                           maxops, tvb, ext_a, ext_b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// AP/DM prep (rgsw-acc-dm.cpp:62-77): one thread per gate writes its op list
+// ---------------------------------------------------------------------------
+__global__ void k_prep_dm(GateInputs in, GateArgs g, uint16_t* __restrict__ ops, uint32_t* __restrict__ nops,
+                          uint32_t* __restrict__ tvb, uint32_t maxops, uint32_t baseR, uint32_t digitsR) {
+    const uint32_t gate = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gate >= g.count) return;
+    const uint32_t qm = g.q - 1, n = g.n;
+    uint16_t* o = ops + (size_t)gate * maxops;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t aI = (g.q - combine(in, in.a, (size_t)gate * n + i, 0, qm, g.xor_double)) & qm;
+        for (uint32_t d = 0; d < digitsR; ++d, aI /= baseR) {
+            const uint32_t a0 = aI % baseR;
+            if (a0) o[k++] = (uint16_t)((i * baseR + a0) * digitsR + d);
+        }
+    }
+    nops[gate] = k;
+    tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
+}
+
+hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops, uint32_t* nops, uint32_t* tvb,
+                          uint32_t maxops, uint32_t baseR, uint32_t digitsR, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (in.k < 1 || in.k > 4 || (size_t)g.n * digitsR > maxops || (size_t)g.n * baseR * digitsR > 0x8000u)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_prep_dm, dim3((g.count + 63) / 64), dim3(64), 0, s, in, g, ops, nops, tvb, maxops, baseR,
+                       digitsR);
     return hipGetLastError();
 }
 

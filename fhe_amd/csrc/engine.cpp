@@ -119,8 +119,11 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     // component h -- one 512-byte coalesced load per wave-instruction in the kernels.
     //   GINX   raw [n][2][dG2][2][N]                 -> [n][2][dG2][16][64]
     //   LMKCDEY raw [n][dG2][2][N] ++ [nA+1][2][2][N] -> [n][dG2][16][64] ++ [nA+1][2][16][64]
-    const size_t nrgsw = p_.method == M_GINX ? (size_t)n * 2 : (size_t)n;  // RGSW keys of dG2 rows
-    const size_t nauto = p_.method == M_GINX ? 0 : (size_t)p_.numAutoKeys + 1;
+    //   AP     raw [n][baseR][digitsR][dG2][2][N]    -> [n][baseR][digitsR][dG2][16][64]
+    const size_t nrgsw = p_.method == M_GINX ? (size_t)n * 2
+                         : p_.method == M_AP ? (size_t)n * p_.baseR * p_.digitsR
+                                             : (size_t)n;  // RGSW keys of dG2 rows
+    const size_t nauto = p_.method == M_LMKCDEY ? (size_t)p_.numAutoKeys + 1 : 0;
     const uint32_t dA = p_.digitsG - 1;
     std::vector<uint32_t> dev(nrgsw * dG2 * 2 * N + nauto * dA * 2 * N);
     auto pack = [&](const uint64_t* src_key, uint32_t rows, uint32_t* dst_key) {
@@ -224,7 +227,7 @@ void Engine::ensure_work(size_t count) {
     FHE_HIP_CHECK(hipMalloc(&d_tvb_, count * sizeof(uint32_t)));
     FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
     FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
-    if (p_.method == M_LMKCDEY) {
+    if (p_.method == M_LMKCDEY || p_.method == M_AP) {
         for (void* ptr : {(void*)d_ops_, (void*)d_nops_, (void*)d_scratch_})
             if (ptr) FHE_HIP_CHECK(hipFree(ptr));
         d_ops_ = nullptr; d_nops_ = nullptr; d_scratch_ = nullptr;
@@ -250,6 +253,11 @@ void Engine::ensure_host_stage(size_t count) {
 void Engine::prep_device(const GateArgs& g, const GateInputs& in, size_t offset, hipStream_t s) {
     if (p_.method == M_GINX) {
         FHE_HIP_CHECK(launch_prep_ginx(g, in, d_idx_ + offset * p_.n, d_tvb_ + offset, s));
+    } else if (p_.method == M_AP) {
+        if (g.ctmod != p_.q)  // EvalAcc DM reads a_i modulo the parameter q (rgsw-acc-dm.cpp:64-69)
+            throw std::invalid_argument("AP accumulator: ciphertext modulus must be q");
+        FHE_HIP_CHECK(launch_prep_dm(g, in, d_ops_ + offset * maxops_, d_nops_ + offset, d_tvb_ + offset, maxops_,
+                                     p_.baseR, p_.digitsR, s));
     } else {
         FHE_HIP_CHECK(launch_prep_lmk(g, in, d_logGen_, d_scratch_ + offset * (p_.N + p_.n), d_ops_ + offset * maxops_,
                                       d_nops_ + offset, d_tvb_ + offset, maxops_, p_.numAutoKeys, s));
@@ -261,7 +269,7 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
     } else {
         FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_bsk_, d_autok_, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
-                                              d_ext_b_, s));
+                                              d_ext_b_, p_.method == M_AP, s));
     }
 }
 

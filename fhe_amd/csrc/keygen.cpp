@@ -108,6 +108,34 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
                 }
             }
         }
+    } else if (p.method == M_AP) {
+        // KeyGenAcc DM (rgsw-acc-dm.cpp:39-58): key [i][j][k] = KeyGenDM(s_i * j * baseR^k) for
+        // j in [1, baseR), k < digitsR; KeyGenDM (:80-114): +-G on X^mm, mm = (m mod q) * (2N/q)
+        const uint32_t bR = p.baseR, dR = p.digitsR;
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int64_t i = 0; i < (int64_t)n; ++i) {
+            const int64_t s = signed_of(sk[i], p.qKS);
+            std::vector<uint64_t> msg(N);
+            int64_t rk = 1;
+            for (uint32_t k = 0; k < dR; ++k, rk *= bR)
+                for (uint32_t j = 1; j < bR; ++j) {
+                    const int64_t m = s * (int64_t)j * rk;
+                    int64_t mm = (((m % (int64_t)p.q) + p.q) % p.q) * (2 * N / p.q);
+                    bool neg = false;
+                    if (mm >= (int64_t)N) { mm -= N; neg = true; }
+                    const size_t slot = ((size_t)i * bR + j) * dR + k;
+                    Rng r(seed, T_BSK, slot);
+                    uint64_t* key = out.bsk.data() + slot * rg;
+                    for (uint32_t row = 0; row < dG2; ++row) {
+                        std::fill(msg.begin(), msg.end(), 0);
+                        const uint64_t g = p.gpow[(row >> 1) + 1];
+                        msg[mm] = neg ? Q - g : g;
+                        ntt.forward(msg.data());
+                        rgsw_row_pair(key + (size_t)row * 2 * N, key + ((size_t)row * 2 + 1) * N, r, msg.data(),
+                                      row & 1);
+                    }
+                }
+        }
     } else {
 #pragma omp parallel for schedule(dynamic, 4)
         for (int64_t i = 0; i < (int64_t)n; ++i) {

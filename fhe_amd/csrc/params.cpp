@@ -10,6 +10,8 @@ namespace fhe_amd {
 
 size_t Params::bsk_words() const {
     if (method == M_GINX) return (size_t)n * 2 * digitsG2 * 2 * N;
+    // AP: [n][baseR][digitsR][digitsG2][2][N], the j = 0 slots unused (rgsw-acc-dm.cpp:39-58)
+    if (method == M_AP) return (size_t)n * baseR * digitsR * digitsG2 * 2 * N;
     return (size_t)n * digitsG2 * 2 * N + (size_t)(numAutoKeys + 1) * (digitsG - 1) * 2 * N;
 }
 
@@ -38,11 +40,13 @@ Params make_params(int paramset, int method) {
     int kd;
     switch (paramset) {
         case PS_TOY:            bits = 27; cyc = 1024; n = 64;  q = 512;  qks = 0;     bks = 25; bg = 512;  nauto = 9;  kd = KD_UNIFORM_TERNARY; break;
+        case PS_STD128_AP:
         case PS_STD128:         bits = 27; cyc = 2048; n = 503; q = 1024; qks = 16384; bks = 32; bg = 512;  nauto = 10; kd = KD_UNIFORM_TERNARY; break;
         case PS_STD128_LMKCDEY: bits = 28; cyc = 2048; n = 447; q = 2048; qks = 16384; bks = 32; bg = 1024; nauto = 10; kd = KD_GAUSSIAN; break;
-        default: throw std::invalid_argument("unsupported parameter set (TOY, STD128, STD128_LMKCDEY)");
+        default: throw std::invalid_argument("unsupported parameter set (TOY, STD128_AP, STD128, STD128_LMKCDEY)");
     }
-    if (method != M_GINX && method != M_LMKCDEY) throw std::invalid_argument("unsupported method (GINX, LMKCDEY)");
+    if (method != M_GINX && method != M_LMKCDEY && method != M_AP)
+        throw std::invalid_argument("unsupported method (AP, GINX, LMKCDEY)");
     Params p;
     p.paramset = paramset;
     p.method = method;
@@ -59,6 +63,8 @@ Params make_params(int paramset, int method) {
     p.digitsG2 = (p.digitsG - 1) * 2;
     p.numAutoKeys = nauto;
     p.keyDist = kd;
+    p.baseR = 32;  // baseRK column of every row (binfhecontext.cpp:113-159)
+    p.digitsR = (uint32_t)std::ceil(std::log((double)q) / std::log((double)p.baseR));
     p.psi = root_of_unity(cyc, p.Q);
     uint64_t v = 1;
     for (uint32_t i = 0; i < p.digitsG; ++i) {

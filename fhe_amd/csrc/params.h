@@ -12,7 +12,7 @@
 namespace fhe_amd {
 
 // reference enum values (src/binfhe/include/binfhe-constants.h:49-126)
-enum ParamSet : int { PS_TOY = 0, PS_STD128 = 3, PS_STD128_LMKCDEY = 21 };
+enum ParamSet : int { PS_TOY = 0, PS_STD128_AP = 2, PS_STD128 = 3, PS_STD128_LMKCDEY = 21 };
 enum Method : int { M_AP = 1, M_GINX = 2, M_LMKCDEY = 3 };
 enum Gate : int { G_OR = 0, G_AND, G_NOR, G_NAND, G_XOR, G_XNOR, G_MAJORITY, G_AND3, G_OR3, G_AND4, G_OR4,
                   G_XOR_FAST, G_XNOR_FAST, G_CMUX };
@@ -22,6 +22,7 @@ struct Params {
     int paramset = 0, method = 0;
     uint32_t n = 0, N = 0, q = 0, qKS = 0, baseKS = 0, digitsKS = 0;
     uint32_t baseG = 0, gBits = 0, digitsG = 0, digitsG2 = 0, numAutoKeys = 0;
+    uint32_t baseR = 0, digitsR = 0;  // AP/DM refresh base and digit count (rgsw-cryptoparameters.cpp:37-46)
     int keyDist = KD_UNIFORM_TERNARY;
     uint64_t Q = 0, psi = 0;
     std::vector<uint64_t> gpow;  // Gpow[i] = baseG^i mod Q (rgsw-cryptoparameters.cpp:69-74)

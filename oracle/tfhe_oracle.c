@@ -97,11 +97,12 @@ int tfo_params_init(int paramset, int method, tfo_params* p) {
     uint32_t bits, cyc, n, q, qks, bks, bg, nauto;
     switch (paramset) {
         case TFO_TOY:            bits = 27; cyc = 1024; n = 64;  q = 512;  qks = 0;     bks = 25; bg = 512;  nauto = 9;  break;
+        case TFO_STD128_AP:
         case TFO_STD128:         bits = 27; cyc = 2048; n = 503; q = 1024; qks = 16384; bks = 32; bg = 512;  nauto = 10; break;
         case TFO_STD128_LMKCDEY: bits = 28; cyc = 2048; n = 447; q = 2048; qks = 16384; bks = 32; bg = 1024; nauto = 10; break;
         default: return -1;
     }
-    if (method != TFO_GINX && method != TFO_LMKCDEY) return -2;
+    if (method != TFO_GINX && method != TFO_LMKCDEY && method != TFO_AP) return -2;
     memset(p, 0, sizeof(*p));
     p->paramset = paramset; p->method = method;
     p->n = n; p->N = cyc / 2; p->q = q;
@@ -113,6 +114,8 @@ int tfo_params_init(int paramset, int method, tfo_params* p) {
     p->digitsG = (uint32_t)ceil(log((double)p->Q) / log((double)bg));
     p->numAutoKeys = nauto;
     p->psi = tfo_root_of_unity(cyc, p->Q);
+    p->baseR = 32;                                              /* baseR column (binfhecontext.cpp:113-159) */
+    p->digitsR = (uint32_t)ceil(log((double)q) / log((double)p->baseR));
     return 0;
 }
 
@@ -309,6 +312,20 @@ static void add_to_acc_lmk(const boot_ctx* c, const uint64_t* ek, uint64_t* acc,
         }
 }
 
+/* EvalAcc DM (rgsw-acc-dm.cpp:62-77): for each i and base-baseR digit a0 of (q - a_i) mod q,
+ * acc <- external product with key [i][a0][k] (AddToAccDM :119-145 == add_to_acc_lmk) */
+static void eval_acc_dm(const boot_ctx* c, const uint64_t* bsk, const uint64_t* a, uint64_t* acc, uint64_t* work) {
+    const tfo_params* p = c->p; const uint32_t N = p->N;
+    const size_t rg = (size_t)c->dG2 * 2 * N;
+    for (uint32_t i = 0; i < p->n; ++i) {
+        uint64_t aI = (p->q - a[i] % p->q) % p->q;
+        for (uint32_t k = 0; k < p->digitsR; ++k, aI /= p->baseR) {
+            const uint64_t a0 = aI % p->baseR;
+            if (a0) add_to_acc_lmk(c, bsk + (((size_t)i * p->baseR + a0) * p->digitsR + k) * rg, acc, work);
+        }
+    }
+}
+
 /* Automorphism: rgsw-acc-lmkcdey.cpp:257-287 */
 static void lmk_automorphism(const boot_ctx* c, uint32_t k, const uint64_t* ak, uint64_t* acc, uint64_t* work) {
     const tfo_params* p = c->p; const uint32_t N = p->N, dG = p->digitsG - 1; const uint64_t Q = p->Q;
@@ -471,6 +488,7 @@ static void eval_core(const boot_ctx* c, const uint64_t* bsk, const uint64_t* ks
     }
     ntt_fwd(&c->T, acc + N);
     if (p->method == TFO_GINX) eval_acc_cggi(c, bsk, a, q, acc, work);
+    else if (p->method == TFO_AP) eval_acc_dm(c, bsk, a, acc, work);
     else eval_acc_lmk(c, bsk, a, acc, work);
     /* Transpose acc0 (automorphism 2N-1), iNTT both */
     uint64_t* t0 = work;
@@ -593,6 +611,7 @@ static void bootstrap_func1(const boot_ctx* c, const uint64_t* bsk, const uint64
     for (uint64_t j = 0; j < (ctmod >> 1); ++j) acc[N + j * factor] = tv[(b + ctmod - j) % ctmod];
     ntt_fwd(&c->T, acc + N);
     if (p->method == TFO_GINX) eval_acc_cggi(c, bsk, a, ctmod, acc, work);
+    else if (p->method == TFO_AP) eval_acc_dm(c, bsk, a, acc, work);
     else eval_acc_lmk(c, bsk, a, acc, work);
     uint64_t* t0 = work;
     automorphism(p, 2 * N - 1, acc, t0);

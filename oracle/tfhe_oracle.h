@@ -14,6 +14,7 @@
  * Raw layouts (u64 words, polynomials of N coefficients; EVALUATION-domain
  * polynomials in the reference's bit-reversed order):
  *   GINX    bsk : [n][2 (s=+1,s=-1)][digitsG2][2][N]      rgsw-acc-cggi.cpp:39-57
+ *   AP bsk      : [n][baseR][digitsR][digitsG2][2][N]  (j = 0 slots unused)  rgsw-acc-dm.cpp:39-58
  *   LMKCDEY bsk : [n][digitsG2][2][N] ++ [numAutoKeys+1][digitsG-1][2][N]
  *                                                          rgsw-acc-lmkcdey.cpp:39-68
  *   ksk A : [N][baseKS][digitsKS][n],  ksk B : [N][baseKS][digitsKS]
@@ -31,11 +32,12 @@ extern "C" {
 #endif
 
 /* reference enum values (src/binfhe/include/binfhe-constants.h:49-126) */
-enum { TFO_TOY = 0, TFO_STD128 = 3, TFO_STD128_LMKCDEY = 21 };
+enum { TFO_TOY = 0, TFO_STD128_AP = 2, TFO_STD128 = 3, TFO_STD128_LMKCDEY = 21 };
 enum { TFO_AP = 1, TFO_GINX = 2, TFO_LMKCDEY = 3 };
 
 typedef struct {
     uint32_t n, N, q, qKS, baseKS, digitsKS, baseG, gBits, digitsG, numAutoKeys, method, paramset;
+    uint32_t baseR, digitsR;  /* AP/DM refresh decomposition of a_i (rgsw-cryptoparameters.cpp:37-46) */
     uint64_t Q, psi;
 } tfo_params;
 

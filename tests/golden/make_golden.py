@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
-from oracle_lib import GINX, LMKCDEY, STD128, STD128_LMKCDEY, Ref  # noqa: E402
+from oracle_lib import AP, GINX, LMKCDEY, STD128, STD128_AP, STD128_LMKCDEY, Ref  # noqa: E402
 
 NTT_MODULI = {
     "q60": 1152921504606830593,   # poly-benchmark-1k (benchmark/src/poly-benchmark-1k.cpp:40-50)
@@ -43,7 +43,7 @@ def make_ntt():
         print(name, Q, psi, "ok")
 
 
-GATE_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY)}
+GATE_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "ap": (STD128_AP, AP)}
 GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}
 PER_GATE = 8
 

@@ -18,8 +18,8 @@ RESTATE_SO = os.path.join(ROOT, "oracle", "_ref", "libtfhe_oracle.so")
 u64p = ctypes.POINTER(ctypes.c_uint64)
 vp = ctypes.c_void_p
 
-TOY, STD128, STD128_LMKCDEY = 0, 3, 21
-GINX, LMKCDEY = 2, 3
+TOY, STD128_AP, STD128, STD128_LMKCDEY = 0, 2, 3, 21
+AP, GINX, LMKCDEY = 1, 2, 3
 GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}
 MAJORITY, AND3, OR3, AND4, OR4, CMUX = 6, 7, 8, 9, 10, 13
 
@@ -201,7 +201,7 @@ class Ref:
 class _Params(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint32) for f in
                 ("n", "N", "q", "qKS", "baseKS", "digitsKS", "baseG", "gBits", "digitsG", "numAutoKeys",
-                 "method", "paramset")] + [("Q", ctypes.c_uint64), ("psi", ctypes.c_uint64)]
+                 "method", "paramset", "baseR", "digitsR")] + [("Q", ctypes.c_uint64), ("psi", ctypes.c_uint64)]
 
 
 class Restatement:

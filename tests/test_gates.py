@@ -9,7 +9,7 @@ import pytest
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 TRUTH = {0: np.logical_or, 1: np.logical_and, 2: lambda a, b: ~(a | b) & 1, 3: lambda a, b: ~(a & b) & 1,
          4: np.logical_xor, 5: lambda a, b: ~(a ^ b) & 1}
-SETS = ["std128", "lmkcdey"]
+SETS = ["std128", "lmkcdey", "ap"]
 
 
 def sha(a):

@@ -9,7 +9,8 @@ sys.path.insert(0, ".")
 from fhe_amd import binfhe as bf  # noqa: E402
 from fhe_amd._lib import check, lib, ptr, vp  # noqa: E402
 
-ps, m = (bf.STD128, bf.GINX) if (len(sys.argv) < 2 or sys.argv[1] == "ginx") else (bf.STD128_LMKCDEY, bf.LMKCDEY)
+SETS = {"ginx": (bf.STD128, bf.GINX), "lmk": (bf.STD128_LMKCDEY, bf.LMKCDEY), "ap": (bf.STD128_AP, bf.AP)}
+ps, m = SETS[sys.argv[1] if len(sys.argv) > 1 else "ginx"]
 batches = [int(x) for x in sys.argv[2:]] or [1024, 8192]
 t0 = time.time()
 keys = bf.keygen(ps, m, 1234)
