@@ -76,6 +76,11 @@ def _setup(L):
     L.fhe_hip_eval_decomp_parts.argtypes = [vp, u64, vp]
     L.fhe_hip_eval_decomp_batch.argtypes = [vp, sz, vp, vp, u64, vp, vp]
     L.fhe_hip_bootstrap_func_batch.argtypes = [vp, sz, vp, vp, ctypes.c_uint32, vp, u64, vp, vp]
+    L.fhe_hip_pack_lwe_batch.argtypes = [ctypes.c_uint32, sz, vp, vp, ctypes.c_uint32, vp, sz, vp]
+    L.fhe_hip_unpack_lwe_batch.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.fhe_hip_eval_bingate_packed.argtypes = [vp, ctypes.c_int, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp]
+    L.fhe_hip_pack_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
+    L.fhe_hip_load_keys_packed.argtypes = [vp, vp, sz, vp, sz]
     L.fhe_hip_multi_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.fhe_hip_multi_destroy.argtypes = [vp]
     L.fhe_hip_multi_destroy.restype = None
@@ -166,6 +171,43 @@ def _ptrs(arrs):
     return t
 
 
+# ---- the reference's packed transfer format (backend/packed.h) ----
+LWE_PACK_INTERLEAVED = 1
+
+
+def pack_lwe_batch(a, b, flags=0):
+    """PackLWEBatch-compatible bytes (backend/packed.cpp:144-211)."""
+    a, b = _u64(np.atleast_2d(a)), _u64(np.atleast_1d(b))
+    size = ctypes.c_size_t()
+    check(L().fhe_hip_pack_lwe_batch(a.shape[1], len(b), ptr(a), ptr(b), flags, None, 0, ctypes.byref(size)))
+    out = np.zeros(size.value, np.uint8)
+    check(L().fhe_hip_pack_lwe_batch(a.shape[1], len(b), ptr(a), ptr(b), flags, ptr(out), out.size,
+                                     ctypes.byref(size)))
+    return out.tobytes()
+
+
+def unpack_lwe_batch(data):
+    buf = np.frombuffer(data, np.uint8)
+    n, cnt = ctypes.c_uint32(), ctypes.c_size_t()
+    check(L().fhe_hip_unpack_lwe_batch(ptr(buf), buf.size, ctypes.byref(n), ctypes.byref(cnt), None, None))
+    a = np.zeros((cnt.value, n.value), np.uint64)
+    b = np.zeros(cnt.value, np.uint64)
+    check(L().fhe_hip_unpack_lwe_batch(ptr(buf), buf.size, ctypes.byref(n), ctypes.byref(cnt), ptr(a), ptr(b)))
+    return a, b
+
+
+def pack_keys(paramset, method, keys):
+    """(packed bootstrapping key, packed switching key) bytes."""
+    bsk, A, B = _u64(keys.bsk), _u64(keys.kskA), _u64(keys.kskB)
+    s1, s2 = ctypes.c_size_t(), ctypes.c_size_t()
+    check(L().fhe_hip_pack_keys(paramset, method, ptr(bsk), bsk.size, ptr(A), ptr(B), None, 0, ctypes.byref(s1), None,
+                                0, ctypes.byref(s2)))
+    ob, ok = np.zeros(s1.value, np.uint8), np.zeros(s2.value, np.uint8)
+    check(L().fhe_hip_pack_keys(paramset, method, ptr(bsk), bsk.size, ptr(A), ptr(B), ptr(ob), ob.size,
+                                ctypes.byref(s1), ptr(ok), ok.size, ctypes.byref(s2)))
+    return ob, ok
+
+
 class GateEngine:
     """One MI355X context (fhe_hip_ctx): resident keys + batched gate bootstrapping."""
 
@@ -203,6 +245,21 @@ class GateEngine:
         check(L().fhe_hip_eval_bingate_batch(self._h, gate, cnt, ptr(a1), ptr(b1), ptr(a2), ptr(b2), ptr(ao),
                                              ptr(bo)))
         return ao, bo
+
+    def eval_gate_packed(self, gate, in1, in2, out_flags=0):
+        """EvalBinGate on two PackLWEBatch buffers; returns the packed result."""
+        p1, p2 = np.frombuffer(in1, np.uint8), np.frombuffer(in2, np.uint8)
+        size = ctypes.c_size_t()
+        check(L().fhe_hip_eval_bingate_packed(self._h, gate, ptr(p1), p1.size, ptr(p2), p2.size, out_flags, None, 0,
+                                              ctypes.byref(size)))
+        out = np.zeros(size.value, np.uint8)
+        check(L().fhe_hip_eval_bingate_packed(self._h, gate, ptr(p1), p1.size, ptr(p2), p2.size, out_flags, ptr(out),
+                                              out.size, ctypes.byref(size)))
+        return out.tobytes()
+
+    def load_keys_packed(self, bsk_packed, ksk_packed):
+        check(L().fhe_hip_load_keys_packed(self._h, ptr(bsk_packed), bsk_packed.size, ptr(ksk_packed),
+                                           ksk_packed.size))
 
     def eval_gate_extended(self, gate, a1, b1, a2, b2):
         a1, b1, a2, b2 = _u64(a1), _u64(b1), _u64(a2), _u64(b2)

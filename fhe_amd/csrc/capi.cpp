@@ -1,6 +1,8 @@
 // capi.cpp -- extern "C" boundary (include/fhe_hip.h).  No exception crosses it.
 #include <hip/hip_runtime.h>
 
+#include <string.h>
+
 #include <exception>
 #include <new>
 #include <string>
@@ -9,6 +11,7 @@
 
 #include "../../include/fhe_hip.h"
 #include "engine.h"
+#include "packed.h"
 #include "multi.h"
 #include "keygen.h"
 #include "ntt.h"
@@ -222,6 +225,87 @@ int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint6
 static bool io_ok(size_t count, const void* a, const void* b, const void* c, const void* d, const void* e,
                   const void* f) {
     return count == 0 || (a && b && c && d && e && f);
+}
+
+// ---- packed transfer format (reference backend/packed.h) ----
+int fhe_hip_pack_lwe_batch(uint32_t n, size_t count, const uint64_t* a, const uint64_t* b, uint32_t flags,
+                           uint8_t* out, size_t capacity, size_t* size) {
+    if (!size || (count && (!a || !b))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        *size = packed_lwe_batch_size(n, count);
+        if (!out) return FHE_HIP_OK;
+        if (capacity < *size) return fail(FHE_HIP_ERR_INVALID_PARAM, "output buffer too small");
+        pack_lwe_batch(n, count, a, b, flags, out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_unpack_lwe_batch(const uint8_t* data, size_t size, uint32_t* n, size_t* count, uint64_t* a, uint64_t* b) {
+    if (!data || !n || !count) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        unpack_lwe_batch(data, size, n, count, a, b);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_bingate_packed(fhe_hip_ctx* ctx, int gate, const uint8_t* in1, size_t size1, const uint8_t* in2,
+                                size_t size2, uint32_t out_flags, uint8_t* out, size_t capacity, size_t* size) {
+    if (!ctx || !in1 || !in2 || !size) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        uint32_t n1, n2;
+        size_t c1, c2;
+        unpack_lwe_batch(in1, size1, &n1, &c1, nullptr, nullptr);
+        unpack_lwe_batch(in2, size2, &n2, &c2, nullptr, nullptr);
+        const uint32_t n = ctx->eng.params().n;
+        if (n1 != n || n2 != n) return fail(FHE_HIP_ERR_INVALID_PARAM, "packed batch dimension != n");
+        if (c1 != c2) return fail(FHE_HIP_ERR_INVALID_PARAM, "packed batches differ in size");
+        *size = packed_lwe_batch_size(n, c1);
+        if (!out) return FHE_HIP_OK;
+        if (capacity < *size) return fail(FHE_HIP_ERR_INVALID_PARAM, "output buffer too small");
+        std::vector<uint64_t> a1(c1 * n), b1(c1), a2(c1 * n), b2(c1), ao(c1 * n), bo(c1);
+        unpack_lwe_batch(in1, size1, &n1, &c1, a1.data(), b1.data());
+        unpack_lwe_batch(in2, size2, &n2, &c2, a2.data(), b2.data());
+        ctx->eng.eval_gate_host(gate, c1, a1.data(), b1.data(), a2.data(), b2.data(), ao.data(), bo.data());
+        pack_lwe_batch(n, c1, ao.data(), bo.data(), out_flags, out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_pack_keys(int paramset, int method, const uint64_t* bsk, size_t bsk_words, const uint64_t* A,
+                      const uint64_t* B, uint8_t* bsk_out, size_t bsk_cap, size_t* bsk_size, uint8_t* ksk_out,
+                      size_t ksk_cap, size_t* ksk_size) {
+    if (!bsk_size || !ksk_size) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const Params p = make_params(paramset, method);
+        *bsk_size = sizeof(PackedBskHdr) + p.bsk_words() * 8;
+        *ksk_size = sizeof(PackedKskHdr) + p.ksk_rows() * ((size_t)p.n + 1) * 8;
+        if (bsk_out) {
+            if (!bsk || bsk_cap < *bsk_size) return fail(FHE_HIP_ERR_INVALID_PARAM, "bsk buffer missing or too small");
+            auto v = pack_bsk(p, bsk, bsk_words);
+            memcpy(bsk_out, v.data(), v.size());
+        }
+        if (ksk_out) {
+            if (!A || !B || ksk_cap < *ksk_size) return fail(FHE_HIP_ERR_INVALID_PARAM, "ksk buffer missing or too small");
+            auto v = pack_ksk(p, A, B);
+            memcpy(ksk_out, v.data(), v.size());
+        }
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_load_keys_packed(fhe_hip_ctx* ctx, const uint8_t* bsk, size_t bsk_size, const uint8_t* ksk,
+                             size_t ksk_size) {
+    if (!ctx || !bsk || !ksk) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const Params& p = ctx->eng.params();
+        size_t words = 0;
+        const uint64_t* raw = unpack_bsk(p, bsk, bsk_size, &words);
+        const uint64_t *A = nullptr, *B = nullptr;
+        unpack_ksk(p, ksk, ksk_size, &A, &B);
+        ctx->eng.load_bsk(raw, words);
+        ctx->eng.load_ksk(A, p.ksk_rows() * p.n, B, p.ksk_rows());
+        return FHE_HIP_OK;
+    });
 }
 
 int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,

@@ -1,0 +1,151 @@
+// packed.cpp -- the reference's packed transfer format (see packed.h).
+#include "packed.h"
+
+#include <string.h>
+
+#include <stdexcept>
+
+#include "params.h"
+
+namespace fhe_amd {
+
+namespace {
+PackedHeader header(uint16_t type, uint64_t total, uint64_t count, uint32_t flags) {
+    PackedHeader h{};
+    h.magic = kPackedMagic;
+    h.version = kPackedVersion;
+    h.type = type;
+    h.total_size = total;
+    h.element_count = count;
+    h.flags = flags;
+    return h;
+}
+
+// ValidatePackedHeader (packed.cpp:17-34) + the expected type
+const PackedHeader& check_header(const uint8_t* data, size_t size, uint16_t type, size_t block) {
+    if (!data || size < sizeof(PackedHeader)) throw std::invalid_argument("packed data too short");
+    const auto* h = reinterpret_cast<const PackedHeader*>(data);
+    if (h->magic != kPackedMagic) throw std::invalid_argument("packed data: bad magic");
+    if (h->version > kPackedVersion) throw std::invalid_argument("packed data: unsupported version");
+    if (h->total_size > size) throw std::invalid_argument("packed data: truncated");
+    if (h->type != type) throw std::invalid_argument("packed data: unexpected type");
+    if (size < block) throw std::invalid_argument("packed data too short for its header");
+    return *h;
+}
+
+uint32_t log2u(uint64_t x) {
+    uint32_t r = 0;
+    while ((1ull << (r + 1)) <= x) ++r;
+    return r;
+}
+}  // namespace
+
+size_t packed_lwe_batch_size(uint32_t n, size_t count) {
+    return sizeof(PackedLWEBatchHdr) + count * ((size_t)n + 1) * 8;
+}
+
+void pack_lwe_batch(uint32_t n, size_t count, const uint64_t* a, const uint64_t* b, uint32_t flags, uint8_t* out) {
+    PackedLWEBatchHdr h{};
+    h.h = header(PT_LWE_BATCH, packed_lwe_batch_size(n, count), count, flags);
+    h.n = n;
+    h.log_q = 64;  // as PackLWEBatch writes it (packed.cpp:174-176)
+    h.q = 0;
+    h.count = count;
+    h.stride = (uint32_t)(((size_t)n + 1) * 8);
+    memcpy(out, &h, sizeof(h));
+    uint64_t* w = reinterpret_cast<uint64_t*>(out + sizeof(h));
+    if (flags & LWE_PACK_INTERLEAVED) {  // [j][ct] then b[ct]
+        for (uint32_t j = 0; j < n; ++j)
+            for (size_t i = 0; i < count; ++i) *w++ = a[i * n + j];
+        for (size_t i = 0; i < count; ++i) *w++ = b[i];
+    } else {  // [ct][a..., b]
+        for (size_t i = 0; i < count; ++i) {
+            memcpy(w, a + i * n, (size_t)n * 8);
+            w += n;
+            *w++ = b[i];
+        }
+    }
+}
+
+void unpack_lwe_batch(const uint8_t* data, size_t size, uint32_t* n, size_t* count, uint64_t* a, uint64_t* b) {
+    const PackedHeader& ph = check_header(data, size, PT_LWE_BATCH, sizeof(PackedLWEBatchHdr));
+    const auto* h = reinterpret_cast<const PackedLWEBatchHdr*>(data);
+    if (h->count > (1ull << 32) || h->n == 0 || h->n > (1u << 20)) throw std::invalid_argument("packed LWE batch: bad n/count");
+    if (size < packed_lwe_batch_size(h->n, h->count)) throw std::invalid_argument("packed LWE batch: truncated");
+    *n = h->n;
+    *count = (size_t)h->count;
+    if (!a || !b) return;
+    const size_t nn = h->n, cnt = (size_t)h->count;
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(data + sizeof(PackedLWEBatchHdr));
+    if (ph.flags & LWE_PACK_INTERLEAVED) {
+        for (size_t j = 0; j < nn; ++j)
+            for (size_t i = 0; i < cnt; ++i) a[i * nn + j] = *w++;
+        for (size_t i = 0; i < cnt; ++i) b[i] = *w++;
+    } else {
+        for (size_t i = 0; i < cnt; ++i) {
+            memcpy(a + i * nn, w, nn * 8);
+            w += nn;
+            b[i] = *w++;
+        }
+    }
+}
+
+std::vector<uint8_t> pack_bsk(const Params& p, const uint64_t* bsk, size_t words) {
+    if (words != p.bsk_words()) throw std::invalid_argument("bsk has wrong length");
+    std::vector<uint8_t> out(sizeof(PackedBskHdr) + words * 8);
+    PackedBskHdr h{};
+    h.h = header(PT_BSK, out.size(), 1, (uint32_t)p.method);
+    h.lwe_n = p.n;
+    h.lwe_log_q = log2u(p.q);
+    h.rlwe_N = p.N;
+    h.rlwe_num_limbs = 1;
+    h.decomp_levels = p.digitsG2;
+    h.decomp_base_log = p.gBits;
+    h.key_size = words * 8;
+    h.key_layout = KEY_LAYOUT_NTT;
+    memcpy(out.data(), &h, sizeof(h));
+    memcpy(out.data() + sizeof(h), bsk, words * 8);
+    return out;
+}
+
+const uint64_t* unpack_bsk(const Params& p, const uint8_t* data, size_t size, size_t* words) {
+    const PackedHeader& ph = check_header(data, size, PT_BSK, sizeof(PackedBskHdr));
+    const auto* h = reinterpret_cast<const PackedBskHdr*>(data);
+    if (ph.flags != (uint32_t)p.method || h->lwe_n != p.n || h->rlwe_N != p.N || h->decomp_levels != p.digitsG2 ||
+        h->decomp_base_log != p.gBits || h->rlwe_num_limbs != 1 || !(h->key_layout & KEY_LAYOUT_NTT))
+        throw std::invalid_argument("packed bootstrapping key does not match the context's parameters");
+    if (h->key_size != p.bsk_words() * 8 || size < sizeof(PackedBskHdr) + h->key_size)
+        throw std::invalid_argument("packed bootstrapping key: wrong size");
+    *words = (size_t)(h->key_size / 8);
+    return reinterpret_cast<const uint64_t*>(data + sizeof(PackedBskHdr));
+}
+
+std::vector<uint8_t> pack_ksk(const Params& p, const uint64_t* A, const uint64_t* B) {
+    const size_t rows = p.ksk_rows();
+    std::vector<uint8_t> out(sizeof(PackedKskHdr) + rows * ((size_t)p.n + 1) * 8);
+    PackedKskHdr h{};
+    h.h = header(PT_KSK, out.size(), rows, 0);
+    h.input_n = p.N;
+    h.output_n = p.n;
+    h.decomp_levels = p.digitsKS;
+    h.decomp_base_log = log2u(p.baseKS);
+    h.Q = p.qKS;
+    memcpy(out.data(), &h, sizeof(h));
+    memcpy(out.data() + sizeof(h), A, rows * p.n * 8);
+    memcpy(out.data() + sizeof(h) + rows * p.n * 8, B, rows * 8);
+    return out;
+}
+
+void unpack_ksk(const Params& p, const uint8_t* data, size_t size, const uint64_t** A, const uint64_t** B) {
+    check_header(data, size, PT_KSK, sizeof(PackedKskHdr));
+    const auto* h = reinterpret_cast<const PackedKskHdr*>(data);
+    const size_t rows = p.ksk_rows();
+    if (h->input_n != p.N || h->output_n != p.n || h->decomp_levels != p.digitsKS ||
+        (1u << h->decomp_base_log) != p.baseKS || h->Q != p.qKS)
+        throw std::invalid_argument("packed switching key does not match the context's parameters");
+    if (size < sizeof(PackedKskHdr) + rows * ((size_t)p.n + 1) * 8) throw std::invalid_argument("packed switching key: truncated");
+    *A = reinterpret_cast<const uint64_t*>(data + sizeof(PackedKskHdr));
+    *B = *A + rows * p.n;
+}
+
+}  // namespace fhe_amd

@@ -97,6 +97,25 @@ void* fhe_hip_stream(fhe_hip_ctx* ctx);
 /* upload keys (BTKeyLoad, binfhecontext.h:273-275; Backend::PackBootstrappingKey) */
 int fhe_hip_load_bsk(fhe_hip_ctx* ctx, const uint64_t* bsk, size_t n_words);
 int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint64_t* B, size_t nB);
+/* ---- the reference's packed transfer format (src/binfhe/include/backend/packed.h:29-307) ----
+ * LWE batches byte-compatible with PackLWEBatch / UnpackLWEBatch (backend/packed.cpp:144-279):
+ * 64-byte header ("LUXF", type LWE_BATCH = 2), u64 coefficients, sequential or INTERLEAVED (flag 1).
+ * pack: out = NULL reports *size.  unpack: a/b = NULL report *n and *count. */
+int fhe_hip_pack_lwe_batch(uint32_t n, size_t count, const uint64_t* a, const uint64_t* b, uint32_t flags,
+                           uint8_t* out, size_t capacity, size_t* size);
+int fhe_hip_unpack_lwe_batch(const uint8_t* data, size_t size, uint32_t* n, size_t* count, uint64_t* a, uint64_t* b);
+/* EvalBinGate on two packed batches, result packed with out_flags (out = NULL reports *size) */
+int fhe_hip_eval_bingate_packed(fhe_hip_ctx* ctx, int gate, const uint8_t* in1, size_t size1, const uint8_t* in2,
+                                size_t size2, uint32_t out_flags, uint8_t* out, size_t capacity, size_t* size);
+/* Packed keys: PackedBootstrappingKey (type 5) / PackedSwitchingKey (type 6) headers of
+ * backend/packed.h (the reference's packers are TODO stubs, packed.cpp:284-328) followed by the
+ * raw u64 layouts above; header.flags of the BSK = BINFHE_METHOD.  NULL outputs report sizes. */
+int fhe_hip_pack_keys(int paramset, int method, const uint64_t* bsk, size_t bsk_words, const uint64_t* A,
+                      const uint64_t* B, uint8_t* bsk_out, size_t bsk_cap, size_t* bsk_size, uint8_t* ksk_out,
+                      size_t ksk_cap, size_t* ksk_size);
+int fhe_hip_load_keys_packed(fhe_hip_ctx* ctx, const uint8_t* bsk, size_t bsk_size, const uint8_t* ksk,
+                             size_t ksk_size);
+
 /* EvalBinGate over count independent pairs (binfhe-base-scheme.cpp:76-126).
  * Inputs mod q, dimension n; outputs likewise.  ct1 and ct2 must not alias
  * (the reference's ct1 == ct2 check, :85-86, becomes a documented precondition). */

@@ -39,6 +39,30 @@ def _p(a):
     return a.ctypes.data_as(vp)
 
 
+def ref_pack_lwe_batch(a, b, flags=0):
+    """the reference's own PackLWEBatch (backend/packed.cpp:144-211) on raw arrays"""
+    L = ctypes.CDLL(REF_SO)
+    a, b = np.ascontiguousarray(a, np.uint64), np.ascontiguousarray(b, np.uint64)
+    size = ctypes.c_size_t()
+    out = np.zeros(64 + a.size * 8 + b.size * 8, np.uint8)
+    rc = L.ref_pack_lwe_batch(ctypes.c_uint32(a.shape[1]), ctypes.c_size_t(len(b)), _p(a), _p(b), ctypes.c_uint32(flags),
+                              out.ctypes.data_as(vp), ctypes.c_size_t(out.size), ctypes.byref(size))
+    assert rc == 0
+    return out[:size.value].tobytes()
+
+
+def ref_unpack_lwe_batch(data, n, count):
+    """the reference's own UnpackLWEBatch (backend/packed.cpp:214-279)"""
+    L = ctypes.CDLL(REF_SO)
+    buf = np.frombuffer(data, np.uint8)
+    a = np.zeros((count, n), np.uint64)
+    b = np.zeros(count, np.uint64)
+    rc = L.ref_unpack_lwe_batch(buf.ctypes.data_as(vp), ctypes.c_size_t(buf.size), ctypes.c_uint32(n),
+                                ctypes.c_size_t(count), _p(a), _p(b))
+    assert rc == 0
+    return a, b
+
+
 def ref_available():
     return os.path.exists(REF_SO)
 
