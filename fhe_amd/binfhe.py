@@ -76,6 +76,8 @@ def _setup(L):
     L.fhe_hip_eval_decomp_parts.argtypes = [vp, u64, vp]
     L.fhe_hip_eval_decomp_batch.argtypes = [vp, sz, vp, vp, u64, vp, vp]
     L.fhe_hip_bootstrap_func_batch.argtypes = [vp, sz, vp, vp, ctypes.c_uint32, vp, u64, vp, vp]
+    L.fhe_hip_btkeygen_device.argtypes = [vp, vp, sz, u64, vp, vp, vp]
+    L.fhe_hip_keygen_secret.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp]
     L.fhe_hip_pack_lwe_batch.argtypes = [ctypes.c_uint32, sz, vp, vp, ctypes.c_uint32, vp, sz, vp]
     L.fhe_hip_unpack_lwe_batch.argtypes = [vp, sz, vp, vp, vp, vp]
     L.fhe_hip_eval_bingate_packed.argtypes = [vp, ctypes.c_int, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp]
@@ -141,6 +143,13 @@ def keygen(paramset, method, seed):
     B = np.zeros(P.ksk_rows, np.uint64)
     check(L().fhe_hip_keygen(paramset, method, seed, ptr(sk), ptr(bsk), ptr(A), ptr(B)))
     return KeySet(sk, bsk, A, B)
+
+
+def keygen_secret(paramset, method, seed):
+    """KeyGen: the LWE secret only (the same sk keygen(seed) returns)."""
+    sk = np.zeros(params(paramset, method).n, np.uint64)
+    check(L().fhe_hip_keygen_secret(paramset, method, seed, ptr(sk)))
+    return sk
 
 
 def encrypt(paramset, method, sk, bits, seed, p=4, mod=0):
@@ -245,6 +254,20 @@ class GateEngine:
         check(L().fhe_hip_eval_bingate_batch(self._h, gate, cnt, ptr(a1), ptr(b1), ptr(a2), ptr(b2), ptr(ao),
                                              ptr(bo)))
         return ao, bo
+
+    def keygen_device(self, sk, seed, export=False):
+        """BTKeyGen on this engine's device; keys identical to keygen(seed) for its sk.  With
+        export=True the raw layouts come back as a KeySet."""
+        sk = _u64(sk)
+        P = self.params
+        if export:
+            ks = KeySet(sk.copy(), np.zeros(P.bsk_words, np.uint64), np.zeros(P.ksk_rows * P.n, np.uint64),
+                        np.zeros(P.ksk_rows, np.uint64))
+            check(L().fhe_hip_btkeygen_device(self._h, ptr(sk), sk.size, seed, ptr(ks.bsk), ptr(ks.kskA),
+                                              ptr(ks.kskB)))
+            return ks
+        check(L().fhe_hip_btkeygen_device(self._h, ptr(sk), sk.size, seed, None, None, None))
+        return None
 
     def eval_gate_packed(self, gate, in1, in2, out_flags=0):
         """EvalBinGate on two PackLWEBatch buffers; returns the packed result."""
@@ -437,13 +460,11 @@ class BinFHEContext:
         return (self._seed * 1000003 + self._ctr) & 0xFFFFFFFFFFFFFFFF
 
     def KeyGen(self):
-        self._keys = keygen(self.paramset, self.method, self._next_seed())
-        return LWEPrivateKey(self._keys.sk)
+        return LWEPrivateKey(keygen_secret(self.paramset, self.method, self._next_seed()))
 
     def BTKeyGen(self, sk):
-        if not np.array_equal(sk.s, self._keys.sk):
-            raise FheHipError(-4, "BTKeyGen: secret key was not produced by this context's KeyGen")
-        self.engine.load_keys(self._keys.bsk, self._keys.kskA, self._keys.kskB)
+        """keys generated on the device (fhe_hip_btkeygen_device); nothing crosses PCIe"""
+        self.engine.keygen_device(sk.s, self._next_seed())
 
     def BTKeyLoad(self, bsk, kskA, kskB):
         self.engine.load_keys(bsk, kskA, kskB)

@@ -222,6 +222,12 @@ int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint6
     return guarded([&]() -> int { ctx->eng.load_ksk(A, nA, B, nB); return FHE_HIP_OK; });
 }
 
+int fhe_hip_btkeygen_device(fhe_hip_ctx* ctx, const uint64_t* sk, size_t n, uint64_t seed, uint64_t* bsk,
+                            uint64_t* kskA, uint64_t* kskB) {
+    if (!ctx || !sk) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int { ctx->eng.keygen_device(sk, n, seed, bsk, kskA, kskB); return FHE_HIP_OK; });
+}
+
 static bool io_ok(size_t count, const void* a, const void* b, const void* c, const void* d, const void* e,
                   const void* f) {
     return count == 0 || (a && b && c && d && e && f);
@@ -537,6 +543,17 @@ int fhe_hip_multi_eval_bingate_batch(fhe_hip_multi* m, int gate, size_t count, c
     if (!m || !io_ok(count, a1, b1, a2, b2, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
         m->eng.eval_gate_host(gate, count, a1, b1, a2, b2, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_keygen_secret(int paramset, int method, uint64_t seed, uint64_t* sk) {
+    if (!sk) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        Params p = make_params(paramset, method);
+        std::vector<uint64_t> s;
+        keygen_secret(p, seed, s);
+        std::copy(s.begin(), s.end(), sk);
         return FHE_HIP_OK;
     });
 }

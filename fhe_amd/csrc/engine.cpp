@@ -3,6 +3,7 @@
 
 #include <algorithm>
 
+#include "keygen.h"
 #include "nt.h"
 
 namespace fhe_amd {
@@ -175,6 +176,47 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
     d_ksk_ = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d_ksk_, dev.size() * 2));
     FHE_HIP_CHECK(hipMemcpy(d_ksk_, dev.data(), dev.size() * 2, hipMemcpyHostToDevice));
+}
+
+void Engine::keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t* bsk_out, uint64_t* kskA_out,
+                           uint64_t* kskB_out) {
+    if (!sk) throw std::invalid_argument("secret key is null");
+    if (n != p_.n) throw std::invalid_argument("secret key has wrong length");
+    const std::vector<uint64_t> s(sk, sk + n);
+    const size_t words = p_.bsk_words(), rows = p_.ksk_rows();
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    if (d_bsk_) FHE_HIP_CHECK(hipFree(d_bsk_));
+    if (d_ksk_) FHE_HIP_CHECK(hipFree(d_ksk_));
+    d_bsk_ = d_autok_ = nullptr;
+    d_ksk_ = nullptr;
+    void* raw = nullptr;
+    uint64_t *rb = nullptr, *ra = nullptr, *rk = nullptr;
+    try {
+        FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * 4));
+        FHE_HIP_CHECK(hipMalloc(&d_ksk_, rows * 512 * 2));
+        const size_t raw_words = (bsk_out ? words : 0) + (kskA_out ? rows * p_.n : 0) + (kskB_out ? rows : 0);
+        if (raw_words) FHE_HIP_CHECK(hipMalloc(&raw, raw_words * 8));
+        uint64_t* cur = static_cast<uint64_t*>(raw);
+        if (bsk_out) { rb = cur; cur += words; }
+        if (kskA_out) { ra = cur; cur += rows * p_.n; }
+        if (kskB_out) rk = cur;
+        keygen_bootstrap_device(p_, s, seed, device_, static_cast<uint32_t*>(d_bsk_), d_ksk_, rb, ra, rk, stream_);
+        if (rb) FHE_HIP_CHECK(hipMemcpy(bsk_out, rb, words * 8, hipMemcpyDeviceToHost));
+        if (ra) FHE_HIP_CHECK(hipMemcpy(kskA_out, ra, rows * p_.n * 8, hipMemcpyDeviceToHost));
+        if (rk) FHE_HIP_CHECK(hipMemcpy(kskB_out, rk, rows * 8, hipMemcpyDeviceToHost));
+    } catch (...) {
+        if (raw) (void)hipFree(raw);
+        if (d_bsk_) (void)hipFree(d_bsk_);
+        if (d_ksk_) (void)hipFree(d_ksk_);
+        d_bsk_ = nullptr;
+        d_ksk_ = nullptr;
+        throw;
+    }
+    if (raw) FHE_HIP_CHECK(hipFree(raw));
+    const size_t nrgsw = p_.method == M_GINX ? (size_t)p_.n * 2
+                         : p_.method == M_AP ? (size_t)p_.n * p_.baseR * p_.digitsR
+                                             : (size_t)p_.n;
+    d_autok_ = static_cast<uint32_t*>(d_bsk_) + nrgsw * p_.digitsG2 * 2 * p_.N;
 }
 
 GateArgs Engine::gate_args(int gate, size_t count, uint32_t p, bool multi) const {

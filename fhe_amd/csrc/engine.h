@@ -47,6 +47,10 @@ public:
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
     void load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB);
+    // BTKeyGen on this device (keygen_dev.hip): keys bit-identical to keygen_bootstrap(sk, seed),
+    // generated in place in the resident layouts; non-null host pointers receive the raw layouts
+    void keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t* bsk_out, uint64_t* kskA_out,
+                       uint64_t* kskB_out);
 
     // EvalBinGate on `count` pairs; device pointers, asynchronous on `s`
     void eval_gate_device(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,

@@ -10,17 +10,15 @@
 namespace fhe_amd {
 namespace {
 
-enum : uint64_t { T_SK = 1, T_SKN, T_BSK, T_KSK, T_ENC, T_AUTO };
-
 // counter-based generator: splitmix64 over (seed, tag, stream, counter)
 struct Rng {
     uint64_t s;
     Rng(uint64_t seed, uint64_t tag, uint64_t stream) {
-        s = seed * 0x9E3779B97F4A7C15ull ^ (tag << 56) ^ (stream * 0xD1B54A32D192ED03ull);
+        s = rng_state(seed, tag, stream);
         next();
     }
     uint64_t next() {
-        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        uint64_t z = (s += kRngGamma);
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         return z ^ (z >> 31);
@@ -40,6 +38,8 @@ inline uint64_t lift(int64_t v, uint64_t m) {
 // signed value of x stored mod m (SwitchModulus semantics, mubintvecnat.cpp:109-122)
 inline int64_t signed_of(uint64_t x, uint64_t m) { return x > (m >> 1) ? (int64_t)x - (int64_t)m : (int64_t)x; }
 
+}  // namespace
+
 void auto_eval(const Params& p, uint32_t k, const uint64_t* in, uint64_t* out) {
     // AutomorphismTransform(k) in EVALUATION (poly-impl.h:350-356)
     const uint32_t N = p.N, logN = ilog2(N), mask = N - 1;
@@ -49,7 +49,11 @@ void auto_eval(const Params& p, uint32_t k, const uint64_t* in, uint64_t* out) {
     }
 }
 
-}  // namespace
+void keygen_ring_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& skN) {
+    skN.assign(p.N, 0);
+    Rng r(seed, T_SKN, 0);
+    for (uint32_t i = 0; i < p.N; ++i) skN[i] = lift(p.keyDist == KD_GAUSSIAN ? r.cbd() : r.ternary(), p.Q);
+}
 
 void keygen_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& sk) {
     sk.assign(p.n, 0);
@@ -67,12 +71,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
     ntt.init(N, Q, p.psi);
 
     // RLWE secret skN and its EVAL form
-    out.skN.assign(N, 0);
-    {
-        Rng r(seed, T_SKN, 0);
-        for (uint32_t i = 0; i < N; ++i)
-            out.skN[i] = lift(p.keyDist == KD_GAUSSIAN ? r.cbd() : r.ternary(), Q);
-    }
+    keygen_ring_secret(p, seed, out.skN);
     std::vector<uint64_t> S(out.skN);
     ntt.forward(S.data());
 

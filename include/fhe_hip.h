@@ -97,6 +97,13 @@ void* fhe_hip_stream(fhe_hip_ctx* ctx);
 /* upload keys (BTKeyLoad, binfhecontext.h:273-275; Backend::PackBootstrappingKey) */
 int fhe_hip_load_bsk(fhe_hip_ctx* ctx, const uint64_t* bsk, size_t n_words);
 int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint64_t* B, size_t nB);
+/* BTKeyGen on the context's device (BinFHEContext::BTKeyGen binfhecontext.cpp:185-200 -> KeyGenAcc
+ * rgsw-acc-cggi.cpp:39-96 / rgsw-acc-dm.cpp:39-114 / rgsw-acc-lmkcdey.cpp:39-226, KeySwitchGen
+ * lwe-pke.cpp:264-344): generates and loads the keys for sk[n] (mod qKS); bit-identical to
+ * fhe_hip_keygen(..., seed, ...) for the sk it returns.  bsk / kskA / kskB (raw layouts, may be
+ * NULL) receive a host copy. */
+int fhe_hip_btkeygen_device(fhe_hip_ctx* ctx, const uint64_t* sk, size_t n, uint64_t seed, uint64_t* bsk,
+                            uint64_t* kskA, uint64_t* kskB);
 /* ---- the reference's packed transfer format (src/binfhe/include/backend/packed.h:29-307) ----
  * LWE batches byte-compatible with PackLWEBatch / UnpackLWEBatch (backend/packed.cpp:144-279):
  * 64-byte header ("LUXF", type LWE_BATCH = 2), u64 coefficients, sequential or INTERLEAVED (flag 1).
@@ -204,6 +211,8 @@ int fhe_hip_multi_eval_bingate_batch(fhe_hip_multi* m, int gate, size_t count, c
 /* Deterministic host key material (KeyGen / BTKeyGen / Encrypt / Decrypt,   */
 /*   binfhecontext.cpp:185-307) -- seeded, same structure as the reference. */
 /* ------------------------------------------------------------------------ */
+/* KeyGen (binfhecontext.cpp:185-190): sk[n] (mod qKS) only */
+int fhe_hip_keygen_secret(int paramset, int method, uint64_t seed, uint64_t* sk);
 /* sk[n] (mod qKS), bsk[bsk_words], kskA[ksk_rows*n], kskB[ksk_rows] */
 int fhe_hip_keygen(int paramset, int method, uint64_t seed, uint64_t* sk, uint64_t* bsk, uint64_t* kskA,
                    uint64_t* kskB);

@@ -52,12 +52,18 @@ def gate_inputs(ps, m, key_seed):
     """Deterministic keys (fhe_amd host keygen, seeded) + encrypted inputs."""
     from fhe_amd import binfhe as bf
     keys = bf.keygen(ps, m, key_seed)
+    return (keys,) + gate_inputs_for(ps, m, key_seed, keys.sk)
+
+
+def gate_inputs_for(ps, m, key_seed, sk):
+    """the encrypted inputs of gate_inputs() under the secret key sk (= keygen(key_seed).sk)"""
+    from fhe_amd import binfhe as bf
     rng = np.random.default_rng(key_seed)
     bits1 = rng.integers(0, 2, size=(len(GATES), PER_GATE))
     bits2 = rng.integers(0, 2, size=(len(GATES), PER_GATE))
-    a1, b1 = bf.encrypt(ps, m, keys.sk, bits1.ravel(), key_seed + 1)
-    a2, b2 = bf.encrypt(ps, m, keys.sk, bits2.ravel(), key_seed + 2)
-    return keys, bits1, bits2, a1, b1, a2, b2
+    a1, b1 = bf.encrypt(ps, m, sk, bits1.ravel(), key_seed + 1)
+    a2, b2 = bf.encrypt(ps, m, sk, bits2.ravel(), key_seed + 2)
+    return bits1, bits2, a1, b1, a2, b2
 
 
 def make_gates(names=("std128", "lmkcdey")):
