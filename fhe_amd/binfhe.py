@@ -78,6 +78,11 @@ def _setup(L):
     L.fhe_hip_bootstrap_func_batch.argtypes = [vp, sz, vp, vp, ctypes.c_uint32, vp, u64, vp, vp]
     L.fhe_hip_btkeygen_device.argtypes = [vp, vp, sz, u64, vp, vp, vp]
     L.fhe_hip_keygen_secret.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp]
+    L.fhe_hip_load_keys_cereal.argtypes = [vp, vp, sz, vp, sz]
+    L.fhe_hip_cereal_read_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, sz, vp, vp, vp]
+    L.fhe_hip_cereal_write_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
+    L.fhe_hip_cereal_read_lwe.argtypes = [vp, sz, ctypes.c_int, vp, ctypes.c_uint32, vp, vp, vp]
+    L.fhe_hip_cereal_write_lwe.argtypes = [vp, ctypes.c_uint32, u64, u64, ctypes.c_int, vp, sz, vp]
     L.fhe_hip_pack_lwe_batch.argtypes = [ctypes.c_uint32, sz, vp, vp, ctypes.c_uint32, vp, sz, vp]
     L.fhe_hip_unpack_lwe_batch.argtypes = [vp, sz, vp, vp, vp, vp]
     L.fhe_hip_eval_bingate_packed.argtypes = [vp, ctypes.c_int, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp]
@@ -217,6 +222,56 @@ def pack_keys(paramset, method, keys):
     return ob, ok
 
 
+# ---- the reference's serialized objects (Serial::Serialize(..., SerType::BINARY)) ----
+def _buf(data):
+    return np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data
+
+
+def cereal_read_keys(paramset, method, refresh, switching):
+    """raw KeySet (sk = None) from a serialized RingGSWACCKey and LWESwitchingKey"""
+    P = params(paramset, method)
+    r, w = _buf(refresh), _buf(switching)
+    ks = KeySet(None, np.zeros(P.bsk_words, np.uint64), np.zeros(P.ksk_rows * P.n, np.uint64),
+                np.zeros(P.ksk_rows, np.uint64))
+    check(L().fhe_hip_cereal_read_keys(paramset, method, ptr(r), r.size, ptr(w), w.size, ptr(ks.bsk), ptr(ks.kskA),
+                                       ptr(ks.kskB)))
+    return ks
+
+
+def cereal_write_keys(paramset, method, keys):
+    """(refresh key bytes, switching key bytes) as the reference's SerializeToFile writes them"""
+    bsk, A, B = _u64(keys.bsk), _u64(keys.kskA), _u64(keys.kskB)
+    s1, s2 = ctypes.c_size_t(), ctypes.c_size_t()
+    args = (paramset, method, ptr(bsk), bsk.size, ptr(A), ptr(B))
+    check(L().fhe_hip_cereal_write_keys(*args, None, 0, ctypes.byref(s1), None, 0, ctypes.byref(s2)))
+    o1, o2 = np.zeros(s1.value, np.uint8), np.zeros(s2.value, np.uint8)
+    check(L().fhe_hip_cereal_write_keys(*args, ptr(o1), o1.size, ctypes.byref(s1), ptr(o2), o2.size,
+                                        ctypes.byref(s2)))
+    return o1.tobytes(), o2.tobytes()
+
+
+def cereal_read_lwe(data, is_key=False):
+    """(a, b, modulus) of a serialized LWECiphertext, or (s, None, modulus) of an LWEPrivateKey"""
+    d = _buf(data)
+    n, b, mod = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
+    check(L().fhe_hip_cereal_read_lwe(ptr(d), d.size, int(is_key), None, 0, ctypes.byref(n), ctypes.byref(b),
+                                      ctypes.byref(mod)))
+    a = np.zeros(n.value, np.uint64)
+    check(L().fhe_hip_cereal_read_lwe(ptr(d), d.size, int(is_key), ptr(a), a.size, ctypes.byref(n), ctypes.byref(b),
+                                      ctypes.byref(mod)))
+    return a, (None if is_key else int(b.value)), int(mod.value)
+
+
+def cereal_write_lwe(a, b, mod, is_key=False):
+    a = _u64(a)
+    size = ctypes.c_size_t()
+    check(L().fhe_hip_cereal_write_lwe(ptr(a), a.size, int(b or 0), mod, int(is_key), None, 0, ctypes.byref(size)))
+    out = np.zeros(size.value, np.uint8)
+    check(L().fhe_hip_cereal_write_lwe(ptr(a), a.size, int(b or 0), mod, int(is_key), ptr(out), out.size,
+                                       ctypes.byref(size)))
+    return out.tobytes()
+
+
 class GateEngine:
     """One MI355X context (fhe_hip_ctx): resident keys + batched gate bootstrapping."""
 
@@ -279,6 +334,11 @@ class GateEngine:
         check(L().fhe_hip_eval_bingate_packed(self._h, gate, ptr(p1), p1.size, ptr(p2), p2.size, out_flags, ptr(out),
                                               out.size, ctypes.byref(size)))
         return out.tobytes()
+
+    def load_keys_cereal(self, refresh, switching):
+        """BTKeyLoad of the reference's serialized refresh / switching keys"""
+        r, w = _buf(refresh), _buf(switching)
+        check(L().fhe_hip_load_keys_cereal(self._h, ptr(r), r.size, ptr(w), w.size))
 
     def load_keys_packed(self, bsk_packed, ksk_packed):
         check(L().fhe_hip_load_keys_packed(self._h, ptr(bsk_packed), bsk_packed.size, ptr(ksk_packed),
@@ -443,6 +503,44 @@ class LWEPrivateKey:
     s: np.ndarray  # stored mod qKS, as the reference stores it
 
 
+@dataclass
+class SerializedKey:
+    """a RingGSWACCKey ("refresh") or LWESwitchingKey stream as Serial::SerializeToFile writes it"""
+    data: bytes
+
+
+class Serial:
+    """Serial::SerializeToFile / DeserializeFromFile with SerType::BINARY (utils/serial.h:95-125) for
+    the objects of boolean-serial-binary.cpp: LWECiphertext, LWEPrivateKey and the two key streams."""
+
+    @staticmethod
+    def SerializeToFile(path, obj):
+        if isinstance(obj, LWECiphertext):
+            data = cereal_write_lwe(obj.a, obj.b, obj.modulus)
+        elif isinstance(obj, LWEPrivateKey):
+            data = cereal_write_lwe(obj.s, None, 1 << 14, is_key=True)
+        elif isinstance(obj, SerializedKey):
+            data = obj.data
+        else:
+            raise TypeError(f"cannot serialize {type(obj).__name__}")
+        with open(path, "wb") as f:
+            f.write(data)
+        return True
+
+    @staticmethod
+    def DeserializeFromFile(path, cls):
+        with open(path, "rb") as f:
+            data = f.read()
+        if cls is LWECiphertext:
+            a, b, mod = cereal_read_lwe(data)
+            return LWECiphertext(a, b, mod)
+        if cls is LWEPrivateKey:
+            return LWEPrivateKey(cereal_read_lwe(data, is_key=True)[0])
+        if cls is SerializedKey:
+            return SerializedKey(data)
+        raise TypeError(f"cannot deserialize {cls.__name__}")
+
+
 class BinFHEContext:
     def __init__(self, device=0, seed=0x5EED):
         self.device = device
@@ -466,8 +564,13 @@ class BinFHEContext:
         """keys generated on the device (fhe_hip_btkeygen_device); nothing crosses PCIe"""
         self.engine.keygen_device(sk.s, self._next_seed())
 
-    def BTKeyLoad(self, bsk, kskA, kskB):
-        self.engine.load_keys(bsk, kskA, kskB)
+    def BTKeyLoad(self, bsk, kskA, kskB=None):
+        """raw arrays (bsk, kskA, kskB), or the deserialized refresh / switching keys
+        (SerializedKey, SerializedKey) as in boolean-serial-binary.cpp"""
+        if isinstance(bsk, SerializedKey):
+            self.engine.load_keys_cereal(bsk.data, kskA.data)
+        else:
+            self.engine.load_keys(bsk, kskA, kskB)
 
     def Encrypt(self, sk, m, output=None, p=4, mod=0):
         """Encrypt(sk, m, SMALL_DIM, p, mod) (binfhecontext.cpp:220-234)"""

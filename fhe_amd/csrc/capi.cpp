@@ -12,6 +12,7 @@
 #include "../../include/fhe_hip.h"
 #include "engine.h"
 #include "packed.h"
+#include "cereal.h"
 #include "multi.h"
 #include "keygen.h"
 #include "ntt.h"
@@ -312,6 +313,79 @@ int fhe_hip_load_keys_packed(fhe_hip_ctx* ctx, const uint8_t* bsk, size_t bsk_si
         ctx->eng.load_ksk(A, p.ksk_rows() * p.n, B, p.ksk_rows());
         return FHE_HIP_OK;
     });
+}
+
+static int emit_bytes(const std::string& v, uint8_t* out, size_t cap, size_t* size) {
+    *size = v.size();
+    if (out) {
+        if (cap < v.size()) return fail(FHE_HIP_ERR_INVALID_PARAM, "output buffer too small");
+        memcpy(out, v.data(), v.size());
+    }
+    return FHE_HIP_OK;
+}
+
+int fhe_hip_load_keys_cereal(fhe_hip_ctx* ctx, const uint8_t* refresh, size_t refresh_size, const uint8_t* sw,
+                             size_t sw_size) {
+    if (!ctx || !refresh || !sw) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const Params& p = ctx->eng.params();
+        std::vector<uint64_t> bsk, A, B;
+        cereal_read_bsk(p, refresh, refresh_size, bsk);
+        cereal_read_ksk(p, sw, sw_size, A, B);
+        ctx->eng.load_bsk(bsk.data(), bsk.size());
+        ctx->eng.load_ksk(A.data(), A.size(), B.data(), B.size());
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_cereal_read_keys(int paramset, int method, const uint8_t* refresh, size_t refresh_size, const uint8_t* sw,
+                             size_t sw_size, uint64_t* bsk, uint64_t* kskA, uint64_t* kskB) {
+    if (!refresh || !sw || !bsk || !kskA || !kskB) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const Params p = make_params(paramset, method);
+        std::vector<uint64_t> b, A, B;
+        cereal_read_bsk(p, refresh, refresh_size, b);
+        cereal_read_ksk(p, sw, sw_size, A, B);
+        std::copy(b.begin(), b.end(), bsk);
+        std::copy(A.begin(), A.end(), kskA);
+        std::copy(B.begin(), B.end(), kskB);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_cereal_write_keys(int paramset, int method, const uint64_t* bsk, size_t bsk_words, const uint64_t* kskA,
+                              const uint64_t* kskB, uint8_t* refresh_out, size_t refresh_cap, size_t* refresh_size,
+                              uint8_t* sw_out, size_t sw_cap, size_t* sw_size) {
+    if (!bsk || !kskA || !kskB || !refresh_size || !sw_size) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const Params p = make_params(paramset, method);
+        if (bsk_words != p.bsk_words()) return fail(FHE_HIP_ERR_INVALID_PARAM, "bsk has wrong length");
+        int rc = emit_bytes(cereal_write_bsk(p, bsk), refresh_out, refresh_cap, refresh_size);
+        if (rc) return rc;
+        return emit_bytes(cereal_write_ksk(p, kskA, kskB), sw_out, sw_cap, sw_size);
+    });
+}
+
+int fhe_hip_cereal_read_lwe(const uint8_t* data, size_t size, int is_key, uint64_t* a, uint32_t cap_n, uint32_t* n,
+                            uint64_t* b, uint64_t* mod) {
+    if (!data || !n || !mod) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        CerealLwe v = cereal_read_lwe(data, size, is_key != 0);
+        *n = (uint32_t)v.a.size();
+        *mod = v.mod;
+        if (b) *b = v.b;
+        if (a) {
+            if (cap_n < v.a.size()) return fail(FHE_HIP_ERR_INVALID_PARAM, "output buffer too small");
+            std::copy(v.a.begin(), v.a.end(), a);
+        }
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_cereal_write_lwe(const uint64_t* a, uint32_t n, uint64_t b, uint64_t mod, int is_key, uint8_t* out,
+                             size_t cap, size_t* size) {
+    if ((!a && n) || !size) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int { return emit_bytes(cereal_write_lwe(a, n, b, mod, is_key != 0), out, cap, size); });
 }
 
 int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,

@@ -111,6 +111,24 @@ int fhe_hip_btkeygen_device(fhe_hip_ctx* ctx, const uint64_t* sk, size_t n, uint
 int fhe_hip_pack_lwe_batch(uint32_t n, size_t count, const uint64_t* a, const uint64_t* b, uint32_t flags,
                            uint8_t* out, size_t capacity, size_t* size);
 int fhe_hip_unpack_lwe_batch(const uint8_t* data, size_t size, uint32_t* n, size_t* count, uint64_t* a, uint64_t* b);
+/* ---- the reference's serialized objects: Serial::Serialize(obj, s, SerType::BINARY) streams
+ * (utils/serial.h:95-125, cereal PortableBinary; binfhecontext-ser.h registrations) ----
+ * RingGSWACCKey "refresh key" (cc.GetRefreshKey()) + LWESwitchingKey (cc.GetSwitchKey()): loaded
+ * straight into the context (BTKeyLoad of deserialized keys, boolean-serial-binary.cpp flow). */
+int fhe_hip_load_keys_cereal(fhe_hip_ctx* ctx, const uint8_t* refresh, size_t refresh_size, const uint8_t* sw,
+                             size_t sw_size);
+/* the same streams to / from the raw layouts (out = NULL reports the sizes) */
+int fhe_hip_cereal_read_keys(int paramset, int method, const uint8_t* refresh, size_t refresh_size, const uint8_t* sw,
+                             size_t sw_size, uint64_t* bsk, uint64_t* kskA, uint64_t* kskB);
+int fhe_hip_cereal_write_keys(int paramset, int method, const uint64_t* bsk, size_t bsk_words, const uint64_t* kskA,
+                              const uint64_t* kskB, uint8_t* refresh_out, size_t refresh_cap, size_t* refresh_size,
+                              uint8_t* sw_out, size_t sw_cap, size_t* sw_size);
+/* LWECiphertext (is_key = 0: a[n], b, modulus) or LWEPrivateKey (is_key = 1: s[n], modulus);
+ * read with a = NULL reports *n */
+int fhe_hip_cereal_read_lwe(const uint8_t* data, size_t size, int is_key, uint64_t* a, uint32_t cap_n, uint32_t* n,
+                            uint64_t* b, uint64_t* mod);
+int fhe_hip_cereal_write_lwe(const uint64_t* a, uint32_t n, uint64_t b, uint64_t mod, int is_key, uint8_t* out,
+                             size_t cap, size_t* size);
 /* EvalBinGate on two packed batches, result packed with out_flags (out = NULL reports *size) */
 int fhe_hip_eval_bingate_packed(fhe_hip_ctx* ctx, int gate, const uint8_t* in1, size_t size1, const uint8_t* in2,
                                 size_t size2, uint32_t out_flags, uint8_t* out, size_t capacity, size_t* size);

@@ -63,6 +63,52 @@ def ref_unpack_lwe_batch(data, n, count):
     return a, b
 
 
+def ref_serialize_key(ref, which):
+    """the reference's Serial::Serialize(BINARY) of its loaded refresh (0) / switching (1) key"""
+    L = ctypes.CDLL(REF_SO)
+    size = ctypes.c_size_t()
+    fn = L.ref_serialize_key
+    fn.argtypes = [vp, ctypes.c_int, vp, ctypes.c_size_t, vp]
+    assert fn(ref.h, which, None, 0, ctypes.byref(size)) == 0
+    out = np.zeros(size.value, np.uint8)
+    assert fn(ref.h, which, out.ctypes.data_as(vp), out.size, ctypes.byref(size)) == 0
+    return out.tobytes()
+
+
+def ref_deserialize_keys(ref, refresh, switching):
+    """Serial::Deserialize both keys and BTKeyLoad them into the reference context"""
+    L = ctypes.CDLL(REF_SO)
+    fn = L.ref_deserialize_keys
+    fn.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t]
+    ref._chk(fn(ref.h, refresh, len(refresh), switching, len(switching)))
+
+
+def ref_serialize_lwe(a, b, mod, is_key=False):
+    L = ctypes.CDLL(REF_SO)
+    a = np.ascontiguousarray(a, np.uint64)
+    size = ctypes.c_size_t()
+    out = np.zeros(64 + a.size * 8, np.uint8)
+    if is_key:
+        fn = L.ref_serialize_sk
+        fn.argtypes = [ctypes.c_uint32, vp, ctypes.c_uint64, vp, ctypes.c_size_t, vp]
+        assert fn(a.size, _p(a), mod, out.ctypes.data_as(vp), out.size, ctypes.byref(size)) == 0
+    else:
+        fn = L.ref_serialize_ct
+        fn.argtypes = [ctypes.c_uint32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, ctypes.c_size_t, vp]
+        assert fn(a.size, _p(a), b, mod, out.ctypes.data_as(vp), out.size, ctypes.byref(size)) == 0
+    return out[:size.value].tobytes()
+
+
+def ref_deserialize_ct(data, cap_n=4096):
+    L = ctypes.CDLL(REF_SO)
+    fn = L.ref_deserialize_ct
+    fn.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp, vp, vp]
+    a = np.zeros(cap_n, np.uint64)
+    b, n, mod = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint64()
+    assert fn(data, len(data), cap_n, _p(a), ctypes.byref(b), ctypes.byref(n), ctypes.byref(mod)) == 0
+    return a[:n.value], int(b.value), int(mod.value)
+
+
 def ref_available():
     return os.path.exists(REF_SO)
 
