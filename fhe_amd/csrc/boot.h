@@ -22,7 +22,10 @@ struct BootTables {
     const uint32_t* mono;     // kMonoHalfWords: psi^(2f) - 1 -> EVAL(X^m - 1) = omega_j^m - 1, m even
     const uint32_t* mono_full;  // kMonoTableWords: psi^e - 1, any m
     uint32_t Q, Q2, qinv;     // qinv = -Q^-1 mod 2^32
-    uint32_t ninvR, w1ninvR;  // N^-1 and TableI[1] * N^-1 (Montgomery) for the last iNTT stage
+    // The resident keys carry a factor N^-1 (folded in at packing), so the EVALUATION accumulator
+    // is N^-1 * acc and the last inverse stage needs no N^-1 multiply: it scales by TableI[1] only.
+    uint32_t ninvR;  // N^-1 (Montgomery): scales the initial accumulator
+    uint32_t w1R;    // TableI[1] (Montgomery) for the last iNTT stage
 };
 
 struct GateArgs {

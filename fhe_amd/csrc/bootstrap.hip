@@ -192,9 +192,10 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
     }
 }
 
-// inverse NTT: B' (EVAL, inputs < 2Q) -> A' (COEF), outputs canonical [0, Q)
+// inverse NTT of N^-1-scaled data (BootTables::w1R): B' (EVAL, inputs < 2Q) -> A' (COEF),
+// outputs canonical [0, Q)
 FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
-                      const uint32_t* s_twB, uint32_t ninvR, uint32_t w1ninvR, const Mod& m) {
+                      const uint32_t* s_twB, uint32_t w1R, const Mod& m) {
 #pragma unroll
     for (int b = 0; b <= 4; ++b) {
 #pragma unroll
@@ -221,16 +222,37 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             bf_fence(r);
         }
     }
-    // bit 9 with N^-1 folded in (transformnat-impl.h:599-623)
+    // bit 9 (transformnat-impl.h:599-623); its N^-1 factor is already in the data
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         uint32_t x = v[r], y = v[r | 16];
-        v[r]      = csub(mont_mul(x + y, ninvR, m), m.Q);
-        v[r | 16] = csub(mont_mul(x + m.Q2 - y, w1ninvR, m), m.Q);
+        v[r]      = csub(csub(x + y, m.Q2), m.Q);
+        v[r | 16] = csub(mont_mul(x + m.Q2 - y, w1R, m), m.Q);
     }
 }
 
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
+
+// SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = 3: centre x in [0, Q) to
+// d in [-Q/2, Q/2), drop the lowest balanced base-2^g digit, return the next two.  The balanced
+// digits of d are the plain base-2^g digits of d + C, C = 2^(g-1) (1 + 2^g + 2^2g), minus 2^(g-1)
+// (the sequential sign-extend-and-subtract of the reference computes the same unique balanced
+// representation; its last digit sign-extends the low g bits of the remainder, which is what the
+// bit field gives too).  Digits come out as r + Q in [Q - 2^(g-1), Q + 2^(g-1)) (< 2Q: fwd_pass
+// input bound).  Needs C + Q < 2^32 (g <= 10 with Q < 2^28; checked by Engine::gate_args).
+struct Dec {
+    uint32_t Q, Qh, C, CmQ, g, off;
+};
+FHE_DEV Dec make_dec(uint32_t Q, uint32_t g) {
+    const uint32_t h = 1u << (g - 1);
+    return Dec{Q, Q >> 1, h * (1u + (1u << g) + (1u << (2 * g))), h * (1u + (1u << g) + (1u << (2 * g))) - Q, g,
+               Q - h};
+}
+FHE_DEV void decompose2(uint32_t x, const Dec& c, uint32_t& dA, uint32_t& dB) {
+    const uint32_t u = x >= c.Qh ? x + c.CmQ : x + c.C;  // d + C, d = x or x - Q
+    dA               = __builtin_amdgcn_ubfe(u, c.g, c.g) + c.off;
+    dB               = __builtin_amdgcn_ubfe(u, 2 * c.g, c.g) + c.off;
+}
 
 // ModSwitch RoundqQ (lwe-pke.cpp:41-46): floor(0.5 + v*to/from) mod to, in IEEE double in
 // the reference.  For v*to < 2^53, v < from and odd `from` (or power-of-two from/to) the
@@ -332,15 +354,15 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             acc[r] = v;
         }
         fwd_pass(acc, tile, l, T.twA_fwd, s_twBf, m);
+        // canonical, then scaled by N^-1 like everything the keys produce (BootTables::w1R)
 #pragma unroll
-        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), m.Q);
+        for (int r = 0; r < 32; ++r)
+            acc[r] = csub(mont_mul(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), T.ninvR, m), m.Q);
     }
 
     const uint16_t* gidx = idx + (size_t)gate * g.n;
     const uint32_t lbase = 2 * brv5(l) + 1;
-    const int32_t sh     = 32 - (int32_t)g.gbits;
-    const int32_t Qs     = (int32_t)m.Q;
-    const uint32_t Qh    = m.Q >> 1;
+    const Dec dec        = make_dec(m.Q, g.gbits);
     const uint2* ki      = bsk + lane;
     const uint2* kinext  = ki + 2 * 4 * 16 * 64;
     for (uint32_t i = 0; i < g.n; ++i) {
@@ -350,20 +372,11 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         // --- iNTT of a copy of acc -> canonical COEF (AddToAccCGGI :104-106)
 #pragma unroll
         for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-        inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+        inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
         // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
         //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
 #pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            int32_t d  = dA[r] < Qh ? (int32_t)dA[r] : (int32_t)dA[r] - Qs;
-            int32_t r0 = (d << sh) >> sh;
-            d          = (d - r0) >> g.gbits;
-            r0         = (d << sh) >> sh;
-            d          = (d - r0) >> g.gbits;
-            int32_t r1 = (d << sh) >> sh;
-            dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
-            dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
-        }
+        for (int r = 0; r < 32; ++r) decompose2(dA[r], dec, dA[r], dB[r]);
         // --- NTT of the four digit polynomials (two per pass, one per half)
 #if FHE_FWD_FUSED
         fwd_pass2(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
@@ -464,7 +477,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
     // 2N-1), both to COEF; ctExt = (acc0 coefficients, (Q>>3)+1 + acc1[0]); then ModSwitch to qKS.
     // In COEF, Transpose maps coefficient k to -a_(N-k) (k >= 1), a_0 to itself.
-    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
     wave_lds_sync();
     if (h == 0) {
 #pragma unroll
@@ -643,15 +656,15 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             acc[r] = v;
         }
         fwd_pass(acc, tile, l, T.twA_fwd, s_twBf, m);
+        // canonical, then scaled by N^-1 like everything the keys produce (BootTables::w1R)
 #pragma unroll
-        for (int r = 0; r < 32; ++r) acc[r] = csub(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), m.Q);
+        for (int r = 0; r < 32; ++r)
+            acc[r] = csub(mont_mul(csub(csub(csub(acc[r], 4 * m.Q2), 2 * m.Q2), m.Q2), T.ninvR, m), m.Q);
         // acc1 <- acc1(X^(2N-5))   (:99); applied to both halves, acc0 = 0 is invariant
         if (!DM) automorphism_eval(acc, tile, l, M - 5);
     }
 
-    const int32_t sh  = 32 - (int32_t)g.gbits;
-    const int32_t Qs  = (int32_t)m.Q;
-    const uint32_t Qh = m.Q >> 1;
+    const Dec dec     = make_dec(m.Q, g.gbits);
     const uint16_t* gops = ops + (size_t)gate * maxops;
     const uint32_t cnt   = nops[gate];
     for (uint32_t it = 0; it < cnt; ++it) {
@@ -661,18 +674,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                int32_t d  = dA[r] < Qh ? (int32_t)dA[r] : (int32_t)dA[r] - Qs;
-                int32_t r0 = (d << sh) >> sh;
-                d          = (d - r0) >> g.gbits;
-                r0         = (d << sh) >> sh;
-                d          = (d - r0) >> g.gbits;
-                int32_t r1 = (d << sh) >> sh;
-                dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
-                dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
-            }
+            for (int r = 0; r < 32; ++r) decompose2(dA[r], dec, dA[r], dB[r]);
             fwd_pass2(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
             const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
             uint2 kk[2][4];
@@ -708,17 +712,10 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);  // half 0: COEF acc0'
+            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);  // half 0: COEF acc0'
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
-                int32_t d  = dA[r] < Qh ? (int32_t)dA[r] : (int32_t)dA[r] - Qs;
-                int32_t r0 = (d << sh) >> sh;
-                d          = (d - r0) >> g.gbits;
-                r0         = (d << sh) >> sh;
-                d          = (d - r0) >> g.gbits;
-                int32_t r1 = (d << sh) >> sh;
-                dA[r]      = (uint32_t)(r0 < 0 ? r0 + Qs : r0);
-                dB[r]      = (uint32_t)(r1 < 0 ? r1 + Qs : r1);
+                decompose2(dA[r], dec, dA[r], dB[r]);
                 // (half 0's digit A, half 0's digit B) -> lower / upper half of dA
                 auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
                 dA[r]   = sw[0];
@@ -749,7 +746,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     }
 
     // extraction, identical to GINX
-    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.ninvR, T.w1ninvR, m);
+    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
     wave_lds_sync();
     if (h == 0) {
 #pragma unroll

@@ -107,7 +107,7 @@ void Engine::build_tables() {
     tabs_.Q2 = (uint32_t)(2 * Q);
     tabs_.qinv = neg_inv32((uint32_t)Q);
     tabs_.ninvR = to_mont(h.ninv, Q);
-    tabs_.w1ninvR = to_mont(mulmod(h.tabI[1], h.ninv, Q), Q);
+    tabs_.w1R = to_mont(h.tabI[1], Q);
 }
 
 void Engine::load_bsk(const uint64_t* bsk, size_t words) {
@@ -127,6 +127,8 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     const size_t nauto = p_.method == M_LMKCDEY ? (size_t)p_.numAutoKeys + 1 : 0;
     const uint32_t dA = p_.digitsG - 1;
     std::vector<uint32_t> dev(nrgsw * dG2 * 2 * N + nauto * dA * 2 * N);
+    // keys carry N^-1 (BootTables::w1R): the kernels' last inverse stage skips the N^-1 multiply
+    const uint64_t ninv = invmod(N, Q);
     auto pack = [&](const uint64_t* src_key, uint32_t rows, uint32_t* dst_key) {
         for (uint32_t d = 0; d < rows; ++d)
             for (uint32_t k = 0; k < 16; ++k)
@@ -134,8 +136,8 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
                     const uint32_t h = lane >> 5, l = lane & 31;
                     const size_t src = ((size_t)d * 2 + h) * N + l * 32 + 2 * k;
                     const size_t dst = (((size_t)d * 16 + k) * 64 + lane) * 2;
-                    dst_key[dst] = to_mont(src_key[src] % Q, Q);
-                    dst_key[dst + 1] = to_mont(src_key[src + 1] % Q, Q);
+                    dst_key[dst] = to_mont(mulmod(src_key[src] % Q, ninv, Q), Q);
+                    dst_key[dst + 1] = to_mont(mulmod(src_key[src + 1] % Q, ninv, Q), Q);
                 }
     };
 #pragma omp parallel for schedule(static)
@@ -307,6 +309,10 @@ void Engine::prep_device(const GateArgs& g, const GateInputs& in, size_t offset,
 }
 
 void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
+    // the kernels' digit decomposition (bootstrap.hip decompose2) works on d + C in 32 bits
+    const uint64_t h = 1ull << (g.gbits - 1);
+    if (g.gbits < 2 || h * (1 + (1ull << g.gbits) + (1ull << (2 * g.gbits))) + p_.Q >= (1ull << 32))
+        throw std::invalid_argument("device path expects log2(baseG) <= 10");
     if (p_.method == M_GINX) {
         FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
     } else {

@@ -78,7 +78,8 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
                                                    const uint64_t* __restrict__ S,
                                                    const uint64_t* __restrict__ skAuto,
                                                    const uint64_t* __restrict__ A, const uint64_t* __restrict__ T,
-                                                   uint32_t* __restrict__ bsk, uint64_t* __restrict__ raw) {
+                                                   uint64_t ninv, uint32_t* __restrict__ bsk,
+                                                   uint64_t* __restrict__ raw) {
     const KgDesc k = D[blockIdx.x];
     const uint64_t* a = A + (size_t)blockIdx.x * N;
     const uint64_t* e = T + (size_t)blockIdx.x * 2 * N;
@@ -95,10 +96,10 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
         uint64_t r0 = av + m[j];
         r0 = r0 >= Q ? r0 - Q : r0;
         // engine layout (Engine::load_bsk): slot c = l*32 + 2kk + e of component h at
-        // ((kk * 64 + h * 32 + l) * 2 + e), values in Montgomery form (x * 2^32 mod Q)
+        // ((kk * 64 + h * 32 + l) * 2 + e), values x * N^-1 in Montgomery form (* 2^32 mod Q)
         const uint32_t l = j >> 5, kk = (j & 31) >> 1, el = j & 1;
-        bsk[base + ((kk * 64 + l) * 2 + el)] = (uint32_t)((r0 << 32) % Q);
-        bsk[base + ((kk * 64 + 32 + l) * 2 + el)] = (uint32_t)((r1 << 32) % Q);
+        bsk[base + ((kk * 64 + l) * 2 + el)] = (uint32_t)((((r0 * ninv) % Q) << 32) % Q);
+        bsk[base + ((kk * 64 + 32 + l) * 2 + el)] = (uint32_t)((((r1 * ninv) % Q) << 32) % Q);
         if (raw) {
             raw[base + j] = r0;
             raw[base + N + j] = r1;
@@ -255,7 +256,7 @@ void keygen_bootstrap_device(const Params& p, const std::vector<uint64_t>& sk, u
         k_kg_sample<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dA.p, dT.p);
         FHE_HIP_CHECK(hipGetLastError());
         FHE_HIP_CHECK(ntt1024_launch(plan, dT.p, dT.p, 2 * nc, false, s));
-        k_kg_finish<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dS.p, dAuto.p, dA.p, dT.p, d_bsk, raw_bsk);
+        k_kg_finish<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dS.p, dAuto.p, dA.p, dT.p, invmod(N, Q), d_bsk, raw_bsk);
         FHE_HIP_CHECK(hipGetLastError());
     }
 
