@@ -155,7 +155,10 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 }
 
 // two forward NTTs at once (the digit polynomials D_h and D_{2+h}): each twiddle
-// load feeds two butterflies and every stage has 32 independent butterflies
+// load feeds two butterflies and every stage has 32 independent butterflies.
+// LZ (Q < 2^27): no reduction between the halves -- inputs < 2Q grow by < 2Q per stage to
+// < 22Q < 2^32 after all ten; otherwise < 12Q is reduced to < 6Q at the transpose (< 16Q out).
+template <bool LZ>
 FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int l,
                        const uint32_t* __restrict__ twA, const uint32_t* s_twB, const Mod& m) {
 #pragma unroll
@@ -169,10 +172,12 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
             ct_bf(u[r], u[r | (1 << rb)], w, m);
         }
     }
+    if (!LZ) {
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
-        v[r] = csub(csub(v[r], 4 * m.Q2), m.Q2);
-        u[r] = csub(csub(u[r], 4 * m.Q2), m.Q2);
+        for (int r = 0; r < 32; ++r) {
+            v[r] = csub(csub(v[r], 4 * m.Q2), m.Q2);
+            u[r] = csub(csub(u[r], 4 * m.Q2), m.Q2);
+        }
     }
     transpose32(v, tile, l);
     transpose32(u, tile, l);
@@ -308,7 +313,7 @@ constexpr size_t boot_lds(bool full) {
 // MFULL: full-resolution monomial table (ciphertext modulus 2N, any exponent); otherwise the
 // half-resolution table (even exponents: every gate), where slots r and r ^ 1 share a monomial
 // and the compiler drops half of the table reads.
-template <bool MFULL>
+template <bool MFULL, bool LZ>
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
                         const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
@@ -379,7 +384,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         for (int r = 0; r < 32; ++r) decompose2(dA[r], dec, dA[r], dB[r]);
         // --- NTT of the four digit polynomials (two per pass, one per half)
 #if FHE_FWD_FUSED
-        fwd_pass2(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+        fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
 #elif FHE_FWD_SHARED
         // one copy of the forward-pass code for both digit polynomials (instruction-cache
         // footprint): transform dA, swap, transform (old dB), swap back
@@ -464,7 +469,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #else
                 const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
 #endif
-                // t1, t2 < 4.5Q (digits < 14Q) -> S < 9Q^2 -> mont_red < 1.6Q; acc kept in [0, 2Q)
+                // digits < 16Q (Q < 2^28) or < 22Q (LZ, Q < 2^27): S1, S2 < 64 Q^2 or 88 Q^2 ->
+                // t1, t2 < 5Q or 3.75Q; S < 10Q^2 -> mont_red < 1.7Q; acc kept in [0, 2Q)
                 acc[r]            = csub(acc[r] + mont_red(S, m), m.Q2);
             }
 #undef KP
@@ -513,12 +519,23 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
-    if (g.ctmod == 2 * g.N)
-        hipLaunchKernelGGL(k_blind_rotate_ginx<true>, dim3(blocks), dim3(256), boot_lds(true), s, g, t,
-                           reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
-    else
-        hipLaunchKernelGGL(k_blind_rotate_ginx<false>, dim3(blocks), dim3(256), boot_lds(false), s, g, t,
-                           reinterpret_cast<const uint2*>(bsk), idx, tvb, ext_a, ext_b);
+    const uint2* k = reinterpret_cast<const uint2*>(bsk);
+    const bool lz  = t.Q < (1u << 27);
+    if (g.ctmod == 2 * g.N) {
+        if (lz)
+            hipLaunchKernelGGL((k_blind_rotate_ginx<true, true>), dim3(blocks), dim3(256), boot_lds(true), s, g, t, k,
+                               idx, tvb, ext_a, ext_b);
+        else
+            hipLaunchKernelGGL((k_blind_rotate_ginx<true, false>), dim3(blocks), dim3(256), boot_lds(true), s, g, t,
+                               k, idx, tvb, ext_a, ext_b);
+    } else {
+        if (lz)
+            hipLaunchKernelGGL((k_blind_rotate_ginx<false, true>), dim3(blocks), dim3(256), boot_lds(false), s, g, t,
+                               k, idx, tvb, ext_a, ext_b);
+        else
+            hipLaunchKernelGGL((k_blind_rotate_ginx<false, false>), dim3(blocks), dim3(256), boot_lds(false), s, g, t,
+                               k, idx, tvb, ext_a, ext_b);
+    }
     return hipGetLastError();
 }
 
@@ -620,7 +637,7 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
 
 // DM: the AP/DM accumulator runs the same op loop with external products only (AddToAccDM ==
 // AddToAccLMKCDEY, rgsw-acc-dm.cpp:119-145) and no initial automorphism of acc1.
-template <bool DM>
+template <bool DM, bool LZ>
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
@@ -677,7 +694,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2(dA[r], dec, dA[r], dB[r]);
-            fwd_pass2(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+            fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
             const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
             uint2 kk[2][4];
 #pragma unroll
@@ -698,7 +715,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                                  (uint64_t)p01[1] * (e ? kk[k & 1][1].y : kk[k & 1][1].x) +
                                  (uint64_t)p23[0] * (e ? kk[k & 1][2].y : kk[k & 1][2].x) +
                                  (uint64_t)p23[1] * (e ? kk[k & 1][3].y : kk[k & 1][3].x);
-                    acc[r] = csub(csub(mont_red(S, m), 2 * m.Q2), m.Q2);  // < 4.5Q -> [0, 2Q)
+                    // digits < 16Q: S < 64 Q^2 -> < 5Q; LZ: digits < 22Q, Q < 2^27 -> < 3.75Q
+                    const uint32_t t = mont_red(S, m);
+                    acc[r] = csub(LZ ? t : csub(t, 2 * m.Q2), m.Q2);  // -> [0, 2Q)
                 }
             }
         } else {
@@ -785,13 +804,20 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
     if (g.count == 0) return hipSuccess;
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
     const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile) * 4;
-    if (dm)
-        hipLaunchKernelGGL(k_blind_rotate_lmk<true>, dim3(blocks), dim3(256), lds, s, g, t,
-                           reinterpret_cast<const uint2*>(bsk), reinterpret_cast<const uint2*>(autok), ops, nops,
+    const uint2* k  = reinterpret_cast<const uint2*>(bsk);
+    const uint2* ak = reinterpret_cast<const uint2*>(autok);
+    const bool lz   = t.Q < (1u << 27);
+    if (dm && lz)
+        hipLaunchKernelGGL((k_blind_rotate_lmk<true, true>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
+                           maxops, tvb, ext_a, ext_b);
+    else if (dm)
+        hipLaunchKernelGGL((k_blind_rotate_lmk<true, false>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
+                           maxops, tvb, ext_a, ext_b);
+    else if (lz)
+        hipLaunchKernelGGL((k_blind_rotate_lmk<false, true>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
                            maxops, tvb, ext_a, ext_b);
     else
-        hipLaunchKernelGGL(k_blind_rotate_lmk<false>, dim3(blocks), dim3(256), lds, s, g, t,
-                           reinterpret_cast<const uint2*>(bsk), reinterpret_cast<const uint2*>(autok), ops, nops,
+        hipLaunchKernelGGL((k_blind_rotate_lmk<false, false>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
                            maxops, tvb, ext_a, ext_b);
     return hipGetLastError();
 }
