@@ -56,8 +56,10 @@ FHE_DEV void bf_fence(int idx) {
 constexpr int kTile = 32 * 33;  // one half-wave transpose tile (u32 words)
 
 struct Mod {
-    uint32_t Q, Q2, qinv;
+    uint32_t Q, Q2, qinv;  // qinv = -Q^-1 mod 2^32
+    uint32_t qinvp;        // Q^-1 mod 2^32 (signed Montgomery)
 };
+FHE_DEV Mod make_mod(const BootTables& T) { return Mod{T.Q, T.Q2, T.qinv, 0u - T.qinv}; }
 
 // a * bR * 2^-32 mod Q, lazily: result < Q (1 + a / 2^32 * ...) < 2Q for a < 4Q, Q < 2^28
 FHE_DEV uint32_t mont_mul(uint32_t a, uint32_t bR, const Mod& m) {
@@ -69,6 +71,19 @@ FHE_DEV uint32_t mont_red(uint64_t t, const Mod& m) {  // t < 16 Q^2 -> result <
     uint32_t mm = (uint32_t)t * m.qinv;
     return (uint32_t)((t + (uint64_t)mm * m.Q) >> 32);
 }
+// sum of four digit x key products as a non-negative 64-bit value for mont_red: unsigned digits
+// (< 16Q) directly; signed digits (LZ, |d| < 10Q + 2^9, Q < 2^27) plus moff = 64 Q^2 (a multiple
+// of Q above the most negative sum 4 (10Q + 2^9) Q)
+template <bool LZ>
+FHE_DEV uint64_t mac4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t k0, uint32_t k1, uint32_t k2,
+                      uint32_t k3, uint64_t moff) {
+    if (LZ) {
+        const int64_t s = (int64_t)(int32_t)d0 * (int32_t)k0 + (int64_t)(int32_t)d1 * (int32_t)k1 +
+                          (int64_t)(int32_t)d2 * (int32_t)k2 + (int64_t)(int32_t)d3 * (int32_t)k3;
+        return (uint64_t)(s + (int64_t)moff);
+    }
+    return (uint64_t)d0 * k0 + (uint64_t)d1 * k1 + (uint64_t)d2 * k2 + (uint64_t)d3 * k3;
+}
 // Cooley-Tukey (forward), lazy: t = y w < 2Q for any y < 2^32, so x, y < B in gives
 // x + t, x + 2Q - t < B + 2Q out (no reduction; fwd_pass bounds the growth)
 FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
@@ -76,6 +91,19 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
     uint32_t s = x + m.Q2;
     y          = s - t;
     x          = x + t;
+}
+// signed Montgomery (the Q < 2^27 path): a read as int32, bR < Q -> (a b 2^-32 mod Q) in (-Q, Q)
+// for any |a| < 2^31: |a bR - mm Q| < 2^31 Q + 2^31 Q
+FHE_DEV uint32_t smont_mul(uint32_t a, uint32_t bR, const Mod& m) {
+    const int64_t t  = (int64_t)(int32_t)a * (int64_t)(int32_t)bR;
+    const int32_t mm = (int32_t)((uint32_t)t * m.qinvp);
+    return (uint32_t)(int32_t)((t + (int64_t)mm * (int64_t)(-(int32_t)m.Q)) >> 32);  // one v_mad_i64_i32
+}
+// signed Cooley-Tukey: |x|, |y| < B in, < B + Q out, two adds and no offset
+FHE_DEV void ct_bf_s(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
+    const uint32_t t = smont_mul(y, wR, m);
+    y                = x - t;
+    x                = x + t;
 }
 // Gentleman-Sande (inverse): x, y < 2Q in, < 2Q out
 FHE_DEV void gs_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
@@ -156,8 +184,9 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 
 // two forward NTTs at once (the digit polynomials D_h and D_{2+h}): each twiddle
 // load feeds two butterflies and every stage has 32 independent butterflies.
-// LZ (Q < 2^27): no reduction between the halves -- inputs < 2Q grow by < 2Q per stage to
-// < 22Q < 2^32 after all ten; otherwise < 12Q is reduced to < 6Q at the transpose (< 16Q out).
+// LZ (Q < 2^27): signed digits |d| <= 2^(g-1) and signed butterflies -- |v| grows by < Q per
+// stage to < 10Q + 2^(g-1) < 2^31, no reduction anywhere.  Otherwise unsigned digits < 2Q grow by
+// < 2Q per stage; < 12Q is reduced to < 6Q at the transpose (< 16Q out, Q < 2^28).
 template <bool LZ>
 FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int l,
                        const uint32_t* __restrict__ twA, const uint32_t* s_twB, const Mod& m) {
@@ -168,8 +197,13 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << rb)) continue;
             const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
-            ct_bf(v[r], v[r | (1 << rb)], w, m);
-            ct_bf(u[r], u[r | (1 << rb)], w, m);
+            if (LZ) {
+                ct_bf_s(v[r], v[r | (1 << rb)], w, m);
+                ct_bf_s(u[r], u[r | (1 << rb)], w, m);
+            } else {
+                ct_bf(v[r], v[r | (1 << rb)], w, m);
+                ct_bf(u[r], u[r | (1 << rb)], w, m);
+            }
         }
     }
     if (!LZ) {
@@ -191,8 +225,13 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
 #else
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
 #endif
-            ct_bf(v[r], v[r | (1 << b)], w, m);
-            ct_bf(u[r], u[r | (1 << b)], w, m);
+            if (LZ) {
+                ct_bf_s(v[r], v[r | (1 << b)], w, m);
+                ct_bf_s(u[r], u[r | (1 << b)], w, m);
+            } else {
+                ct_bf(v[r], v[r | (1 << b)], w, m);
+                ct_bf(u[r], u[r | (1 << b)], w, m);
+            }
         }
     }
 }
@@ -245,18 +284,26 @@ FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 // representation; its last digit sign-extends the low g bits of the remainder, which is what the
 // bit field gives too).  Digits come out as r + Q in [Q - 2^(g-1), Q + 2^(g-1)) (< 2Q: fwd_pass
 // input bound).  Needs C + Q < 2^32 (g <= 10 with Q < 2^28; checked by Engine::gate_args).
+// SG: the digits themselves, signed (field f -> f - 2^(g-1) is the sign-extension of f with its
+// top bit flipped, so one XOR with M and a signed bit-field extract per digit).
 struct Dec {
-    uint32_t Q, Qh, C, CmQ, g, off;
+    uint32_t Q, Qh, C, CmQ, g, off, M;
 };
 FHE_DEV Dec make_dec(uint32_t Q, uint32_t g) {
-    const uint32_t h = 1u << (g - 1);
-    return Dec{Q, Q >> 1, h * (1u + (1u << g) + (1u << (2 * g))), h * (1u + (1u << g) + (1u << (2 * g))) - Q, g,
-               Q - h};
+    const uint32_t h = 1u << (g - 1), C = h * (1u + (1u << g) + (1u << (2 * g)));
+    return Dec{Q, Q >> 1, C, C - Q, g, Q - h, (h << g) | (h << (2 * g))};
 }
+template <bool SG>
 FHE_DEV void decompose2(uint32_t x, const Dec& c, uint32_t& dA, uint32_t& dB) {
     const uint32_t u = x >= c.Qh ? x + c.CmQ : x + c.C;  // d + C, d = x or x - Q
-    dA               = __builtin_amdgcn_ubfe(u, c.g, c.g) + c.off;
-    dB               = __builtin_amdgcn_ubfe(u, 2 * c.g, c.g) + c.off;
+    if (SG) {
+        const int32_t w = (int32_t)(u ^ c.M);
+        dA              = (uint32_t)__builtin_amdgcn_sbfe(w, c.g, c.g);
+        dB              = (uint32_t)__builtin_amdgcn_sbfe(w, 2 * c.g, c.g);
+    } else {
+        dA = __builtin_amdgcn_ubfe(u, c.g, c.g) + c.off;
+        dB = __builtin_amdgcn_ubfe(u, 2 * c.g, c.g) + c.off;
+    }
 }
 
 // ModSwitch RoundqQ (lwe-pke.cpp:41-46): floor(0.5 + v*to/from) mod to, in IEEE double in
@@ -342,7 +389,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     if (gate >= g.count) return;  // no workgroup barrier below this point
     uint32_t* tileW = s_tile + wave * 2 * kTile;
     uint32_t* tile  = tileW + h * kTile;
-    const Mod m{T.Q, T.Q2, T.qinv};
+    const Mod m = make_mod(T);
 
     // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[32];
@@ -368,6 +415,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     const uint16_t* gidx = idx + (size_t)gate * g.n;
     const uint32_t lbase = 2 * brv5(l) + 1;
     const Dec dec        = make_dec(m.Q, g.gbits);
+    const uint64_t moff  = 64ull * m.Q * m.Q;
     const uint2* ki      = bsk + lane;
     const uint2* kinext  = ki + 2 * 4 * 16 * 64;
     for (uint32_t i = 0; i < g.n; ++i) {
@@ -381,7 +429,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
         //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
 #pragma unroll
-        for (int r = 0; r < 32; ++r) decompose2(dA[r], dec, dA[r], dB[r]);
+        for (int r = 0; r < 32; ++r) decompose2<LZ>(dA[r], dec, dA[r], dB[r]);
         // --- NTT of the four digit polynomials (two per pass, one per half)
 #if FHE_FWD_FUSED
         fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
@@ -457,10 +505,10 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                 auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                 auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
                 const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
-                uint64_t S1 = (uint64_t)D0 * (e ? KP(0).y : KP(0).x) + (uint64_t)D1 * (e ? KP(1).y : KP(1).x) +
-                              (uint64_t)D2 * (e ? KP(2).y : KP(2).x) + (uint64_t)D3 * (e ? KP(3).y : KP(3).x);
-                uint64_t S2 = (uint64_t)D0 * (e ? KN(0).y : KN(0).x) + (uint64_t)D1 * (e ? KN(1).y : KN(1).x) +
-                              (uint64_t)D2 * (e ? KN(2).y : KN(2).x) + (uint64_t)D3 * (e ? KN(3).y : KN(3).x);
+                const uint64_t S1 = mac4<LZ>(D0, D1, D2, D3, e ? KP(0).y : KP(0).x, e ? KP(1).y : KP(1).x,
+                                             e ? KP(2).y : KP(2).x, e ? KP(3).y : KP(3).x, moff);
+                const uint64_t S2 = mac4<LZ>(D0, D1, D2, D3, e ? KN(0).y : KN(0).x, e ? KN(1).y : KN(1).x,
+                                             e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, moff);
                 const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
                 const uint32_t u  = __builtin_amdgcn_readfirstlane((as * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & umask) * 66;
@@ -469,8 +517,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #else
                 const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
 #endif
-                // digits < 16Q (Q < 2^28) or < 22Q (LZ, Q < 2^27): S1, S2 < 64 Q^2 or 88 Q^2 ->
-                // t1, t2 < 5Q or 3.75Q; S < 10Q^2 -> mont_red < 1.7Q; acc kept in [0, 2Q)
+                // digits < 16Q (Q < 2^28): S1, S2 < 64 Q^2 -> t1, t2 < 5Q; LZ (Q < 2^27): |digits| <
+                // 10Q + 2^9, S1, S2 < 105 Q^2 -> t1, t2 < 4.3Q; S < 10Q^2 -> mont_red < 1.7Q;
+                // acc kept in [0, 2Q)
                 acc[r]            = csub(acc[r] + mont_red(S, m), m.Q2);
             }
 #undef KP
@@ -656,7 +705,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     if (gate >= g.count) return;
     uint32_t* tileW = s_tile + wave * 2 * kTile;
     uint32_t* tile  = tileW + h * kTile;
-    const Mod m{T.Q, T.Q2, T.qinv};
+    const Mod m = make_mod(T);
     const uint32_t M = 2 * g.N;
 
     uint32_t acc[32];
@@ -682,6 +731,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     }
 
     const Dec dec     = make_dec(m.Q, g.gbits);
+    const uint64_t moff = 64ull * m.Q * m.Q;
     const uint16_t* gops = ops + (size_t)gate * maxops;
     const uint32_t cnt   = nops[gate];
     for (uint32_t it = 0; it < cnt; ++it) {
@@ -693,7 +743,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
             inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) decompose2(dA[r], dec, dA[r], dB[r]);
+            for (int r = 0; r < 32; ++r) decompose2<LZ>(dA[r], dec, dA[r], dB[r]);
             fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
             const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
             uint2 kk[2][4];
@@ -711,13 +761,12 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                     const int r = 2 * k + e;
                     auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                     auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
-                    uint64_t S = (uint64_t)p01[0] * (e ? kk[k & 1][0].y : kk[k & 1][0].x) +
-                                 (uint64_t)p01[1] * (e ? kk[k & 1][1].y : kk[k & 1][1].x) +
-                                 (uint64_t)p23[0] * (e ? kk[k & 1][2].y : kk[k & 1][2].x) +
-                                 (uint64_t)p23[1] * (e ? kk[k & 1][3].y : kk[k & 1][3].x);
-                    // digits < 16Q: S < 64 Q^2 -> < 5Q; LZ: digits < 22Q, Q < 2^27 -> < 3.75Q
-                    const uint32_t t = mont_red(S, m);
-                    acc[r] = csub(LZ ? t : csub(t, 2 * m.Q2), m.Q2);  // -> [0, 2Q)
+                    const uint64_t S = mac4<LZ>(p01[0], p01[1], p23[0], p23[1], e ? kk[k & 1][0].y : kk[k & 1][0].x,
+                                                e ? kk[k & 1][1].y : kk[k & 1][1].x,
+                                                e ? kk[k & 1][2].y : kk[k & 1][2].x,
+                                                e ? kk[k & 1][3].y : kk[k & 1][3].x, moff);
+                    // digits < 16Q: S < 64 Q^2 -> < 5Q; LZ: S < 105 Q^2 (offset included) -> < 4.3Q
+                    acc[r] = csub(csub(mont_red(S, m), 2 * m.Q2), m.Q2);  // -> [0, 2Q)
                 }
             }
         } else {
@@ -734,7 +783,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);  // half 0: COEF acc0'
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
-                decompose2(dA[r], dec, dA[r], dB[r]);
+                decompose2<false>(dA[r], dec, dA[r], dB[r]);
                 // (half 0's digit A, half 0's digit B) -> lower / upper half of dA
                 auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
                 dA[r]   = sw[0];
