@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=8192, help="gates per GPU per step")
     ap.add_argument("--method", default="ginx", choices=["ginx", "lmkcdey"])
     ap.add_argument("--ntt-count", type=int, default=4096)
-    ap.add_argument("--cpu-sample", type=int, default=256, help="gates in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=3072, help="gates in the CPU-baseline sample (~12 s of host work)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
