@@ -21,11 +21,14 @@ struct BootTables {
     const uint32_t* twB_inv;  // 992 words: same for TableI
     const uint32_t* mono;     // kMonoHalfWords: psi^(2f) - 1 -> EVAL(X^m - 1) = omega_j^m - 1, m even
     const uint32_t* mono_full;  // kMonoTableWords: psi^e - 1, any m
+    const uint32_t* monoP;       // plain (non-Montgomery) copies of mono / mono_full: the signed
+    const uint32_t* monoP_full;  // accumulator multiplies the unreduced 64-bit digit-key sums by both
     uint32_t Q, Q2, qinv;     // qinv = -Q^-1 mod 2^32
     // The resident keys carry a factor N^-1 (folded in at packing), so the EVALUATION accumulator
     // is N^-1 * acc and the last inverse stage needs no N^-1 multiply: it scales by TableI[1] only.
     uint32_t ninvR;  // N^-1 (Montgomery): scales the initial accumulator
     uint32_t w1R;    // TableI[1] (Montgomery) for the last iNTT stage
+    uint32_t oneR;   // 2^32 mod Q (Montgomery 1): x -> x mod Q by one signed Montgomery product
 };
 
 struct GateArgs {

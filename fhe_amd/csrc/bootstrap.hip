@@ -54,6 +54,7 @@ FHE_DEV void bf_fence(int idx) {
 }
 
 constexpr int kTile = 32 * 33;  // one half-wave transpose tile (u32 words)
+constexpr int kAccBoundLZ = 28; // GINX, Q < 2^27: |acc| < 2.8 Q between iterations (units of Q/10)
 
 struct Mod {
     uint32_t Q, Q2, qinv;  // qinv = -Q^-1 mod 2^32
@@ -92,12 +93,38 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
     y          = s - t;
     x          = x + t;
 }
+// v_mad_i64_i32 (a * b + c, 32 x 32 -> 64 signed), emitted explicitly: written as C the compiler
+// sometimes widens a hoisted -Q into a 64-bit constant and expands the product into 5 instructions
+#ifndef FHE_ASM_MAD
+#define FHE_ASM_MAD 1
+#endif
+#ifndef FHE_MAC_NEW
+#define FHE_MAC_NEW 1   // LZ: one reduction per slot, acc folded in (signed acc)
+#endif
+#ifndef FHE_INV_S
+#define FHE_INV_S 1     // LZ: signed inverse NTT
+#endif
+FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
+#if FHE_ASM_MAD
+    int64_t d;
+    uint64_t junk;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(junk) : "v"(a), "v"(b), "v"(c));
+    return d;
+#else
+    return (int64_t)a * b + c;
+#endif
+}
 // signed Montgomery (the Q < 2^27 path): a read as int32, bR < Q -> (a b 2^-32 mod Q) in (-Q, Q)
 // for any |a| < 2^31: |a bR - mm Q| < 2^31 Q + 2^31 Q
 FHE_DEV uint32_t smont_mul(uint32_t a, uint32_t bR, const Mod& m) {
-    const int64_t t  = (int64_t)(int32_t)a * (int64_t)(int32_t)bR;
+    const int64_t t  = mad_i64_i32((int32_t)a, (int32_t)bR, 0);
     const int32_t mm = (int32_t)((uint32_t)t * m.qinvp);
-    return (uint32_t)(int32_t)((t + (int64_t)mm * (int64_t)(-(int32_t)m.Q)) >> 32);  // one v_mad_i64_i32
+    return (uint32_t)(mad_i64_i32(mm, -(int32_t)m.Q, t) >> 32);
+}
+// signed Montgomery reduction of a 64-bit t, |t| < 2^63 - 2^31 Q: t 2^-32 mod Q in (|t| 2^-32 +- Q/2)
+FHE_DEV uint32_t smont_red(int64_t t, const Mod& m) {
+    const int32_t mm = (int32_t)((uint32_t)t * m.qinvp);
+    return (uint32_t)(mad_i64_i32(mm, -(int32_t)m.Q, t) >> 32);
 }
 // signed Cooley-Tukey: |x|, |y| < B in, < B + Q out, two adds and no offset
 FHE_DEV void ct_bf_s(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
@@ -275,6 +302,122 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
     }
 }
 
+// ---- signed inverse NTT (Q < 2^27) ------------------------------------------------------------
+// Gentleman-Sande on signed residues: x' = x + y, y' = smont(x - y, w) in (-Q, Q): two adds and
+// no reduction per butterfly.  Sums grow; |x +- y| must stay < 2^31 = 16Q, so elements whose
+// bound would overflow are brought back to (-Q, Q) by one signed Montgomery product with 2^32 mod Q.
+// Bounds are tracked per register at compile time (units of Q/10): in layout B' the register index
+// is the slot's low 5 bits, so the bound of every element a register holds is the same.  At the
+// transpose every register mixes, so the largest bound is carried into the A' stages.
+struct InvPlanS {
+    bool red1[5][32];  // reduce register r before B' stage b
+    bool redT[32];     // ... before the transpose
+    bool red2[4][32];  // ... before the A' stage on register bit rb
+    bool red3[32];     // ... before the last stage (bit 9)
+    int fin[16];       // last-stage sum x + y: |.| < 2^fin Q -> add 2^fin Q, then fin + 1 conditional subtractions
+};
+constexpr int kLimS = 160;  // |x| + |y| <= 16 Q < 2^31
+constexpr void plan_half(int (&B)[32], bool (&red)[5][32], int stages) {
+    for (int b = 0; b < stages; ++b)
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << b)) continue;
+            const int s = r | (1 << b);
+            while (B[r] + B[s] > kLimS) {
+                const int e = B[r] >= B[s] ? r : s;
+                B[e]         = 10;
+                red[b][e]    = true;
+            }
+            B[r] = B[r] + B[s];
+            B[s] = 10;
+        }
+}
+template <int BIN>
+constexpr InvPlanS make_inv_plan() {
+    InvPlanS p{};
+    int B[32] = {};
+    for (int r = 0; r < 32; ++r) B[r] = BIN;
+    plan_half(B, p.red1, 5);
+    int U = 0;
+    for (int r = 0; r < 32; ++r) {
+        if (B[r] > 20) {
+            p.redT[r] = true;
+            B[r]      = 10;
+        }
+        U = B[r] > U ? B[r] : U;
+    }
+    for (int r = 0; r < 32; ++r) B[r] = U;
+    bool red2[5][32] = {};
+    plan_half(B, red2, 4);
+    for (int b = 0; b < 4; ++b)
+        for (int r = 0; r < 32; ++r) p.red2[b][r] = red2[b][r];
+    for (int r = 0; r < 16; ++r) {
+        while (B[r] + B[r | 16] > kLimS) {
+            const int e = B[r] >= B[r | 16] ? r : (r | 16);
+            B[e]        = 10;
+            p.red3[e]   = true;
+        }
+        int f = 0;
+        while ((10 << f) < B[r] + B[r | 16]) ++f;
+        p.fin[r] = f;
+    }
+    return p;
+}
+
+// B' (EVAL, |inputs| < BIN Q / 10, signed) -> A' (COEF), canonical [0, Q) like inv_pass
+template <int BIN>
+FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
+                        const uint32_t* s_twB, uint32_t w1R, uint32_t oneR, const Mod& m) {
+    constexpr InvPlanS P = make_inv_plan<BIN>();
+#pragma unroll
+    for (int b = 0; b <= 4; ++b) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << b)) continue;
+            const int s = r | (1 << b);
+            if (P.red1[b][r]) v[r] = smont_mul(v[r], oneR, m);
+            if (P.red1[b][s]) v[s] = smont_mul(v[s], oneR, m);
+            const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+            const uint32_t x = v[r], y = v[s];
+            v[r]             = x + y;
+            v[s]             = smont_mul(x - y, w, m);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 32; ++r)
+        if (P.redT[r]) v[r] = smont_mul(v[r], oneR, m);
+    transpose32(v, tile, l);
+#pragma unroll
+    for (int b = 5; b <= 8; ++b) {
+        const int rb = b - 5;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            const int s = r | (1 << rb);
+            if (P.red2[rb][r]) v[r] = smont_mul(v[r], oneR, m);
+            if (P.red2[rb][s]) v[s] = smont_mul(v[s], oneR, m);
+            const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
+            const uint32_t x = v[r], y = v[s];
+            v[r]             = x + y;
+            v[s]             = smont_mul(x - y, w, m);
+        }
+    }
+    // bit 9 (transformnat-impl.h:599-623); its N^-1 factor is already in the data.  Signed results
+    // to [0, Q): the sum by adding 2^f Q and f + 1 conditional subtractions, the product (in
+    // (-Q, Q)) by min(d, d + Q) on the unsigned words.
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (P.red3[r]) v[r] = smont_mul(v[r], oneR, m);
+        if (P.red3[r | 16]) v[r | 16] = smont_mul(v[r | 16], oneR, m);
+        const uint32_t x = v[r], y = v[r | 16];
+        uint32_t s       = x + y + (m.Q << P.fin[r]);
+#pragma unroll
+        for (int f = P.fin[r]; f >= 0; --f) s = csub(s, m.Q << f);
+        const uint32_t d = smont_mul(x - y, w1R, m);
+        v[r]             = s;
+        v[r | 16]        = min(d, d + m.Q);
+    }
+}
+
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 
 // SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = 3: centre x in [0, Q) to
@@ -353,8 +496,9 @@ __global__ void k_prep_ginx(GateInputs in, GateArgs g, uint16_t* __restrict__ id
 // fused blind rotation, 4 gates (waves) per 256-thread workgroup
 // ---------------------------------------------------------------------------
 constexpr int kWaves = 4;
-constexpr size_t boot_lds(bool full) {
-    return (size_t)(992 * 2 + (full ? kMonoTableWords : kMonoHalfWords) + kWaves * 2 * kTile) * 4;
+// LZ: the monomial table holds (plain, Montgomery) pairs
+constexpr size_t boot_lds(bool full, bool lz) {
+    return (size_t)(992 * 2 + (lz && FHE_MAC_NEW ? 2 : 1) * (full ? kMonoTableWords : kMonoHalfWords) + kWaves * 2 * kTile) * 4;
 }
 
 // MFULL: full-resolution monomial table (ciphertext modulus 2N, any exponent); otherwise the
@@ -369,16 +513,21 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     uint32_t* s_twBi = sm + 992;
     // the dynamic LDS size and the tile region follow the table (launch_blind_rotate_ginx)
     constexpr bool mfull = MFULL;
+    constexpr int mwords = mfull ? kMonoTableWords : kMonoHalfWords;
     uint32_t* s_mono = sm + 1984;
-    uint32_t* s_tile = sm + 1984 + (mfull ? kMonoTableWords : kMonoHalfWords);
+    uint2* s_mono2   = reinterpret_cast<uint2*>(sm + 1984);  // LZ: (plain, Montgomery) pairs
+    uint32_t* s_tile = sm + 1984 + (LZ && FHE_MAC_NEW ? 2 : 1) * mwords;
     for (int i = threadIdx.x; i < 992; i += 256) {
         s_twBf[i] = T.twB_fwd[i];
         s_twBi[i] = T.twB_inv[i];
     }
     {
         const uint32_t* src = mfull ? T.mono_full : T.mono;
-        const int words     = mfull ? kMonoTableWords : kMonoHalfWords;
-        for (int i = threadIdx.x; i < words; i += 256) s_mono[i] = src[i];
+        const uint32_t* srp = mfull ? T.monoP_full : T.monoP;
+        for (int i = threadIdx.x; i < mwords; i += 256) {
+            if (LZ && FHE_MAC_NEW) s_mono2[i] = make_uint2(srp[i], src[i]);
+            else s_mono[i] = src[i];
+        }
     }
     constexpr uint32_t msh = mfull ? 0u : 1u, emask = mfull ? 2047u : 1023u, umask = mfull ? 31u : 15u;
     constexpr uint32_t eper = mfull ? 4096u : 2048u;
@@ -425,13 +574,19 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         // --- iNTT of a copy of acc -> canonical COEF (AddToAccCGGI :104-106)
 #pragma unroll
         for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-        inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
+#if defined(FHE_ABL) && (FHE_ABL & 16)
+        if (0)  // ablation: no inverse pass
+#endif
+        if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20>(dA, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
+        else inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
         // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
         //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
 #pragma unroll
         for (int r = 0; r < 32; ++r) decompose2<LZ>(dA[r], dec, dA[r], dB[r]);
         // --- NTT of the four digit polynomials (two per pass, one per half)
-#if FHE_FWD_FUSED
+#if defined(FHE_ABL) && (FHE_ABL & 32)
+        // ablation: no forward passes
+#elif FHE_FWD_FUSED
         fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
 #elif FHE_FWD_SHARED
         // one copy of the forward-pass code for both digit polynomials (instruction-cache
@@ -505,22 +660,41 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                 auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                 auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
                 const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
-                const uint64_t S1 = mac4<LZ>(D0, D1, D2, D3, e ? KP(0).y : KP(0).x, e ? KP(1).y : KP(1).x,
-                                             e ? KP(2).y : KP(2).x, e ? KP(3).y : KP(3).x, moff);
-                const uint64_t S2 = mac4<LZ>(D0, D1, D2, D3, e ? KN(0).y : KN(0).x, e ? KN(1).y : KN(1).x,
-                                             e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, moff);
-                const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
                 const uint32_t u  = __builtin_amdgcn_readfirstlane((as * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & umask) * 66;
+                if (LZ && FHE_MAC_NEW) {
+                    // S1, S2 = sum_d D_d K(+/-)_d unreduced (|.| < 40 Q^2 < 2^60, keys x 2^32); the monomial
+                    // products S (X^m - 1) = lo(S) m + hi(S) (m 2^32) use the (plain, Montgomery) table pair,
+                    // and acc is folded in as acc (2^32 mod Q): one signed Montgomery reduction per slot.
+                    // |acc| < 2.75 Q in and out (S < 2^32 Q (2 + 1/8) + 2.75 Q^2).
+                    const int64_t S1 = (int64_t)mac4<true>(D0, D1, D2, D3, e ? KP(0).y : KP(0).x, e ? KP(1).y : KP(1).x,
+                                                           e ? KP(2).y : KP(2).x, e ? KP(3).y : KP(3).x, 0);
+                    const int64_t S2 = (int64_t)mac4<true>(D0, D1, D2, D3, e ? KN(0).y : KN(0).x, e ? KN(1).y : KN(1).x,
+                                                           e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, 0);
 #if defined(FHE_ABL) && (FHE_ABL & 2)
-                const uint64_t S  = (uint64_t)t1 * (Pp + u) + (uint64_t)t2 * (Pn - u);  // ablation: no monomial reads
+                    const uint2 mp = make_uint2(Pp + u, Pp ^ u), mn = make_uint2(Pn - u, Pn ^ u);
 #else
-                const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
+                    const uint2 mp = s_mono2[Pp + u], mn = s_mono2[Pn - u];
 #endif
-                // digits < 16Q (Q < 2^28): S1, S2 < 64 Q^2 -> t1, t2 < 5Q; LZ (Q < 2^27): |digits| <
-                // 10Q + 2^9, S1, S2 < 105 Q^2 -> t1, t2 < 4.3Q; S < 10Q^2 -> mont_red < 1.7Q;
-                // acc kept in [0, 2Q)
-                acc[r]            = csub(acc[r] + mont_red(S, m), m.Q2);
+                    int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
+                    S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
+                    S += (int64_t)(int32_t)acc[r] * (int32_t)T.oneR;
+                    acc[r] = smont_red(S, m);
+                } else {
+                    const uint64_t S1 = mac4<LZ>(D0, D1, D2, D3, e ? KP(0).y : KP(0).x, e ? KP(1).y : KP(1).x,
+                                                 e ? KP(2).y : KP(2).x, e ? KP(3).y : KP(3).x, moff);
+                    const uint64_t S2 = mac4<LZ>(D0, D1, D2, D3, e ? KN(0).y : KN(0).x, e ? KN(1).y : KN(1).x,
+                                                 e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, moff);
+                    const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
+#if defined(FHE_ABL) && (FHE_ABL & 2)
+                    const uint64_t S  = (uint64_t)t1 * (Pp + u) + (uint64_t)t2 * (Pn - u);  // ablation: no monomial reads
+#else
+                    const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
+#endif
+                    // digits < 16Q (Q < 2^28): S1, S2 < 64 Q^2 -> t1, t2 < 5Q; S < 10Q^2 -> mont_red < 1.7Q;
+                    // acc kept in [0, 2Q)
+                    acc[r]            = csub(acc[r] + mont_red(S, m), m.Q2);
+                }
             }
 #undef KP
 #undef KN
@@ -532,7 +706,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
     // 2N-1), both to COEF; ctExt = (acc0 coefficients, (Q>>3)+1 + acc1[0]); then ModSwitch to qKS.
     // In COEF, Transpose maps coefficient k to -a_(N-k) (k >= 1), a_0 to itself.
-    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
+    if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
+    else inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
     wave_lds_sync();
     if (h == 0) {
 #pragma unroll
@@ -572,17 +747,17 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
     const bool lz  = t.Q < (1u << 27);
     if (g.ctmod == 2 * g.N) {
         if (lz)
-            hipLaunchKernelGGL((k_blind_rotate_ginx<true, true>), dim3(blocks), dim3(256), boot_lds(true), s, g, t, k,
+            hipLaunchKernelGGL((k_blind_rotate_ginx<true, true>), dim3(blocks), dim3(256), boot_lds(true, true), s, g, t, k,
                                idx, tvb, ext_a, ext_b);
         else
-            hipLaunchKernelGGL((k_blind_rotate_ginx<true, false>), dim3(blocks), dim3(256), boot_lds(true), s, g, t,
+            hipLaunchKernelGGL((k_blind_rotate_ginx<true, false>), dim3(blocks), dim3(256), boot_lds(true, false), s, g, t,
                                k, idx, tvb, ext_a, ext_b);
     } else {
         if (lz)
-            hipLaunchKernelGGL((k_blind_rotate_ginx<false, true>), dim3(blocks), dim3(256), boot_lds(false), s, g, t,
+            hipLaunchKernelGGL((k_blind_rotate_ginx<false, true>), dim3(blocks), dim3(256), boot_lds(false, true), s, g, t,
                                k, idx, tvb, ext_a, ext_b);
         else
-            hipLaunchKernelGGL((k_blind_rotate_ginx<false, false>), dim3(blocks), dim3(256), boot_lds(false), s, g, t,
+            hipLaunchKernelGGL((k_blind_rotate_ginx<false, false>), dim3(blocks), dim3(256), boot_lds(false, false), s, g, t,
                                k, idx, tvb, ext_a, ext_b);
     }
     return hipGetLastError();

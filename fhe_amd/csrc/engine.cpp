@@ -43,13 +43,15 @@ void Engine::build_tables() {
     const uint64_t Q = p_.Q;
     HostNtt h;
     h.init(p_.N, Q, p_.psi);
-    std::vector<uint32_t> t(32 + 32 + 992 + 992 + kMonoHalfWords + kMonoTableWords, 0);
+    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2 * (kMonoHalfWords + kMonoTableWords), 0);
     uint32_t* twAf = t.data();
     uint32_t* twAi = twAf + 32;
     uint32_t* twBf = twAi + 32;
     uint32_t* twBi = twBf + 992;
     uint32_t* mono = twBi + 992;
     uint32_t* monoF = mono + kMonoHalfWords;
+    uint32_t* monoP = monoF + kMonoTableWords;
+    uint32_t* monoPF = monoP + kMonoHalfWords;
     for (int i = 0; i < 32; ++i) {
         twAf[i] = to_mont(h.tab[i], Q);
         twAi[i] = to_mont(h.tabI[i], Q);
@@ -73,11 +75,13 @@ void Engine::build_tables() {
         uint64_t x = 1;
         for (uint32_t f = 0; f <= 2 * p_.N; ++f) {
             mono[f + (f >> 5)] = to_mont(submod(x, 1, Q), Q);
+            monoP[f + (f >> 5)] = (uint32_t)submod(x, 1, Q);
             x = mulmod(x, psi2, Q);
         }
         x = 1;
         for (uint32_t e = 0; e <= 4 * p_.N; ++e) {
             monoF[e + (e >> 5)] = to_mont(submod(x, 1, Q), Q);
+            monoPF[e + (e >> 5)] = (uint32_t)submod(x, 1, Q);
             x = mulmod(x, p_.psi, Q);
         }
     }
@@ -103,11 +107,14 @@ void Engine::build_tables() {
     tabs_.twB_inv = d + 64 + 992;
     tabs_.mono = d + 64 + 1984;                     // kMonoHalfWords words
     tabs_.mono_full = tabs_.mono + kMonoHalfWords;  // kMonoTableWords words
+    tabs_.monoP = tabs_.mono_full + kMonoTableWords;
+    tabs_.monoP_full = tabs_.monoP + kMonoHalfWords;
     tabs_.Q = (uint32_t)Q;
     tabs_.Q2 = (uint32_t)(2 * Q);
     tabs_.qinv = neg_inv32((uint32_t)Q);
     tabs_.ninvR = to_mont(h.ninv, Q);
     tabs_.w1R = to_mont(h.tabI[1], Q);
+    tabs_.oneR = to_mont(1, Q);
 }
 
 void Engine::load_bsk(const uint64_t* bsk, size_t words) {
