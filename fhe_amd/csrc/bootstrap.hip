@@ -59,8 +59,9 @@ constexpr int kAccBoundLZ = 28; // GINX, Q < 2^27: |acc| < 2.8 Q between iterati
 struct Mod {
     uint32_t Q, Q2, qinv;  // qinv = -Q^-1 mod 2^32
     uint32_t qinvp;        // Q^-1 mod 2^32 (signed Montgomery)
+    int32_t nQ;            // -Q (signed Montgomery; see fresh_nq)
 };
-FHE_DEV Mod make_mod(const BootTables& T) { return Mod{T.Q, T.Q2, T.qinv, 0u - T.qinv}; }
+FHE_DEV Mod make_mod(const BootTables& T) { return Mod{T.Q, T.Q2, T.qinv, 0u - T.qinv, -(int32_t)T.Q}; }
 
 // a * bR * 2^-32 mod Q, lazily: result < Q (1 + a / 2^32 * ...) < 2Q for a < 4Q, Q < 2^28
 FHE_DEV uint32_t mont_mul(uint32_t a, uint32_t bR, const Mod& m) {
@@ -95,8 +96,11 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 }
 // v_mad_i64_i32 (a * b + c, 32 x 32 -> 64 signed), emitted explicitly: written as C the compiler
 // sometimes widens a hoisted -Q into a 64-bit constant and expands the product into 5 instructions
+// 2: plain C, with -Q re-materialised inside each loop body (fresh_nq) so that instruction
+// selection sees a sign-extended 32-bit operand; inline asm makes the hazard recognizer put an
+// s_nop after every such instruction (600 per iteration)
 #ifndef FHE_ASM_MAD
-#define FHE_ASM_MAD 1
+#define FHE_ASM_MAD 2
 #endif
 #ifndef FHE_MAC_NEW
 #define FHE_MAC_NEW 1   // LZ: one reduction per slot, acc folded in (signed acc)
@@ -105,7 +109,7 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #define FHE_INV_S 1     // LZ: signed inverse NTT
 #endif
 FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
-#if FHE_ASM_MAD
+#if FHE_ASM_MAD == 1
     int64_t d;
     uint64_t junk;
     asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(junk) : "v"(a), "v"(b), "v"(c));
@@ -119,12 +123,19 @@ FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
 FHE_DEV uint32_t smont_mul(uint32_t a, uint32_t bR, const Mod& m) {
     const int64_t t  = mad_i64_i32((int32_t)a, (int32_t)bR, 0);
     const int32_t mm = (int32_t)((uint32_t)t * m.qinvp);
-    return (uint32_t)(mad_i64_i32(mm, -(int32_t)m.Q, t) >> 32);
+    return (uint32_t)(mad_i64_i32(mm, m.nQ, t) >> 32);
 }
 // signed Montgomery reduction of a 64-bit t, |t| < 2^63 - 2^31 Q: t 2^-32 mod Q in (|t| 2^-32 +- Q/2)
 FHE_DEV uint32_t smont_red(int64_t t, const Mod& m) {
     const int32_t mm = (int32_t)((uint32_t)t * m.qinvp);
-    return (uint32_t)(mad_i64_i32(mm, -(int32_t)m.Q, t) >> 32);
+    return (uint32_t)(mad_i64_i32(mm, m.nQ, t) >> 32);
+}
+// -Q as a value defined inside the current loop body (an empty asm the optimizer cannot hoist)
+FHE_DEV Mod fresh_nq(Mod m) {
+#if FHE_ASM_MAD == 2
+    asm volatile("" : "+s"(m.nQ));
+#endif
+    return m;
 }
 // signed Cooley-Tukey: |x|, |y| < B in, < B + Q out, two adds and no offset
 FHE_DEV void ct_bf_s(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
@@ -538,7 +549,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     if (gate >= g.count) return;  // no workgroup barrier below this point
     uint32_t* tileW = s_tile + wave * 2 * kTile;
     uint32_t* tile  = tileW + h * kTile;
-    const Mod m = make_mod(T);
+    const Mod m0 = make_mod(T);
+    const Mod& m  = m0;
 
     // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[32];
@@ -565,9 +577,12 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     const uint32_t lbase = 2 * brv5(l) + 1;
     const Dec dec        = make_dec(m.Q, g.gbits);
     const uint64_t moff  = 64ull * m.Q * m.Q;
-    const uint2* ki      = bsk + lane;
-    const uint2* kinext  = ki + 2 * 4 * 16 * 64;
+    const uint32_t lofs  = (uint32_t)lane;
     for (uint32_t i = 0; i < g.n; ++i) {
+        const Mod m = fresh_nq(m0);
+        // wave-uniform base + per-lane 32-bit offset: saddr loads with immediate offsets
+        const uint2* kb = bsk + (size_t)i * (2 * 4 * 16 * 64);
+#define ki (kb + lofs)
         uint2 kbuf[FHE_KEY_PF + 1][8];
         const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
         uint32_t dA[32], dB[32];
@@ -699,8 +714,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #undef KP
 #undef KN
         }
-        ki = kinext;
-        kinext += 2 * 4 * 16 * 64;
+#undef ki
     }
 
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
@@ -880,7 +894,8 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     if (gate >= g.count) return;
     uint32_t* tileW = s_tile + wave * 2 * kTile;
     uint32_t* tile  = tileW + h * kTile;
-    const Mod m = make_mod(T);
+    const Mod m0 = make_mod(T);
+    const Mod& m  = m0;
     const uint32_t M = 2 * g.N;
 
     uint32_t acc[32];
@@ -910,6 +925,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     const uint16_t* gops = ops + (size_t)gate * maxops;
     const uint32_t cnt   = nops[gate];
     for (uint32_t it = 0; it < cnt; ++it) {
+        const Mod m       = fresh_nq(m0);
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
         uint32_t dA[32], dB[32];
         if (DM || !(op & 0x8000u)) {
