@@ -60,8 +60,9 @@ struct Mod {
     uint32_t Q, Q2, qinv;  // qinv = -Q^-1 mod 2^32
     uint32_t qinvp;        // Q^-1 mod 2^32 (signed Montgomery)
     int32_t nQ;            // -Q (signed Montgomery; see fresh_nq)
+    uint32_t oneR;         // 2^32 mod Q: smont_mul(x, oneR) = x mod Q in (-Q, Q)
 };
-FHE_DEV Mod make_mod(const BootTables& T) { return Mod{T.Q, T.Q2, T.qinv, 0u - T.qinv, -(int32_t)T.Q}; }
+FHE_DEV Mod make_mod(const BootTables& T) { return Mod{T.Q, T.Q2, T.qinv, 0u - T.qinv, -(int32_t)T.Q, T.oneR}; }
 
 // a * bR * 2^-32 mod Q, lazily: result < Q (1 + a / 2^32 * ...) < 2Q for a < 4Q, Q < 2^28
 FHE_DEV uint32_t mont_mul(uint32_t a, uint32_t bR, const Mod& m) {
@@ -107,6 +108,12 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #endif
 #ifndef FHE_INV_S
 #define FHE_INV_S 1     // LZ: signed inverse NTT
+#endif
+#ifndef FHE_LMK_WAVES
+#define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
+#endif
+#ifndef FHE_LMK_S
+#define FHE_LMK_S 1     // op-list kernel (LMKCDEY, AP/DM): signed residues, Q < 2^28
 #endif
 FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
 #if FHE_ASM_MAD == 1
@@ -225,9 +232,13 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 // LZ (Q < 2^27): signed digits |d| <= 2^(g-1) and signed butterflies -- |v| grows by < Q per
 // stage to < 10Q + 2^(g-1) < 2^31, no reduction anywhere.  Otherwise unsigned digits < 2Q grow by
 // < 2Q per stage; < 12Q is reduced to < 6Q at the transpose (< 16Q out, Q < 2^28).
-template <bool LZ>
+// FM (forward mode): 0 unsigned lazy (above), 1 signed without reduction (Q < 2^27), 2 signed for
+// Q < 2^28: after 5 stages |v| < 5Q + 2^(g-1); the x inputs of the first B' stage (registers 0..15)
+// are reduced to (-Q, Q), so the B' outputs stay < 6Q (a Cooley-Tukey output is bounded by |x| + Q)
+template <int FM>
 FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int l,
                        const uint32_t* __restrict__ twA, const uint32_t* s_twB, const Mod& m) {
+    constexpr bool LZ = FM != 0;
 #pragma unroll
     for (int b = 9; b >= 5; --b) {
         const int rb = b - 5;
@@ -253,6 +264,13 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
     }
     transpose32(v, tile, l);
     transpose32(u, tile, l);
+    if (FM == 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            v[r] = smont_mul(v[r], m.oneR, m);
+            u[r] = smont_mul(u[r], m.oneR, m);
+        }
+    }
 #pragma unroll
     for (int b = 4; b >= 0; --b) {
 #pragma unroll
@@ -270,6 +288,34 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
                 ct_bf(v[r], v[r | (1 << b)], w, m);
                 ct_bf(u[r], u[r | (1 << b)], w, m);
             }
+        }
+    }
+}
+
+// one signed forward pass (FM 1 or 2 as in fwd_pass2): the LMKCDEY automorphism step
+template <int FM>
+FHE_DEV void fwd_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
+                        const uint32_t* s_twB, const Mod& m) {
+#pragma unroll
+    for (int b = 9; b >= 5; --b) {
+        const int rb = b - 5;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            ct_bf_s(v[r], v[r | (1 << rb)], twA[(1 << (9 - b)) + (r >> (rb + 1))], m);
+        }
+    }
+    transpose32(v, tile, l);
+    if (FM == 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = smont_mul(v[r], m.oneR, m);
+    }
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << b)) continue;
+            ct_bf_s(v[r], v[r | (1 << b)], s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l], m);
         }
     }
 }
@@ -327,8 +373,10 @@ struct InvPlanS {
     bool red3[32];     // ... before the last stage (bit 9)
     int fin[16];       // last-stage sum x + y: |.| < 2^fin Q -> add 2^fin Q, then fin + 1 conditional subtractions
 };
-constexpr int kLimS = 160;  // |x| + |y| <= 16 Q < 2^31
-constexpr void plan_half(int (&B)[32], bool (&red)[5][32], int stages) {
+// LIM: the bound on |x| + |y| (units of Q/10) that keeps sums below 2^31: 16 Q for Q < 2^27,
+// 8 Q for Q < 2^28
+constexpr int lim_s(bool lz) { return lz ? 160 : 80; }
+constexpr void plan_half(int (&B)[32], bool (&red)[5][32], int stages, int kLimS) {
     for (int b = 0; b < stages; ++b)
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << b)) continue;
@@ -342,12 +390,12 @@ constexpr void plan_half(int (&B)[32], bool (&red)[5][32], int stages) {
             B[s] = 10;
         }
 }
-template <int BIN>
+template <int BIN, int kLimS>
 constexpr InvPlanS make_inv_plan() {
     InvPlanS p{};
     int B[32] = {};
     for (int r = 0; r < 32; ++r) B[r] = BIN;
-    plan_half(B, p.red1, 5);
+    plan_half(B, p.red1, 5, kLimS);
     int U = 0;
     for (int r = 0; r < 32; ++r) {
         if (B[r] > 20) {
@@ -358,7 +406,7 @@ constexpr InvPlanS make_inv_plan() {
     }
     for (int r = 0; r < 32; ++r) B[r] = U;
     bool red2[5][32] = {};
-    plan_half(B, red2, 4);
+    plan_half(B, red2, 4, kLimS);
     for (int b = 0; b < 4; ++b)
         for (int r = 0; r < 32; ++r) p.red2[b][r] = red2[b][r];
     for (int r = 0; r < 16; ++r) {
@@ -374,11 +422,12 @@ constexpr InvPlanS make_inv_plan() {
     return p;
 }
 
-// B' (EVAL, |inputs| < BIN Q / 10, signed) -> A' (COEF), canonical [0, Q) like inv_pass
-template <int BIN>
+// B' (EVAL, |inputs| < BIN Q / 10, signed) -> A' (COEF), canonical [0, Q) like inv_pass.
+// LZ: Q < 2^27 (sums up to 16 Q), else Q < 2^28 (8 Q; the final 2^(fin+1) Q <= 16 Q < 2^32)
+template <int BIN, bool LZ = true>
 FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
                         const uint32_t* s_twB, uint32_t w1R, uint32_t oneR, const Mod& m) {
-    constexpr InvPlanS P = make_inv_plan<BIN>();
+    constexpr InvPlanS P = make_inv_plan<BIN, lim_s(LZ)>();
 #pragma unroll
     for (int b = 0; b <= 4; ++b) {
 #pragma unroll
@@ -602,7 +651,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #if defined(FHE_ABL) && (FHE_ABL & 32)
         // ablation: no forward passes
 #elif FHE_FWD_FUSED
-        fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+        fwd_pass2<LZ ? 1 : 0>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
 #elif FHE_FWD_SHARED
         // one copy of the forward-pass code for both digit polynomials (instruction-cache
         // footprint): transform dA, swap, transform (old dB), swap back
@@ -875,8 +924,9 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
 
 // DM: the AP/DM accumulator runs the same op loop with external products only (AddToAccDM ==
 // AddToAccLMKCDEY, rgsw-acc-dm.cpp:119-145) and no initial automorphism of acc1.
+// DM needs no automorphism path and fits 168 VGPRs: 3 waves per SIMD
 template <bool DM, bool LZ>
-__global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3 : FHE_LMK_WAVES)))
     k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
                        const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
@@ -921,9 +971,106 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     }
 
     const Dec dec     = make_dec(m.Q, g.gbits);
-    const uint64_t moff = 64ull * m.Q * m.Q;
     const uint16_t* gops = ops + (size_t)gate * maxops;
     const uint32_t cnt   = nops[gate];
+#if FHE_LMK_S
+    // Signed residues throughout (Q < 2^28): acc in (-2Q, 2Q) between ops (one signed Montgomery
+    // reduction of the digit x key sum), signed inverse NTT to canonical COEF, balanced digits as
+    // signed words, signed forward NTT (FM 1 for Q < 2^27, FM 2 above).
+    constexpr int FM = LZ ? 1 : 2;
+    const uint32_t oneRh = h ? m0.oneR : 0u;  // automorphism: half 1 accumulates, half 0 is replaced
+    for (uint32_t it = 0; it < cnt; ++it) {
+        const Mod m       = fresh_nq(m0);
+        // the uniform twiddles re-read per op: hoisted out of the branchy loop they would hold
+        // 62 VGPRs across it (spills)
+        const uint32_t* twAf = T.twA_fwd;
+        const uint32_t* twAi = T.twA_inv;
+        asm volatile("" : "+s"(twAf), "+s"(twAi));
+        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+        uint32_t dA[32], dB[32];
+        if (DM || !(op & 0x8000u)) {
+            // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
+#pragma unroll
+            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
+            inv_pass_s<20, LZ>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
+            fwd_pass2<FM>(dA, dB, tile, l, twAf, s_twBf, m);
+            const uint2* kb = bsk + (size_t)op * (4 * 16 * 64);
+            uint2 kk[2][4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) kk[0][d] = kb[(d * 16 + 0) * 64 + lane];
+#pragma clang loop unroll(full)
+            for (int k = 0; k < 16; ++k) {
+                if (k + 1 < 16) {  // request chunk k+1 while chunk k is consumed
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) kk[(k + 1) & 1][d] = kb[(d * 16 + k + 1) * 64 + lane];
+                }
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * k + e;
+                    auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
+                    // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28): |S| < 40 Q^2 or 24 Q^2, so
+                    // |S| 2^-32 + Q/2 < 2Q
+                    const int64_t S = (int64_t)mac4<true>(p01[0], p01[1], p23[0], p23[1], e ? kk[k & 1][0].y : kk[k & 1][0].x,
+                                                          e ? kk[k & 1][1].y : kk[k & 1][1].x,
+                                                          e ? kk[k & 1][2].y : kk[k & 1][2].x,
+                                                          e ? kk[k & 1][3].y : kk[k & 1][3].x, 0);
+                    acc[r] = smont_red(S, m);
+                }
+            }
+        } else {
+            // ---- Automorphism(5^t or 2N-5, autokey[t])
+            const uint32_t t = op & 0x7fffu;
+            uint32_t kexp    = M - 5;
+            if (t) {
+                kexp = 1;
+                for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
+            }
+            asm volatile("" : "+s"(kexp));  // no reuse of the prologue's (2N - 5) index math (spills)
+            automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
+#pragma unroll
+            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
+            inv_pass_s<20, LZ>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);  // half 0: COEF acc0'
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                decompose2<true>(dA[r], dec, dA[r], dB[r]);
+                // (half 0's digit A, half 0's digit B) -> lower / upper half of dA
+                auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
+                dA[r]   = sw[0];
+            }
+            fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
+            const uint2* kb = autok + (size_t)t * (2 * 16 * 64);
+            uint2 ka[2][2];
+            ka[0][0] = kb[(0 * 16 + 0) * 64 + lane];
+            ka[0][1] = kb[(1 * 16 + 0) * 64 + lane];
+#pragma clang loop unroll(full)
+            for (int k = 0; k < 16; ++k) {
+                if (k + 1 < 16) {
+                    ka[(k + 1) & 1][0] = kb[(0 * 16 + k + 1) * 64 + lane];
+                    ka[(k + 1) & 1][1] = kb[(1 * 16 + k + 1) * 64 + lane];
+                }
+                asm volatile("" ::: "memory");
+                const uint2 k0 = ka[k & 1][0], k1 = ka[k & 1][1];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * k + e;
+                    auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    // |S| < 2 (6Q) Q + 2Q Q -> |acc| < 14 Q^2 2^-32 + Q/2 < 2Q
+                    int64_t S = (int64_t)(int32_t)p[0] * (int32_t)(e ? k0.y : k0.x) +
+                                (int64_t)(int32_t)p[1] * (int32_t)(e ? k1.y : k1.x);
+                    S += (int64_t)(int32_t)acc[r] * (int32_t)oneRh;
+                    acc[r] = smont_red(S, m);
+                }
+            }
+        }
+    }
+    // extraction, identical to GINX
+    inv_pass_s<20, LZ>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m.oneR, m);
+#else
+    const uint64_t moff = 64ull * m.Q * m.Q;
     for (uint32_t it = 0; it < cnt; ++it) {
         const Mod m       = fresh_nq(m0);
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
@@ -935,7 +1082,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2<LZ>(dA[r], dec, dA[r], dB[r]);
-            fwd_pass2<LZ>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+            fwd_pass2<LZ ? 1 : 0>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
             const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
             uint2 kk[2][4];
 #pragma unroll
@@ -1006,6 +1153,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 
     // extraction, identical to GINX
     inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
+#endif
     wave_lds_sync();
     if (h == 0) {
 #pragma unroll
@@ -1047,6 +1195,7 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
     const uint2* k  = reinterpret_cast<const uint2*>(bsk);
     const uint2* ak = reinterpret_cast<const uint2*>(autok);
     const bool lz   = t.Q < (1u << 27);
+    if (t.Q >= (1u << 28)) return hipErrorInvalidValue;  // signed residue bounds (FHE_LMK_S)
     if (dm && lz)
         hipLaunchKernelGGL((k_blind_rotate_lmk<true, true>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
                            maxops, tvb, ext_a, ext_b);
