@@ -31,6 +31,16 @@ struct BootTables {
     uint32_t oneR;   // 2^32 mod Q (Montgomery 1): x -> x mod Q by one signed Montgomery product
 };
 
+// Digit exchange between the half-waves in the external products: 1 = ds_bpermute of the other
+// half's digits, with the key rows of half 1 stored swapped in pairs (row d at position d ^ 1) so
+// that every lane multiplies (own, other) digits in the same order; 0 = v_permlane32_swap (both
+// digit orders in every lane, plain row order).  Engine::load_bsk and the device key generator
+// write the layout this selects.
+#ifndef FHE_XCHG
+#define FHE_XCHG 1
+#endif
+constexpr bool kBskHalfSwap = FHE_XCHG != 0;
+
 struct GateArgs {
     uint32_t count, n, N, q, qKS;
     uint32_t ctmod;                   // modulus of the bootstrapped ct's a (q; 2q for BootstrapFunc), power of 2

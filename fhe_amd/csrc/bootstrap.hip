@@ -112,9 +112,6 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
-#ifndef FHE_LMK_S
-#define FHE_LMK_S 1     // op-list kernel (LMKCDEY, AP/DM): signed residues, Q < 2^28
-#endif
 FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
 #if FHE_ASM_MAD == 1
     int64_t d;
@@ -478,6 +475,9 @@ FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
     }
 }
 
+// the same register of the other half-wave (lane ^ 32), through the LDS crossbar (no VALU)
+FHE_DEV uint32_t other_half(uint32_t x, int xaddr) { return (uint32_t)__builtin_amdgcn_ds_bpermute(xaddr, (int)x); }
+
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 
 // SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = 3: centre x in [0, Q) to
@@ -627,6 +627,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     const Dec dec        = make_dec(m.Q, g.gbits);
     const uint64_t moff  = 64ull * m.Q * m.Q;
     const uint32_t lofs  = (uint32_t)lane;
+    const int xaddr      = (lane ^ 32) << 2;
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m = fresh_nq(m0);
         // wave-uniform base + per-lane 32-bit offset: saddr loads with immediate offsets
@@ -721,9 +722,14 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * k + e;
                 // all four digits in every lane: D0/D1 = digit A of acc0/acc1, D2/D3 = digit B
+#if FHE_XCHG
+                // (own, other) digit order; the half-1 key rows are stored swapped to match
+                const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
+#else
                 auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                 auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
                 const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
+#endif
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
                 const uint32_t u  = __builtin_amdgcn_readfirstlane((as * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & umask) * 66;
                 if (LZ && FHE_MAC_NEW) {
@@ -973,12 +979,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
     const Dec dec     = make_dec(m.Q, g.gbits);
     const uint16_t* gops = ops + (size_t)gate * maxops;
     const uint32_t cnt   = nops[gate];
-#if FHE_LMK_S
     // Signed residues throughout (Q < 2^28): acc in (-2Q, 2Q) between ops (one signed Montgomery
     // reduction of the digit x key sum), signed inverse NTT to canonical COEF, balanced digits as
     // signed words, signed forward NTT (FM 1 for Q < 2^27, FM 2 above).
     constexpr int FM = LZ ? 1 : 2;
     const uint32_t oneRh = h ? m0.oneR : 0u;  // automorphism: half 1 accumulates, half 0 is replaced
+    const int xaddr      = (lane ^ 32) << 2;
     for (uint32_t it = 0; it < cnt; ++it) {
         const Mod m       = fresh_nq(m0);
         // the uniform twiddles re-read per op: hoisted out of the branchy loop they would hold
@@ -1010,11 +1016,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int r = 2 * k + e;
+#if FHE_XCHG
+                    const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
+#else
                     auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                     auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
+                    const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
+#endif
                     // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28): |S| < 40 Q^2 or 24 Q^2, so
                     // |S| 2^-32 + Q/2 < 2Q
-                    const int64_t S = (int64_t)mac4<true>(p01[0], p01[1], p23[0], p23[1], e ? kk[k & 1][0].y : kk[k & 1][0].x,
+                    const int64_t S = (int64_t)mac4<true>(D0, D1, D2, D3, e ? kk[k & 1][0].y : kk[k & 1][0].x,
                                                           e ? kk[k & 1][1].y : kk[k & 1][1].x,
                                                           e ? kk[k & 1][2].y : kk[k & 1][2].x,
                                                           e ? kk[k & 1][3].y : kk[k & 1][3].x, 0);
@@ -1057,10 +1068,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int r = 2 * k + e;
+#if FHE_XCHG
+                    const uint32_t P0 = dA[r], P1 = other_half(dA[r], xaddr);
+#else
                     auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    const uint32_t P0 = p[0], P1 = p[1];
+#endif
                     // |S| < 2 (6Q) Q + 2Q Q -> |acc| < 14 Q^2 2^-32 + Q/2 < 2Q
-                    int64_t S = (int64_t)(int32_t)p[0] * (int32_t)(e ? k0.y : k0.x) +
-                                (int64_t)(int32_t)p[1] * (int32_t)(e ? k1.y : k1.x);
+                    int64_t S = (int64_t)(int32_t)P0 * (int32_t)(e ? k0.y : k0.x) +
+                                (int64_t)(int32_t)P1 * (int32_t)(e ? k1.y : k1.x);
                     S += (int64_t)(int32_t)acc[r] * (int32_t)oneRh;
                     acc[r] = smont_red(S, m);
                 }
@@ -1069,91 +1085,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
     }
     // extraction, identical to GINX
     inv_pass_s<20, LZ>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m.oneR, m);
-#else
-    const uint64_t moff = 64ull * m.Q * m.Q;
-    for (uint32_t it = 0; it < cnt; ++it) {
-        const Mod m       = fresh_nq(m0);
-        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
-        uint32_t dA[32], dB[32];
-        if (DM || !(op & 0x8000u)) {
-            // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
-#pragma unroll
-            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
-#pragma unroll
-            for (int r = 0; r < 32; ++r) decompose2<LZ>(dA[r], dec, dA[r], dB[r]);
-            fwd_pass2<LZ ? 1 : 0>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
-            const uint2* ki = bsk + (size_t)op * (4 * 16 * 64) + lane;
-            uint2 kk[2][4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) kk[0][d] = ki[(d * 16 + 0) * 64];
-#pragma clang loop unroll(full)
-            for (int k = 0; k < 16; ++k) {
-                if (k + 1 < 16) {  // request chunk k+1 while chunk k is consumed
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) kk[(k + 1) & 1][d] = ki[(d * 16 + k + 1) * 64];
-                }
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int r = 2 * k + e;
-                    auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                    auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
-                    const uint64_t S = mac4<LZ>(p01[0], p01[1], p23[0], p23[1], e ? kk[k & 1][0].y : kk[k & 1][0].x,
-                                                e ? kk[k & 1][1].y : kk[k & 1][1].x,
-                                                e ? kk[k & 1][2].y : kk[k & 1][2].x,
-                                                e ? kk[k & 1][3].y : kk[k & 1][3].x, moff);
-                    // digits < 16Q: S < 64 Q^2 -> < 5Q; LZ: S < 105 Q^2 (offset included) -> < 4.3Q
-                    acc[r] = csub(csub(mont_red(S, m), 2 * m.Q2), m.Q2);  // -> [0, 2Q)
-                }
-            }
-        } else {
-            // ---- Automorphism(5^t or 2N-5, autokey[t])
-            const uint32_t t = op & 0x7fffu;
-            uint32_t kexp    = M - 5;
-            if (t) {
-                kexp = 1;
-                for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
-            }
-            automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
-#pragma unroll
-            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);  // half 0: COEF acc0'
-#pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                decompose2<false>(dA[r], dec, dA[r], dB[r]);
-                // (half 0's digit A, half 0's digit B) -> lower / upper half of dA
-                auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
-                dA[r]   = sw[0];
-            }
-            fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
-            const uint2* ki = autok + (size_t)t * (2 * 16 * 64) + lane;
-            uint2 ka[2][2];
-            ka[0][0] = ki[(0 * 16 + 0) * 64];
-            ka[0][1] = ki[(1 * 16 + 0) * 64];
-#pragma clang loop unroll(full)
-            for (int k = 0; k < 16; ++k) {
-                if (k + 1 < 16) {
-                    ka[(k + 1) & 1][0] = ki[(0 * 16 + k + 1) * 64];
-                    ka[(k + 1) & 1][1] = ki[(1 * 16 + k + 1) * 64];
-                }
-                asm volatile("" ::: "memory");
-                const uint2 k0 = ka[k & 1][0], k1 = ka[k & 1][1];
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int r = 2 * k + e;
-                    auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                    uint64_t S = (uint64_t)p[0] * (e ? k0.y : k0.x) + (uint64_t)p[1] * (e ? k1.y : k1.x);
-                    const uint32_t v = csub(mont_red(S, m), m.Q2);     // < 2.75Q -> < 2Q
-                    acc[r] = h ? csub(acc[r] + v, m.Q2) : v;           // [0, 2Q)
-                }
-            }
-        }
-    }
-
-    // extraction, identical to GINX
-    inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
-#endif
     wave_lds_sync();
     if (h == 0) {
 #pragma unroll
@@ -1195,7 +1126,7 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
     const uint2* k  = reinterpret_cast<const uint2*>(bsk);
     const uint2* ak = reinterpret_cast<const uint2*>(autok);
     const bool lz   = t.Q < (1u << 27);
-    if (t.Q >= (1u << 28)) return hipErrorInvalidValue;  // signed residue bounds (FHE_LMK_S)
+    if (t.Q >= (1u << 28)) return hipErrorInvalidValue;  // signed residue bounds
     if (dm && lz)
         hipLaunchKernelGGL((k_blind_rotate_lmk<true, true>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
                            maxops, tvb, ext_a, ext_b);

@@ -124,7 +124,8 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     const uint64_t Q = p_.Q;
     if (dG2 != 4) throw std::invalid_argument("device path expects digitsG = 3");
     // device uint2 blocks [..][d][16][64 lanes]: lane = h*32 + l holds slots l*32 + 2k, +1 of
-    // component h -- one 512-byte coalesced load per wave-instruction in the kernels.
+    // component h -- one 512-byte coalesced load per wave-instruction in the kernels.  With
+    // kBskHalfSwap the half-1 lanes of position d hold row d ^ 1 (rows come in pairs).
     //   GINX   raw [n][2][dG2][2][N]                 -> [n][2][dG2][16][64]
     //   LMKCDEY raw [n][dG2][2][N] ++ [nA+1][2][2][N] -> [n][dG2][16][64] ++ [nA+1][2][16][64]
     //   AP     raw [n][baseR][digitsR][dG2][2][N]    -> [n][baseR][digitsR][dG2][16][64]
@@ -141,7 +142,8 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
             for (uint32_t k = 0; k < 16; ++k)
                 for (uint32_t lane = 0; lane < 64; ++lane) {
                     const uint32_t h = lane >> 5, l = lane & 31;
-                    const size_t src = ((size_t)d * 2 + h) * N + l * 32 + 2 * k;
+                    const uint32_t row = kBskHalfSwap ? d ^ h : d;  // boot.h FHE_XCHG
+                    const size_t src = ((size_t)row * 2 + h) * N + l * 32 + 2 * k;
                     const size_t dst = (((size_t)d * 16 + k) * 64 + lane) * 2;
                     dst_key[dst] = to_mont(mulmod(src_key[src] % Q, ninv, Q), Q);
                     dst_key[dst + 1] = to_mont(mulmod(src_key[src + 1] % Q, ninv, Q), Q);

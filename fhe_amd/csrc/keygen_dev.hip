@@ -99,7 +99,9 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
         // ((kk * 64 + h * 32 + l) * 2 + e), values x * N^-1 in Montgomery form (* 2^32 mod Q)
         const uint32_t l = j >> 5, kk = (j & 31) >> 1, el = j & 1;
         bsk[base + ((kk * 64 + l) * 2 + el)] = (uint32_t)((((r0 * ninv) % Q) << 32) % Q);
-        bsk[base + ((kk * 64 + 32 + l) * 2 + el)] = (uint32_t)((((r1 * ninv) % Q) << 32) % Q);
+        // component 1 of row rp sits at position rp ^ 1 with kBskHalfSwap (boot.h FHE_XCHG)
+        const size_t base1 = (size_t)(kBskHalfSwap ? k.rp ^ 1 : k.rp) * 2 * N;
+        bsk[base1 + ((kk * 64 + 32 + l) * 2 + el)] = (uint32_t)((((r1 * ninv) % Q) << 32) % Q);
         if (raw) {
             raw[base + j] = r0;
             raw[base + N + j] = r1;

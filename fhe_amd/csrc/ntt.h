@@ -14,6 +14,10 @@ struct NttPlan {
     void* d_tab_fwd = nullptr;
     void* d_tab_inv = nullptr;
     uint64_t ninv = 0, ninv_pre = 0, w1ninv = 0, w1ninv_pre = 0;
+    // Q < 2^27: Table / TableI in Montgomery form (u32, x 2^32 mod Q) for the signed kernel
+    void* d_tabm_fwd = nullptr;
+    void* d_tabm_inv = nullptr;
+    uint32_t qinvp = 0, oneR = 0, ninvR = 0, w1ninvR = 0;
     int device = 0;
     int cus = 256;      // compute units of the device (grid sizing)
 };

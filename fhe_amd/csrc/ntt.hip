@@ -258,6 +258,381 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One polynomial per wave64 (32-bit path, Q < 2^30): 16 coefficients per lane, so a 4096-poly
+// batch is 4096 waves (4 per SIMD) instead of 2048 pairs, and the butterflies of the polynomials
+// whose reads have landed overlap the reads and writes of the others.  Index x (10 bits):
+//   layout A: lane L = x5..x0,              register r  = x9..x6      (coalesced 8-byte rows)
+//   layout B: lane L = (x9..x6) << 2 | x1x0, register r' = x5..x2
+//   layout C: lane L = x7..x2,              register r'' = (x9x8) << 2 | x1x0  (4 consecutive words)
+// Forward: A (stages 9..6, uniform twiddles) -> T1 -> B (stages 5..2) -> T2 -> C (stages 1, 0)
+// -> stores of 4 consecutive u64 per lane and x9x8.  Inverse: the mirror image, C -> B -> A.
+// LDS word address of x in both transposes: x + 4 (x >> 6) (conflict-free for the dword accesses
+// of A and B; C reads/writes 16-byte runs).
+// ---------------------------------------------------------------------------------------------
+#ifndef FHE_NTT_T3
+#define FHE_NTT_T3 1   // k_ntt1024w: global rows in layout A both ways (third LDS transpose)
+#endif
+namespace {
+constexpr int kWTile = 1024 + 64;  // words per wave
+FHE_DEV int wt(int x) { return x + ((x >> 6) << 2); }
+
+// arithmetic policies of k_ntt1024w: Shoup lazy (any Q < 2^30) or signed Montgomery (Q < 2^27:
+// five VALU instructions per butterfly, no reductions in the forward transform)
+struct NttK {
+    uint32_t Q;
+    uint2 lo, hi;                           // Shoup: (N^-1, pre), (w1 N^-1, pre)
+    uint32_t qinvp, oneR, ninvR, w1ninvR;   // signed: Q^-1 mod 2^32, 2^32 mod Q, Montgomery N^-1, w1 N^-1
+};
+struct ShoupA {
+    using TW = uint2;
+    static constexpr bool kSigned = false;
+    ModT<uint32_t> m;
+    uint2 lo, hi;
+    FHE_DEV explicit ShoupA(const NttK& k) : m{k.Q, 2 * k.Q}, lo(k.lo), hi(k.hi) {}
+    FHE_DEV void refresh() {}
+    FHE_DEV void ct(uint32_t& x, uint32_t& y, TW w) const { m.ct(x, y, w); }
+    FHE_DEV void gs(uint32_t& x, uint32_t& y, TW w) const { m.gs(x, y, w); }
+    FHE_DEV void gs_last(uint32_t& x, uint32_t& y) const { m.gs_last(x, y, lo, hi); }
+    FHE_DEV uint32_t fwd_out(uint32_t x) const { return m.fwd_out(x); }
+    FHE_DEV uint32_t red(uint32_t x) const { return x; }
+    // two consecutive twiddles
+    FHE_DEV static void tw2(const TW* p, TW& a, TW& b) {
+        const uint4 q = *reinterpret_cast<const uint4*>(p);
+        a = make_uint2(q.x, q.y);
+        b = make_uint2(q.z, q.w);
+    }
+};
+struct SignedA {
+    using TW = uint32_t;
+    static constexpr bool kSigned = true;
+    uint32_t Q, qinvp, oneR, ninvR, w1R;
+    int32_t nQ;
+    FHE_DEV explicit SignedA(const NttK& k)
+        : Q(k.Q), qinvp(k.qinvp), oneR(k.oneR), ninvR(k.ninvR), w1R(k.w1ninvR), nQ(-(int32_t)k.Q) {}
+    // -Q defined inside the caller's loop body, so that its sign extension is not hoisted out of
+    // the loop (a hoisted 64-bit constant turns each product below into a 64 x 64 multiply)
+    FHE_DEV void refresh() { asm volatile("" : "+s"(nQ)); }
+    // a b 2^-32 mod Q in (-Q, Q) for |a| < 2^31 (a read as signed), bR < Q
+    FHE_DEV uint32_t mul(uint32_t a, uint32_t bR) const {
+        const int64_t t  = (int64_t)(int32_t)a * (int32_t)bR;
+        const int32_t mm = (int32_t)((uint32_t)t * qinvp);
+        return (uint32_t)((t + (int64_t)mm * nQ) >> 32);
+    }
+    FHE_DEV uint32_t canon(uint32_t r) const { return min(r, r + Q); }  // (-Q, Q) -> [0, Q)
+    FHE_DEV void ct(uint32_t& x, uint32_t& y, TW w) const {
+        const uint32_t t = mul(y, w);
+        y = x - t;
+        x = x + t;
+    }
+    FHE_DEV void gs(uint32_t& x, uint32_t& y, TW w) const {
+        const uint32_t t = x + y;
+        y = mul(x - y, w);
+        x = t;
+    }
+    FHE_DEV void gs_last(uint32_t& x, uint32_t& y) const {
+        const uint32_t s = x + y, d = x - y;
+        x = canon(mul(s, ninvR));
+        y = canon(mul(d, w1R));
+    }
+    FHE_DEV uint32_t fwd_out(uint32_t x) const { return canon(mul(x, oneR)); }
+    FHE_DEV uint32_t red(uint32_t x) const { return mul(x, oneR); }
+    FHE_DEV static void tw2(const TW* p, TW& a, TW& b) {
+        const uint2 q = *reinterpret_cast<const uint2*>(p);
+        a = q.x;
+        b = q.y;
+    }
+};
+
+// signed inverse: |x| + |y| of every butterfly must stay < 2^31 = 16 Q (units of Q/10 below);
+// before stage s (execution order: C bit 0, C bit 1, B bits 0..3, A bits 0..2, last) register r is
+// reduced to (-Q, Q) when red[s][r].  Bounds are uniform over a register within a layout and
+// become the maximum at a transpose.
+struct InvPlanW {
+    bool red[10][16];
+};
+constexpr InvPlanW make_inv_plan_w() {
+    InvPlanW p{};
+    int B[16] = {};
+    for (int r = 0; r < 16; ++r) B[r] = 10;
+    const int bits[10] = {0, 1, 0, 1, 2, 3, 0, 1, 2, 3};
+    for (int st = 0; st < 10; ++st) {
+        if (st == 2 || st == 6) {
+            int U = 0;
+            for (int r = 0; r < 16; ++r) U = B[r] > U ? B[r] : U;
+            for (int r = 0; r < 16; ++r) B[r] = U;
+        }
+        const int bt = bits[st];
+        for (int r = 0; r < 16; ++r) {
+            if (r & (1 << bt)) continue;
+            const int q = r | (1 << bt);
+            while (B[r] + B[q] > 160) {
+                const int e  = B[r] >= B[q] ? r : q;
+                B[e]         = 10;
+                p.red[st][e] = true;
+            }
+            B[r] = B[r] + B[q];
+            B[q] = 10;
+        }
+    }
+    return p;
+}
+
+template <bool INV, class A>
+__global__ void __launch_bounds__(512)
+    k_ntt1024w(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
+               const typename A::TW* __restrict__ tab, NttK K) {
+    using TW = typename A::TW;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    TW* s_tw        = reinterpret_cast<TW*>(smem);                            // 1024 entries
+    uint32_t* tiles = reinterpret_cast<uint32_t*>(smem + 1024 * sizeof(TW));  // 8 x kWTile
+    const A a0(K);
+    constexpr InvPlanW P = make_inv_plan_w();
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) s_tw[i] = tab[i];
+
+    const int L     = threadIdx.x & 63;
+    const int wv    = threadIdx.x >> 6;
+    uint32_t* tile  = tiles + wv * kWTile;
+    const int G = L >> 2, j = L & 3;  // layout B lane fields
+    const uint32_t W = gridDim.x * (blockDim.x >> 6);
+    uint32_t poly    = blockIdx.x * (blockDim.x >> 6) + wv;
+    auto rowp        = [&](uint32_t p) -> uint32_t { return p < count ? p : count - 1; };
+
+    // raw loads: forward reads layout A (one dword -- the low word -- of 16 u64 rows of 512 B),
+    // inverse reads layout C (the (lo, hi) words of 4 consecutive u64 per x9x8: 16-byte loads)
+    using Raw = uint4[8];
+    auto load = [&](Raw& buf, uint32_t p) {
+        const uint64_t* src = in + (size_t)rowp(p) * 1024;
+        if (!INV || FHE_NTT_T3) {
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                buf[r].x = s32[2 * ((2 * r) * 64 + L)];
+                buf[r].y = s32[2 * ((2 * r + 1) * 64 + L)];
+            }
+        } else {
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                buf[2 * hh]     = *reinterpret_cast<const uint4*>(src + (hh << 8) + (L << 2));
+                buf[2 * hh + 1] = *reinterpret_cast<const uint4*>(src + (hh << 8) + (L << 2) + 2);
+            }
+        }
+    };
+    auto step = [&](Raw& buf, uint32_t p) {
+        A m = a0;
+        m.refresh();
+        uint32_t v[16];
+        if (!INV) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                v[2 * r]     = buf[r].x;
+                v[2 * r + 1] = buf[r].y;
+            }
+            // A: stages 9..6 on register bits 3..0 (r = x9..x6)
+#pragma unroll
+            for (int b = 9; b >= 6; --b) {
+                const int rb = b - 6;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.ct(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            // T1: A -> B
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tile[wt((r << 6) | L)] = v[r];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = tile[wt((G << 6) | (r << 2) | j)];
+            // B: stages 5..2 on register bits 3..0 (r' = x5..x2)
+#pragma unroll
+            for (int b = 5; b >= 2; --b) {
+                const int rb = b - 2;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.ct(v[r], v[r | (1 << rb)], s_tw[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            // T2: B -> C (16-byte runs)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tile[wt((G << 6) | (r << 2) | j)] = v[r];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const uint4 q = *reinterpret_cast<const uint4*>(tile + wt((hh << 8) | (L << 2)));
+                v[4 * hh] = q.x; v[4 * hh + 1] = q.y; v[4 * hh + 2] = q.z; v[4 * hh + 3] = q.w;
+            }
+            // C: stage 1 (pairs j, j ^ 2) and stage 0 (j, j ^ 1)
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const TW w1 = s_tw[256 + (hh << 6) + L];
+                m.ct(v[4 * hh], v[4 * hh + 2], w1);
+                m.ct(v[4 * hh + 1], v[4 * hh + 3], w1);
+                TW w0a, w0b;
+                A::tw2(s_tw + 512 + (hh << 7) + (L << 1), w0a, w0b);
+                m.ct(v[4 * hh], v[4 * hh + 1], w0a);
+                m.ct(v[4 * hh + 2], v[4 * hh + 3], w0b);
+            }
+            uint64_t* dst = out + (size_t)rowp(p) * 1024;
+#if FHE_NTT_T3
+            // T3: C -> A, then coalesced 512-byte rows
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh)
+                *reinterpret_cast<uint4*>(tile + wt((hh << 8) | (L << 2))) =
+                    make_uint4(m.fwd_out(v[4 * hh]), m.fwd_out(v[4 * hh + 1]), m.fwd_out(v[4 * hh + 2]), m.fwd_out(v[4 * hh + 3]));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dst[(r << 6) + L] = (uint64_t)tile[wt((r << 6) | L)];
+#else
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                *reinterpret_cast<uint4*>(dst + (hh << 8) + (L << 2)) = make_uint4(m.fwd_out(v[4 * hh]), 0, m.fwd_out(v[4 * hh + 1]), 0);
+                *reinterpret_cast<uint4*>(dst + (hh << 8) + (L << 2) + 2) = make_uint4(m.fwd_out(v[4 * hh + 2]), 0, m.fwd_out(v[4 * hh + 3]), 0);
+            }
+#endif
+        } else {
+#if FHE_NTT_T3
+            // T3^-1: A (coalesced rows) -> C
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                tile[wt(((2 * r) << 6) | L)]     = buf[r].x;
+                tile[wt(((2 * r + 1) << 6) | L)] = buf[r].y;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const uint4 q = *reinterpret_cast<const uint4*>(tile + wt((hh << 8) | (L << 2)));
+                v[4 * hh] = q.x; v[4 * hh + 1] = q.y; v[4 * hh + 2] = q.z; v[4 * hh + 3] = q.w;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                v[4 * hh]     = buf[2 * hh].x;
+                v[4 * hh + 1] = buf[2 * hh].z;
+                v[4 * hh + 2] = buf[2 * hh + 1].x;
+                v[4 * hh + 3] = buf[2 * hh + 1].z;
+            }
+#endif
+            // C: stage 0 then stage 1 (GS); signed: planned reductions (InvPlanW)
+            auto redp = [&](int st) {
+                if (A::kSigned) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (P.red[st][r]) v[r] = m.red(v[r]);
+                }
+            };
+            redp(0);
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                TW w0a, w0b;
+                A::tw2(s_tw + 512 + (hh << 7) + (L << 1), w0a, w0b);
+                m.gs(v[4 * hh], v[4 * hh + 1], w0a);
+                m.gs(v[4 * hh + 2], v[4 * hh + 3], w0b);
+            }
+            redp(1);
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const TW w1 = s_tw[256 + (hh << 6) + L];
+                m.gs(v[4 * hh], v[4 * hh + 2], w1);
+                m.gs(v[4 * hh + 1], v[4 * hh + 3], w1);
+            }
+            // T2^-1: C -> B
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh)
+                *reinterpret_cast<uint4*>(tile + wt((hh << 8) | (L << 2))) = make_uint4(v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = tile[wt((G << 6) | (r << 2) | j)];
+            // B: stages 2..5
+#pragma unroll
+            for (int b = 2; b <= 5; ++b) {
+                const int rb = b - 2;
+                redp(b);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.gs(v[r], v[r | (1 << rb)], s_tw[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            // T1^-1: B -> A
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tile[wt((G << 6) | (r << 2) | j)] = v[r];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = tile[wt((r << 6) | L)];
+            // A: stages 6..8, then bit 9 with N^-1 folded (transformnat-impl.h:599-623)
+#pragma unroll
+            for (int b = 6; b <= 8; ++b) {
+                const int rb = b - 6;
+                redp(b);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.gs(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            redp(9);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) m.gs_last(v[r], v[r | 8]);
+            uint64_t* dst = out + (size_t)rowp(p) * 1024;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dst[(r << 6) + L] = (uint64_t)v[r];
+        }
+        // the next step's T1 / T2^-1 writes reuse the tile
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    Raw bufA, bufB;
+    if (poly < count) load(bufA, poly);
+    __syncthreads();  // s_tw ready
+    for (; poly < count; poly += 2 * W) {
+        load(bufB, poly + W);
+        __builtin_amdgcn_sched_barrier(0);
+        step(bufA, poly);
+        if (poly + W >= count) break;
+        load(bufA, poly + 2 * W);
+        __builtin_amdgcn_sched_barrier(0);
+        step(bufB, poly + W);
+    }
+}
+}  // namespace
+
+#ifndef FHE_NTT_WAVE
+#define FHE_NTT_WAVE 1   // 32-bit path: one polynomial per wave (k_ntt1024w)
+#endif
+#ifndef FHE_NTT_SIGNED
+#define FHE_NTT_SIGNED 1 // k_ntt1024w: signed Montgomery arithmetic for Q < 2^27
+#endif
+#ifndef FHE_NTT_WWPS
+#define FHE_NTT_WWPS 5   // k_ntt1024w: resident waves per SIMD the grid is sized for
+#endif
+
 #ifndef FHE_NTT_WPS
 #define FHE_NTT_WPS 2   // resident waves per SIMD the grid is sized for
 #endif
@@ -289,9 +664,36 @@ static hipError_t launch(const NttPlan& p, const uint64_t* in, uint64_t* out, ui
     return hipGetLastError();
 }
 
+static hipError_t launch_wave(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
+                              hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const bool sg = FHE_NTT_SIGNED && p.d_tabm_fwd != nullptr;  // Q < 2^27
+    // 8 waves (polynomials) per workgroup; twiddles (8 or 4 KB) + 8 tiles of 4.25 KB
+    const size_t sm       = 1024 * (sg ? 4 : 8) + (size_t)8 * kWTile * 4;
+    const uint32_t groups = (count + 7) / 8;
+    const uint32_t cap    = (uint32_t)p.cus * 4 * FHE_NTT_WWPS / 8;
+    dim3 grid(groups < cap ? groups : cap), block(512);
+    NttK k{};
+    k.Q  = (uint32_t)p.Q;
+    k.lo = uint2{(uint32_t)p.ninv, (uint32_t)p.ninv_pre};
+    k.hi = uint2{(uint32_t)p.w1ninv, (uint32_t)p.w1ninv_pre};
+    k.qinvp = p.qinvp; k.oneR = p.oneR; k.ninvR = p.ninvR; k.w1ninvR = p.w1ninvR;
+    if (sg) {
+        const uint32_t* tab = static_cast<const uint32_t*>(inverse ? p.d_tabm_inv : p.d_tabm_fwd);
+        if (inverse) hipLaunchKernelGGL((k_ntt1024w<true, SignedA>), grid, block, sm, s, in, out, count, tab, k);
+        else hipLaunchKernelGGL((k_ntt1024w<false, SignedA>), grid, block, sm, s, in, out, count, tab, k);
+    } else {
+        const uint2* tab = reinterpret_cast<const uint2*>(inverse ? p.d_tab_inv : p.d_tab_fwd);
+        if (inverse) hipLaunchKernelGGL((k_ntt1024w<true, ShoupA>), grid, block, sm, s, in, out, count, tab, k);
+        else hipLaunchKernelGGL((k_ntt1024w<false, ShoupA>), grid, block, sm, s, in, out, count, tab, k);
+    }
+    return hipGetLastError();
+}
+
 hipError_t ntt1024_launch(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                           hipStream_t s) {
     if (p.wide) return launch<uint64_t>(p, in, out, count, inverse, s);
+    if (FHE_NTT_WAVE) return launch_wave(p, in, out, count, inverse, s);
     return launch<uint32_t>(p, in, out, count, inverse, s);
 }
 

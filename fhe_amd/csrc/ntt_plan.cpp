@@ -33,6 +33,24 @@ hipError_t ntt_plan_init(NttPlan& p, uint64_t Q, uint64_t psi, uint32_t N, int d
         if ((e = hipMalloc(&p.d_tab_inv, iv.size() * 4)) != hipSuccess) return e;
         if ((e = hipMemcpy(p.d_tab_fwd, f.data(), f.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
         if ((e = hipMemcpy(p.d_tab_inv, iv.data(), iv.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+        if (Q < (1ull << 27)) {
+            auto mont = [&](uint64_t x) { return (uint32_t)(((x % Q) << 32) % Q); };
+            std::vector<uint32_t> fm(N), im(N);
+            for (uint32_t i = 0; i < N; ++i) {
+                fm[i] = mont(h.tab[i]);
+                im[i] = mont(h.tabI[i]);
+            }
+            uint32_t inv = 1;  // Q^-1 mod 2^32 by Newton iteration
+            for (int k = 0; k < 5; ++k) inv *= 2u - (uint32_t)Q * inv;
+            p.qinvp = inv;
+            p.oneR = mont(1);
+            p.ninvR = mont(p.ninv);
+            p.w1ninvR = mont(p.w1ninv);
+            if ((e = hipMalloc(&p.d_tabm_fwd, N * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&p.d_tabm_inv, N * 4)) != hipSuccess) return e;
+            if ((e = hipMemcpy(p.d_tabm_fwd, fm.data(), N * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+            if ((e = hipMemcpy(p.d_tabm_inv, im.data(), N * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+        }
     } else {
         std::vector<uint64_t> f(2 * N), iv(2 * N);
         for (uint32_t i = 0; i < N; ++i) {
@@ -52,7 +70,9 @@ hipError_t ntt_plan_init(NttPlan& p, uint64_t Q, uint64_t psi, uint32_t N, int d
 void ntt_plan_free(NttPlan& p) {
     if (p.d_tab_fwd) (void)hipFree(p.d_tab_fwd);
     if (p.d_tab_inv) (void)hipFree(p.d_tab_inv);
-    p.d_tab_fwd = p.d_tab_inv = nullptr;
+    if (p.d_tabm_fwd) (void)hipFree(p.d_tabm_fwd);
+    if (p.d_tabm_inv) (void)hipFree(p.d_tabm_inv);
+    p.d_tab_fwd = p.d_tab_inv = p.d_tabm_fwd = p.d_tabm_inv = nullptr;
 }
 
 }  // namespace fhe_amd
