@@ -40,6 +40,16 @@ struct BootTables {
 #define FHE_XCHG 1
 #endif
 constexpr bool kBskHalfSwap = FHE_XCHG != 0;
+// GINX: the two ternary keys of an index (BSK+ / BSK-) interleaved per lane as one 16-byte
+// vector (K+[2k], K+[2k+1], K-[2k], K-[2k+1]) per digit row and slot pair: one load per digit
+#ifndef FHE_GINX_U4
+#define FHE_GINX_U4 1
+#endif
+constexpr bool kGinxU4 = FHE_GINX_U4 != 0;
+// word offset, within index i's 2 * dG2 * 2N words, of (sign ks, row d, slot pair k, lane, e)
+__host__ __device__ constexpr size_t ginx_u4_off(uint32_t ks, uint32_t d, uint32_t k, uint32_t lane, uint32_t e) {
+    return (((size_t)d * 16 + k) * 64 + lane) * 4 + ks * 2 + e;
+}
 
 struct GateArgs {
     uint32_t count, n, N, q, qKS;

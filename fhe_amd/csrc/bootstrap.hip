@@ -29,7 +29,7 @@
 #define FHE_BF_GROUP 0   // >0: sched_barrier after every FHE_BF_GROUP butterflies (bounds live temps)
 #endif
 #ifndef FHE_KEY_PF
-#define FHE_KEY_PF 1     // key chunks (2 slots each) requested ahead of use in the CMUX loop
+#define FHE_KEY_PF 2     // key chunks (2 slots each) requested ahead of use in the CMUX loop
 #endif
 #ifndef FHE_FWD_FUSED
 #define FHE_FWD_FUSED 1
@@ -683,6 +683,24 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         const uint32_t Pp = el + (el >> 5);                    // index el + 64k       -> Pp + 66k
         const uint32_t gl = eper - el;
         const uint32_t Pn = gl + (gl >> 5);                    // index eper - el - 64k -> Pn - 66k
+#if FHE_GINX_U4
+        // one 16-byte vector per digit row and slot pair: (K+[2k], K+[2k+1], K-[2k], K-[2k+1])
+        const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)i * (4 * 16 * 64);
+        uint4 kq[FHE_KEY_PF + 1][4];
+#pragma unroll
+        for (int k = 0; k < FHE_KEY_PF; ++k)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) kq[k][d] = kb4[(d * 16 + k) * 64 + lofs];
+#pragma clang loop unroll(full)
+        for (int k = 0; k < 16; ++k) {
+            if (k + FHE_KEY_PF < 16) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) kq[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d] = kb4[(d * 16 + k + FHE_KEY_PF) * 64 + lofs];
+            }
+            asm volatile("" ::: "memory");
+#define KP(d) make_uint2(kq[k % (FHE_KEY_PF + 1)][d].x, kq[k % (FHE_KEY_PF + 1)][d].y)
+#define KN(d) make_uint2(kq[k % (FHE_KEY_PF + 1)][d].z, kq[k % (FHE_KEY_PF + 1)][d].w)
+#else
 #if FHE_KEY_PF > 0
 #pragma unroll
         for (int k = 0; k < FHE_KEY_PF; ++k)
@@ -718,6 +736,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             asm volatile("" ::: "memory");
 #define KP(d) kbuf[k % (FHE_KEY_PF + 1)][d]
 #define KN(d) kbuf[k % (FHE_KEY_PF + 1)][4 + (d)]
+#endif
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * k + e;

@@ -149,9 +149,28 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
                     dst_key[dst + 1] = to_mont(mulmod(src_key[src + 1] % Q, ninv, Q), Q);
                 }
     };
+    if (kGinxU4 && p_.method == M_GINX) {
+        // (BSK+, BSK-) of index i interleaved per lane (boot.h ginx_u4_off)
 #pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < (int64_t)nrgsw; ++i)
-        pack(bsk + (size_t)i * dG2 * 2 * N, dG2, dev.data() + (size_t)i * dG2 * 2 * N);
+        for (int64_t i = 0; i < (int64_t)n; ++i)
+            for (uint32_t ks = 0; ks < 2; ++ks) {
+                const uint64_t* src_key = bsk + ((size_t)i * 2 + ks) * dG2 * 2 * N;
+                uint32_t* dst_key = dev.data() + (size_t)i * 2 * dG2 * 2 * N;
+                for (uint32_t d = 0; d < dG2; ++d)
+                    for (uint32_t k = 0; k < 16; ++k)
+                        for (uint32_t lane = 0; lane < 64; ++lane) {
+                            const uint32_t h = lane >> 5, l = lane & 31;
+                            const uint32_t row = kBskHalfSwap ? d ^ h : d;
+                            const size_t src = ((size_t)row * 2 + h) * N + l * 32 + 2 * k;
+                            for (uint32_t e = 0; e < 2; ++e)
+                                dst_key[ginx_u4_off(ks, d, k, lane, e)] = to_mont(mulmod(src_key[src + e] % Q, ninv, Q), Q);
+                        }
+            }
+    } else {
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < (int64_t)nrgsw; ++i)
+            pack(bsk + (size_t)i * dG2 * 2 * N, dG2, dev.data() + (size_t)i * dG2 * 2 * N);
+    }
     const uint64_t* asrc = bsk + nrgsw * dG2 * 2 * N;
     uint32_t* adst = dev.data() + nrgsw * dG2 * 2 * N;
     for (size_t t = 0; t < nauto; ++t) pack(asrc + t * dA * 2 * N, dA, adst + t * dA * 2 * N);

@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
                                                    const uint64_t* __restrict__ skAuto,
                                                    const uint64_t* __restrict__ A, const uint64_t* __restrict__ T,
                                                    uint64_t ninv, uint32_t* __restrict__ bsk,
-                                                   uint64_t* __restrict__ raw) {
+                                                   uint64_t* __restrict__ raw, uint32_t ginx_u4) {
     const KgDesc k = D[blockIdx.x];
     const uint64_t* a = A + (size_t)blockIdx.x * N;
     const uint64_t* e = T + (size_t)blockIdx.x * 2 * N;
@@ -98,10 +98,18 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
         // engine layout (Engine::load_bsk): slot c = l*32 + 2kk + e of component h at
         // ((kk * 64 + h * 32 + l) * 2 + e), values x * N^-1 in Montgomery form (* 2^32 mod Q)
         const uint32_t l = j >> 5, kk = (j & 31) >> 1, el = j & 1;
-        bsk[base + ((kk * 64 + l) * 2 + el)] = (uint32_t)((((r0 * ninv) % Q) << 32) % Q);
+        const uint32_t v0 = (uint32_t)((((r0 * ninv) % Q) << 32) % Q), v1 = (uint32_t)((((r1 * ninv) % Q) << 32) % Q);
         // component 1 of row rp sits at position rp ^ 1 with kBskHalfSwap (boot.h FHE_XCHG)
-        const size_t base1 = (size_t)(kBskHalfSwap ? k.rp ^ 1 : k.rp) * 2 * N;
-        bsk[base1 + ((kk * 64 + 32 + l) * 2 + el)] = (uint32_t)((((r1 * ninv) % Q) << 32) % Q);
+        const uint32_t rp1 = kBskHalfSwap ? k.rp ^ 1 : k.rp;
+        if (ginx_u4) {
+            // rp = (2 i + ks) dG2 + row with dG2 = 4 (boot.h ginx_u4_off)
+            const size_t bi = (size_t)(k.rp >> 3) * 16 * N;
+            bsk[bi + ginx_u4_off((k.rp >> 2) & 1, k.rp & 3, kk, l, el)]       = v0;
+            bsk[bi + ginx_u4_off((k.rp >> 2) & 1, rp1 & 3, kk, 32 + l, el)]   = v1;
+        } else {
+            bsk[base + ((kk * 64 + l) * 2 + el)]                  = v0;
+            bsk[(size_t)rp1 * 2 * N + ((kk * 64 + 32 + l) * 2 + el)] = v1;
+        }
         if (raw) {
             raw[base + j] = r0;
             raw[base + N + j] = r1;
@@ -258,7 +266,8 @@ void keygen_bootstrap_device(const Params& p, const std::vector<uint64_t>& sk, u
         k_kg_sample<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dA.p, dT.p);
         FHE_HIP_CHECK(hipGetLastError());
         FHE_HIP_CHECK(ntt1024_launch(plan, dT.p, dT.p, 2 * nc, false, s));
-        k_kg_finish<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dS.p, dAuto.p, dA.p, dT.p, invmod(N, Q), d_bsk, raw_bsk);
+        k_kg_finish<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dS.p, dAuto.p, dA.p, dT.p, invmod(N, Q), d_bsk, raw_bsk,
+                                       (kGinxU4 && p.method == M_GINX) ? 1u : 0u);
         FHE_HIP_CHECK(hipGetLastError());
     }
 
