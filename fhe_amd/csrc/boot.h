@@ -46,6 +46,16 @@ constexpr bool kBskHalfSwap = FHE_XCHG != 0;
 #define FHE_GINX_U4 1
 #endif
 constexpr bool kGinxU4 = FHE_GINX_U4 != 0;
+// op-list methods (LMKCDEY, AP/DM, automorphism keys): the 4 slots l*32 + 4kk .. +3 of a lane as
+// one 16-byte vector per row; word offset within a key of (row d, slot pair k = 0..15, lane, e)
+#ifndef FHE_ROW_U4
+#define FHE_ROW_U4 1
+#endif
+constexpr bool kRowU4 = FHE_ROW_U4 != 0;
+__host__ __device__ constexpr size_t row_off(uint32_t d, uint32_t k, uint32_t lane, uint32_t e) {
+    return kRowU4 ? (((size_t)d * 8 + (k >> 1)) * 64 + lane) * 4 + (k & 1) * 2 + e
+                  : (((size_t)d * 16 + k) * 64 + lane) * 2 + e;
+}
 // word offset, within index i's 2 * dG2 * 2N words, of (sign ks, row d, slot pair k, lane, e)
 __host__ __device__ constexpr size_t ginx_u4_off(uint32_t ks, uint32_t d, uint32_t k, uint32_t lane, uint32_t e) {
     return (((size_t)d * 16 + k) * 64 + lane) * 4 + ks * 2 + e;

@@ -1021,6 +1021,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
             fwd_pass2<FM>(dA, dB, tile, l, twAf, s_twBf, m);
+#if FHE_ROW_U4
+            // one 16-byte vector per digit row and 4 slots (boot.h row_off)
+            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)op * (4 * 8 * 64);
+            uint4 kq[2][4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) kq[0][d] = kb4[(d * 8 + 0) * 64 + lane];
+#pragma clang loop unroll(full)
+            for (int kk = 0; kk < 8; ++kk) {
+                if (kk + 1 < 8) {  // request slots 4(kk+1).. while 4kk.. are consumed
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) kq[(kk + 1) & 1][d] = kb4[(d * 8 + kk + 1) * 64 + lane];
+                }
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * kk + e;
+#define KC(d) (e == 0 ? kq[kk & 1][d].x : e == 1 ? kq[kk & 1][d].y : e == 2 ? kq[kk & 1][d].z : kq[kk & 1][d].w)
+#if FHE_XCHG
+                    const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
+#else
+                    auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
+                    const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
+#endif
+                    // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28): |S| < 40 Q^2 or 24 Q^2, so
+                    // |S| 2^-32 + Q/2 < 2Q
+                    const int64_t S = (int64_t)mac4<true>(D0, D1, D2, D3, KC(0), KC(1), KC(2), KC(3), 0);
+                    acc[r] = smont_red(S, m);
+#undef KC
+                }
+            }
+#else
             const uint2* kb = bsk + (size_t)op * (4 * 16 * 64);
             uint2 kk[2][4];
 #pragma unroll
@@ -1051,6 +1083,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
                     acc[r] = smont_red(S, m);
                 }
             }
+#endif
         } else {
             // ---- Automorphism(5^t or 2N-5, autokey[t])
             const uint32_t t = op & 0x7fffu;
@@ -1072,6 +1105,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
                 dA[r]   = sw[0];
             }
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
+#if FHE_ROW_U4
+            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
+            uint4 ka[2][2];
+            ka[0][0] = kb4[(0 * 8 + 0) * 64 + lane];
+            ka[0][1] = kb4[(1 * 8 + 0) * 64 + lane];
+#pragma clang loop unroll(full)
+            for (int kk = 0; kk < 8; ++kk) {
+                if (kk + 1 < 8) {
+                    ka[(kk + 1) & 1][0] = kb4[(0 * 8 + kk + 1) * 64 + lane];
+                    ka[(kk + 1) & 1][1] = kb4[(1 * 8 + kk + 1) * 64 + lane];
+                }
+                asm volatile("" ::: "memory");
+                const uint4 k0 = ka[kk & 1][0], k1 = ka[kk & 1][1];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * kk + e;
+#if FHE_XCHG
+                    const uint32_t P0 = dA[r], P1 = other_half(dA[r], xaddr);
+#else
+                    auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
+                    const uint32_t P0 = p[0], P1 = p[1];
+#endif
+                    const uint32_t c0 = e == 0 ? k0.x : e == 1 ? k0.y : e == 2 ? k0.z : k0.w;
+                    const uint32_t c1 = e == 0 ? k1.x : e == 1 ? k1.y : e == 2 ? k1.z : k1.w;
+                    // |S| < 2 (6Q) Q + 2Q Q -> |acc| < 14 Q^2 2^-32 + Q/2 < 2Q
+                    int64_t S = (int64_t)(int32_t)P0 * (int32_t)c0 + (int64_t)(int32_t)P1 * (int32_t)c1;
+                    S += (int64_t)(int32_t)acc[r] * (int32_t)oneRh;
+                    acc[r] = smont_red(S, m);
+                }
+            }
+#else
             const uint2* kb = autok + (size_t)t * (2 * 16 * 64);
             uint2 ka[2][2];
             ka[0][0] = kb[(0 * 16 + 0) * 64 + lane];
@@ -1100,6 +1164,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
                     acc[r] = smont_red(S, m);
                 }
             }
+#endif
         }
     }
     // extraction, identical to GINX

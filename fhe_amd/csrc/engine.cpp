@@ -144,7 +144,7 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
                     const uint32_t h = lane >> 5, l = lane & 31;
                     const uint32_t row = kBskHalfSwap ? d ^ h : d;  // boot.h FHE_XCHG
                     const size_t src = ((size_t)row * 2 + h) * N + l * 32 + 2 * k;
-                    const size_t dst = (((size_t)d * 16 + k) * 64 + lane) * 2;
+                    const size_t dst = row_off(d, k, lane, 0);  // boot.h
                     dst_key[dst] = to_mont(mulmod(src_key[src] % Q, ninv, Q), Q);
                     dst_key[dst + 1] = to_mont(mulmod(src_key[src + 1] % Q, ninv, Q), Q);
                 }

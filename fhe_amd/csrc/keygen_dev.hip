@@ -107,8 +107,8 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
             bsk[bi + ginx_u4_off((k.rp >> 2) & 1, k.rp & 3, kk, l, el)]       = v0;
             bsk[bi + ginx_u4_off((k.rp >> 2) & 1, rp1 & 3, kk, 32 + l, el)]   = v1;
         } else {
-            bsk[base + ((kk * 64 + l) * 2 + el)]                  = v0;
-            bsk[(size_t)rp1 * 2 * N + ((kk * 64 + 32 + l) * 2 + el)] = v1;
+            bsk[base + row_off(0, kk, l, el)]                  = v0;
+            bsk[(size_t)rp1 * 2 * N + row_off(0, kk, 32 + l, el)] = v1;
         }
         if (raw) {
             raw[base + j] = r0;
