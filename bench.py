@@ -223,8 +223,8 @@ def ntt_roofline(NttPlan, torch, dev, stream, count, reps=20):
     ms = e0.elapsed_time(e1) / reps
     ach = count * NTT_BYTES_PER_POLY / (ms * 1e-3) / 1e9
     plan.close()
-    return {"kernel": "k_ntt1024<u32,fwd>", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_ntt1024", count),
+    return {"kernel": "k_ntt1024w<fwd, SignedA>", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_ntt1024w", count),
             "launch_us": round(ms * 1e3, 3), "polys": count, "Q": Q}
 
 

@@ -91,7 +91,7 @@ hipError_t launch_prep_ginx(const GateArgs& g, const GateInputs& in, uint16_t* i
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 // LMKCDEY: per-gate op schedule (EXT(i) / AUTO(t)), then the fused accumulator
-hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen, uint16_t* scratch,
+hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen,
                            uint16_t* ops, uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys,
                            hipStream_t s);
 // dm = true: the AP/DM accumulator (rgsw-acc-dm.cpp:62-77) -- an op list of external products only

@@ -859,71 +859,8 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
 //   EXT(i)  (i < 0x8000): AddToAccLMKCDEY with (*ek)[0][0][i]            (:228-254)
 //   AUTO(t) (0x8000 | t): Automorphism by 5^t (t >= 1) or by 2N-5 (t = 0)
 //                         with (*ek)[0][1][t]                              (:257-287)
-// k_prep_lmk builds them with a stable counting sort of the a_i into the
+// k_prep_lmk_w builds them with a stable counting sort of the a_i into the
 // logGen groups (permuteMap, :83-94) and replays the nSkips logic (:99-157).
-__global__ void k_prep_lmk(GateInputs in, GateArgs g, const int16_t* __restrict__ logGen, uint16_t* __restrict__ scratch,
-                           uint16_t* __restrict__ ops, uint32_t* __restrict__ nops, uint32_t* __restrict__ tvb,
-                           uint32_t maxops, uint32_t numAutoKeys) {
-    const uint32_t gate = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gate >= g.count) return;
-    const uint32_t N = g.N, M = 2 * N, Nh = N / 2, n = g.n, qm = g.ctmod - 1;
-    uint16_t* end    = scratch + (size_t)gate * (N + n);  // per position: counts -> bucket ends
-    uint16_t* sorted = end + N;
-    for (uint32_t p = 0; p < N; ++p) end[p] = 0;
-    auto pos_of = [&](uint32_t i) -> uint32_t {
-        const uint32_t a = combine(in, in.a, (size_t)gate * n + i, 0, qm, g.xor_double);
-        const uint32_t aodd = ((M - a) & (M - 1)) | 1u;  // (0 - a_i) mod 2N, made odd
-        const int32_t v     = logGen[aodd];
-        if (v == (int32_t)M) return Nh - 1;                          // -1
-        if (v < 0) return Nh - 1 - (uint32_t)(-v);                   // -5^i
-        return 2 * Nh - 1 - (uint32_t)v;                             // +5^i (v = 0 -> N-1)
-    };
-    for (uint32_t i = 0; i < n; ++i) end[pos_of(i)]++;
-    uint32_t run = 0;
-    for (uint32_t p = 0; p < N; ++p) {
-        const uint32_t c = end[p];
-        end[p]           = (uint16_t)run;
-        run += c;
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t p = pos_of(i);
-        sorted[end[p]++] = (uint16_t)i;  // stable: increasing i within a group
-    }
-    uint16_t* o = ops + (size_t)gate * maxops;
-    uint32_t k = 0, nSkips = 0;
-    auto emit_group = [&](uint32_t p) {
-        const uint32_t s = p ? end[p - 1] : 0u;
-        for (uint32_t j = s; j < end[p]; ++j) o[k++] = sorted[j];
-    };
-    for (int half = 0; half < 2; ++half) {
-        const uint32_t base = half ? Nh : 0u;
-        for (uint32_t i = Nh - 1; i > 0; --i) {
-            const uint32_t p = base + (Nh - 1 - i);
-            const uint32_t s = p ? end[p - 1] : 0u;
-            if (end[p] > s) {
-                if (nSkips != 0) {
-                    o[k++] = (uint16_t)(0x8000u | nSkips);
-                    nSkips = 0;
-                }
-                emit_group(p);
-            }
-            nSkips++;
-            if (nSkips == numAutoKeys || i == 1) {
-                o[k++] = (uint16_t)(0x8000u | nSkips);
-                nSkips = 0;
-            }
-        }
-        if (half == 0) {
-            emit_group(Nh - 1);       // -1
-            o[k++] = (uint16_t)0x8000u;  // automorphism by 2N - 5 with key 0
-        } else {
-            emit_group(N - 1);        // 0
-        }
-    }
-    nops[gate] = k;
-    tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
-}
-
 namespace {
 // EVAL-domain automorphism X -> X^k (poly-impl.h:350-356 / PrecomputeAutoMap, nbtheory2.cpp:264-275):
 // out[slot brv(j)] = in[slot brv(((2j+1)k mod 2N) >> 1)].  Through the half-wave's LDS region
@@ -1191,13 +1128,182 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
     }
 }
 
-hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen, uint16_t* scratch,
+// ---------------------------------------------------------------------------
+// Op-list preps, one wave per gate (a thread per gate serialises each gate's ~2000 steps on one
+// lane with its scratch in global memory: 2.1 ms for 8192 LMKCDEY gates, 0.1 ms this way).
+// ---------------------------------------------------------------------------
+namespace {
+FHE_DEV uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+FHE_DEV uint32_t lanes_below(uint64_t m, uint32_t lane) {
+    return __builtin_popcountll(m & ((1ull << lane) - 1ull));
+}
+constexpr int kPrepWaves = 4;
+}  // namespace
+
+// LMKCDEY: the op schedule described at k_blind_rotate_lmk (rgsw-acc-lmkcdey.cpp:83-157).  Lanes compute the group position of every a_i and
+// count them (LDS atomics), a wave scan gives the group starts, a chunked stable placement
+// (rank among equal positions of lower lanes) fills the sorted order, and the nSkips state
+// machine runs on scalar registers over 64-position ballots of the non-empty groups.
+__global__ void __launch_bounds__(64 * kPrepWaves)
+    k_prep_lmk_w(GateInputs in, GateArgs g, const int16_t* __restrict__ logGen, uint16_t* __restrict__ ops,
+                 uint32_t* __restrict__ nops, uint32_t* __restrict__ tvb, uint32_t maxops, uint32_t numAutoKeys) {
+    __shared__ uint32_t s_start[kPrepWaves][1025];
+    __shared__ uint16_t s_fill[kPrepWaves][1024];
+    __shared__ uint16_t s_bkt[kPrepWaves][512];
+    __shared__ uint16_t s_sorted[kPrepWaves][512];
+    __shared__ uint32_t s_part[kPrepWaves][64];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t gate = blockIdx.x * kPrepWaves + wv;
+    if (gate >= g.count) return;  // wave-uniform; no workgroup barrier below
+    const uint32_t N = g.N, M = 2 * N, Nh = N / 2, n = g.n, qm = g.ctmod - 1;
+    uint32_t* start = s_start[wv];
+    uint16_t* fill = s_fill[wv];
+    uint16_t* bkt = s_bkt[wv];
+    uint16_t* sorted = s_sorted[wv];
+    for (uint32_t p = lane; p < N; p += 64) start[p] = 0;
+    wave_lds_sync();
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint32_t a    = combine(in, in.a, (size_t)gate * n + i, 0, qm, g.xor_double);
+        const uint32_t aodd = ((M - a) & (M - 1)) | 1u;  // (0 - a_i) mod 2N, made odd
+        const int32_t v     = logGen[aodd];
+        const uint32_t p    = v == (int32_t)M ? Nh - 1                          // -1
+                            : v < 0 ? Nh - 1 - (uint32_t)(-v)                    // -5^i
+                                    : 2 * Nh - 1 - (uint32_t)v;                  // +5^i (v = 0 -> N-1)
+        bkt[i] = (uint16_t)p;
+        atomicAdd(&start[p], 1u);
+    }
+    wave_lds_sync();
+    // exclusive scan of the N counts: 16 per lane, then across lanes
+    const uint32_t per = N / 64;
+    uint32_t loc = 0;
+    for (uint32_t t = 0; t < per; ++t) loc += start[lane * per + t];
+    s_part[wv][lane] = loc;
+    wave_lds_sync();
+    uint32_t run = 0;
+    for (uint32_t j = 0; j < 64; ++j) run += j < lane ? s_part[wv][j] : 0u;
+    wave_lds_sync();
+    for (uint32_t t = 0; t < per; ++t) {
+        const uint32_t c = start[lane * per + t];
+        start[lane * per + t] = run;
+        fill[lane * per + t]  = (uint16_t)run;
+        run += c;
+    }
+    if (lane == 0) start[N] = n;
+    wave_lds_sync();
+    // stable placement, 64 items at a time (increasing i within a group)
+    for (uint32_t c = 0; c < n; c += 64) {
+        const uint32_t i = c + lane;
+        const bool valid = i < n;
+        const uint32_t b = valid ? bkt[i] : 0xffffu;
+        uint32_t rank = 0;
+        bool last = true;
+        const uint32_t m = n - c < 64 ? n - c : 64;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint32_t bj = bkt[c + j];
+            rank += (bj == b && j < lane) ? 1u : 0u;
+            last = last && !(bj == b && j > lane);
+        }
+        const uint32_t pos = valid ? fill[b] + rank : 0u;
+        wave_lds_sync();
+        if (valid) {
+            sorted[pos] = (uint16_t)i;
+            if (last) fill[b] = (uint16_t)(pos + 1);
+        }
+        wave_lds_sync();
+    }
+    // emission (nSkips logic of rgsw-acc-lmkcdey.cpp:99-157) on scalar state
+    uint16_t* o = ops + (size_t)gate * maxops;
+    uint32_t k = 0, nSkips = 0;
+    auto emit1 = [&](uint32_t x) {
+        if (lane == 0) o[k] = (uint16_t)x;
+        ++k;
+    };
+    auto emit_group = [&](uint32_t s, uint32_t e) {
+        for (uint32_t q = s; q < e; q += 64)
+            if (q + lane < e) o[k + (q - s) + lane] = sorted[q + lane];
+        k += e - s;
+    };
+    for (uint32_t half = 0; half < 2; ++half) {
+        const uint32_t base = half ? Nh : 0u;
+        for (uint32_t tb = 0; tb < Nh - 1; tb += 64) {
+            const uint32_t t = tb + lane;
+            const bool ok = t < Nh - 1;
+            const uint32_t s = ok ? start[base + t] : 0u, e = ok ? start[base + t + 1] : 0u;
+            const uint64_t ne = ballot(ok && e > s);
+            const uint32_t cnt = (Nh - 1 - tb) < 64 ? Nh - 1 - tb : 64;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const uint32_t i = Nh - 1 - (tb + j);
+                if ((ne >> j) & 1ull) {
+                    if (nSkips != 0) {
+                        emit1(0x8000u | nSkips);
+                        nSkips = 0;
+                    }
+                    emit_group(__builtin_amdgcn_readlane(s, j), __builtin_amdgcn_readlane(e, j));
+                }
+                nSkips++;
+                if (nSkips == numAutoKeys || i == 1) {
+                    emit1(0x8000u | nSkips);
+                    nSkips = 0;
+                }
+            }
+        }
+        if (half == 0) {
+            emit_group(start[Nh - 1], start[Nh]);  // -1
+            emit1(0x8000u);                        // automorphism by 2N - 5 with key 0
+        } else {
+            emit_group(start[N - 1], start[N]);    // 0
+        }
+    }
+    if (lane == 0) {
+        nops[gate] = k;
+        tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
+    }
+}
+
+// AP / DM: ops in (i, digit) order; per 64-item chunk each lane emits its 0..digitsR nonzero
+// digits at the count of lower lanes' ops (ballots per digit slot)
+__global__ void __launch_bounds__(64 * kPrepWaves)
+    k_prep_dm_w(GateInputs in, GateArgs g, uint16_t* __restrict__ ops, uint32_t* __restrict__ nops,
+                uint32_t* __restrict__ tvb, uint32_t maxops, uint32_t baseR, uint32_t digitsR) {
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t gate = blockIdx.x * kPrepWaves + wv;
+    if (gate >= g.count) return;
+    const uint32_t qm = g.q - 1, n = g.n;
+    uint16_t* o = ops + (size_t)gate * maxops;
+    uint32_t k = 0;
+    for (uint32_t c = 0; c < n; c += 64) {
+        const uint32_t i = c + lane;
+        const uint32_t a = i < n ? (g.q - combine(in, in.a, (size_t)gate * n + i, 0, qm, g.xor_double)) & qm : 0u;
+        uint32_t cnt = 0, aI = a;
+        for (uint32_t d = 0; d < digitsR; ++d, aI /= baseR) cnt += (aI % baseR) ? 1u : 0u;
+        uint32_t below = 0, total = 0;
+        for (uint32_t t = 0; t < digitsR; ++t) {
+            const uint64_t m = ballot(cnt > t);
+            below += lanes_below(m, lane);
+            total += __builtin_popcountll(m);
+        }
+        uint32_t w = k + below;
+        aI = a;
+        for (uint32_t d = 0; d < digitsR; ++d, aI /= baseR) {
+            const uint32_t a0 = aI % baseR;
+            if (a0) o[w++] = (uint16_t)((i * baseR + a0) * digitsR + d);
+        }
+        k += total;
+    }
+    if (lane == 0) {
+        nops[gate] = k;
+        tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
+    }
+}
+
+hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_t* logGen,
                            uint16_t* ops, uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys,
                            hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_prep_lmk, dim3((g.count + 63) / 64), dim3(64), 0, s, in, g, logGen, scratch, ops, nops, tvb,
-                       maxops, numAutoKeys);
+    if (g.n > 512 || g.N != 1024) return hipErrorInvalidValue;  // k_prep_lmk_w LDS sizes
+    hipLaunchKernelGGL(k_prep_lmk_w, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, in, g,
+                       logGen, ops, nops, tvb, maxops, numAutoKeys);
     return hipGetLastError();
 }
 
@@ -1229,31 +1335,14 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
 // ---------------------------------------------------------------------------
 // AP/DM prep (rgsw-acc-dm.cpp:62-77): one thread per gate writes its op list
 // ---------------------------------------------------------------------------
-__global__ void k_prep_dm(GateInputs in, GateArgs g, uint16_t* __restrict__ ops, uint32_t* __restrict__ nops,
-                          uint32_t* __restrict__ tvb, uint32_t maxops, uint32_t baseR, uint32_t digitsR) {
-    const uint32_t gate = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gate >= g.count) return;
-    const uint32_t qm = g.q - 1, n = g.n;
-    uint16_t* o = ops + (size_t)gate * maxops;
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        uint32_t aI = (g.q - combine(in, in.a, (size_t)gate * n + i, 0, qm, g.xor_double)) & qm;
-        for (uint32_t d = 0; d < digitsR; ++d, aI /= baseR) {
-            const uint32_t a0 = aI % baseR;
-            if (a0) o[k++] = (uint16_t)((i * baseR + a0) * digitsR + d);
-        }
-    }
-    nops[gate] = k;
-    tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
-}
-
 hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops, uint32_t* nops, uint32_t* tvb,
                           uint32_t maxops, uint32_t baseR, uint32_t digitsR, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (in.k < 1 || in.k > 4 || (size_t)g.n * digitsR > maxops || (size_t)g.n * baseR * digitsR > 0x8000u)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_prep_dm, dim3((g.count + 63) / 64), dim3(64), 0, s, in, g, ops, nops, tvb, maxops, baseR,
-                       digitsR);
+    if (digitsR > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_prep_dm_w, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, in, g,
+                       ops, nops, tvb, maxops, baseR, digitsR);
     return hipGetLastError();
 }
 

@@ -33,8 +33,7 @@ Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
-                      (void*)d_scratch_})
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_})
         if (ptr) (void)hipFree(ptr);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -300,12 +299,11 @@ void Engine::ensure_work(size_t count) {
     FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
     FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
     if (p_.method == M_LMKCDEY || p_.method == M_AP) {
-        for (void* ptr : {(void*)d_ops_, (void*)d_nops_, (void*)d_scratch_})
+        for (void* ptr : {(void*)d_ops_, (void*)d_nops_})
             if (ptr) FHE_HIP_CHECK(hipFree(ptr));
-        d_ops_ = nullptr; d_nops_ = nullptr; d_scratch_ = nullptr;
+        d_ops_ = nullptr; d_nops_ = nullptr;
         FHE_HIP_CHECK(hipMalloc(&d_ops_, count * maxops_ * sizeof(uint16_t)));
         FHE_HIP_CHECK(hipMalloc(&d_nops_, count * sizeof(uint32_t)));
-        FHE_HIP_CHECK(hipMalloc(&d_scratch_, count * (p_.N + p_.n) * sizeof(uint16_t)));
     }
     cap_ = count;
 }
@@ -331,7 +329,7 @@ void Engine::prep_device(const GateArgs& g, const GateInputs& in, size_t offset,
         FHE_HIP_CHECK(launch_prep_dm(g, in, d_ops_ + offset * maxops_, d_nops_ + offset, d_tvb_ + offset, maxops_,
                                      p_.baseR, p_.digitsR, s));
     } else {
-        FHE_HIP_CHECK(launch_prep_lmk(g, in, d_logGen_, d_scratch_ + offset * (p_.N + p_.n), d_ops_ + offset * maxops_,
+        FHE_HIP_CHECK(launch_prep_lmk(g, in, d_logGen_, d_ops_ + offset * maxops_,
                                       d_nops_ + offset, d_tvb_ + offset, maxops_, p_.numAutoKeys, s));
     }
 }

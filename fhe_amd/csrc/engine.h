@@ -135,7 +135,6 @@ private:
     uint32_t maxops_ = 0;
     uint16_t* d_ops_ = nullptr;
     uint32_t* d_nops_ = nullptr;
-    uint16_t* d_scratch_ = nullptr;
     uint16_t* d_ksk_ = nullptr;
     // workspace
     size_t cap_ = 0;
