@@ -31,6 +31,12 @@
 #ifndef FHE_KEY_PF
 #define FHE_KEY_PF 2     // key chunks (2 slots each) requested ahead of use in the CMUX loop
 #endif
+#ifndef FHE_MAC_PIPE
+#define FHE_MAC_PIPE 1   // GINX: digit exchange and monomial reads one slot pair ahead
+#endif
+#ifndef FHE_TW_PRE
+#define FHE_TW_PRE 1     // GINX: per-lane twiddles of a pass's B' stages requested together at its start
+#endif
 #ifndef FHE_FWD_FUSED
 #define FHE_FWD_FUSED 1
 #endif
@@ -189,6 +195,14 @@ FHE_DEV void transpose32(uint32_t (&v)[32], uint32_t* tile, int l) {
 
 // offset of stage b's lane-major twiddle block: 32 * (2^(4-b) - 1)
 constexpr int twb_off(int b) { return 32 * ((1 << (4 - b)) - 1); }
+// PRE: the 31 per-lane twiddles of a pass's five B' stages requested together at its start
+// (entry j of stage b is tw[twb_off(b) / 32 + j]) instead of one LDS round trip per stage pair
+#define TWB(b, j) (PRE ? tw[twb_off(b) / 32 + (j)] : s_twB[twb_off(b) + (j) * 32 + l])
+#define TW_PRELOAD                                                    \
+    uint32_t tw[31];                                                  \
+    if (PRE) {                                                        \
+        _Pragma("unroll") for (int j = 0; j < 31; ++j) tw[j] = s_twB[j * 32 + l]; \
+    }
 
 // forward NTT: A' (COEF, inputs < Q) -> B' (EVAL), outputs < 14Q (< 2^32 for Q < 2^28):
 // 5 stages (< 11Q), reduce to < 4Q at the transpose, 5 stages (< 14Q)
@@ -232,7 +246,7 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 // FM (forward mode): 0 unsigned lazy (above), 1 signed without reduction (Q < 2^27), 2 signed for
 // Q < 2^28: after 5 stages |v| < 5Q + 2^(g-1); the x inputs of the first B' stage (registers 0..15)
 // are reduced to (-Q, Q), so the B' outputs stay < 6Q (a Cooley-Tukey output is bounded by |x| + Q)
-template <int FM>
+template <int FM, bool PRE = false>
 FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int l,
                        const uint32_t* __restrict__ twA, const uint32_t* s_twB, const Mod& m) {
     constexpr bool LZ = FM != 0;
@@ -268,6 +282,7 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
             u[r] = smont_mul(u[r], m.oneR, m);
         }
     }
+    TW_PRELOAD
 #pragma unroll
     for (int b = 4; b >= 0; --b) {
 #pragma unroll
@@ -276,7 +291,7 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
 #if defined(FHE_ABL) && (FHE_ABL & 8)
             const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;
 #else
-            const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+            const uint32_t w = TWB(b, r >> (b + 1));
 #endif
             if (LZ) {
                 ct_bf_s(v[r], v[r | (1 << b)], w, m);
@@ -421,10 +436,11 @@ constexpr InvPlanS make_inv_plan() {
 
 // B' (EVAL, |inputs| < BIN Q / 10, signed) -> A' (COEF), canonical [0, Q) like inv_pass.
 // LZ: Q < 2^27 (sums up to 16 Q), else Q < 2^28 (8 Q; the final 2^(fin+1) Q <= 16 Q < 2^32)
-template <int BIN, bool LZ = true>
+template <int BIN, bool LZ = true, bool PRE = false>
 FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* __restrict__ twA,
                         const uint32_t* s_twB, uint32_t w1R, uint32_t oneR, const Mod& m) {
     constexpr InvPlanS P = make_inv_plan<BIN, lim_s(LZ)>();
+    TW_PRELOAD
 #pragma unroll
     for (int b = 0; b <= 4; ++b) {
 #pragma unroll
@@ -433,7 +449,7 @@ FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
             const int s = r | (1 << b);
             if (P.red1[b][r]) v[r] = smont_mul(v[r], oneR, m);
             if (P.red1[b][s]) v[s] = smont_mul(v[s], oneR, m);
-            const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
+            const uint32_t w = TWB(b, r >> (b + 1));
             const uint32_t x = v[r], y = v[s];
             v[r]             = x + y;
             v[s]             = smont_mul(x - y, w, m);
@@ -642,7 +658,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #if defined(FHE_ABL) && (FHE_ABL & 16)
         if (0)  // ablation: no inverse pass
 #endif
-        if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20>(dA, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
+        if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20, true, FHE_TW_PRE != 0>(dA, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
         else inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
         // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
         //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
@@ -652,7 +668,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #if defined(FHE_ABL) && (FHE_ABL & 32)
         // ablation: no forward passes
 #elif FHE_FWD_FUSED
-        fwd_pass2<LZ ? 1 : 0>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+        fwd_pass2<LZ ? 1 : 0, FHE_TW_PRE != 0>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
 #elif FHE_FWD_SHARED
         // one copy of the forward-pass code for both digit polynomials (instruction-cache
         // footprint): transform dA, swap, transform (old dB), swap back
@@ -691,12 +707,38 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         for (int k = 0; k < FHE_KEY_PF; ++k)
 #pragma unroll
             for (int d = 0; d < 4; ++d) kq[k][d] = kb4[(d * 16 + k) * 64 + lofs];
+#if FHE_MAC_PIPE
+        // the other half's digits (ds_bpermute) and the monomial pairs of slot pair k + 1 are
+        // requested before slot pair k is consumed (LDS latency off the critical path)
+        uint32_t xo[2][4];
+        uint2 mo[2][2][2];
+        auto issue = [&](int k, int b) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r      = 2 * k + e;
+                xo[b][2 * e]     = other_half(dA[r], xaddr);
+                xo[b][2 * e + 1] = other_half(dB[r], xaddr);
+                const uint32_t u = __builtin_amdgcn_readfirstlane((as * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & umask) * 66;
+                if (e == 0 || mfull) {
+                    mo[b][e][0] = s_mono2[Pp + u];
+                    mo[b][e][1] = s_mono2[Pn - u];
+                } else {  // half table: slots r, r ^ 1 share the monomial
+                    mo[b][1][0] = mo[b][0][0];
+                    mo[b][1][1] = mo[b][0][1];
+                }
+            }
+        };
+        issue(0, 0);
+#endif
 #pragma clang loop unroll(full)
         for (int k = 0; k < 16; ++k) {
             if (k + FHE_KEY_PF < 16) {
 #pragma unroll
                 for (int d = 0; d < 4; ++d) kq[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d] = kb4[(d * 16 + k + FHE_KEY_PF) * 64 + lofs];
             }
+#if FHE_MAC_PIPE
+            if (k + 1 < 16) issue(k + 1, (k + 1) & 1);
+#endif
             asm volatile("" ::: "memory");
 #define KP(d) make_uint2(kq[k % (FHE_KEY_PF + 1)][d].x, kq[k % (FHE_KEY_PF + 1)][d].y)
 #define KN(d) make_uint2(kq[k % (FHE_KEY_PF + 1)][d].z, kq[k % (FHE_KEY_PF + 1)][d].w)
@@ -741,7 +783,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * k + e;
                 // all four digits in every lane: D0/D1 = digit A of acc0/acc1, D2/D3 = digit B
-#if FHE_XCHG
+#if FHE_MAC_PIPE && FHE_GINX_U4
+                const uint32_t D0 = dA[r], D1 = xo[k & 1][2 * e], D2 = dB[r], D3 = xo[k & 1][2 * e + 1];
+#elif FHE_XCHG
                 // (own, other) digit order; the half-1 key rows are stored swapped to match
                 const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
 #else
@@ -762,6 +806,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                                                            e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, 0);
 #if defined(FHE_ABL) && (FHE_ABL & 2)
                     const uint2 mp = make_uint2(Pp + u, Pp ^ u), mn = make_uint2(Pn - u, Pn ^ u);
+#elif FHE_MAC_PIPE && FHE_GINX_U4
+                    const uint2 mp = mo[k & 1][e][0], mn = mo[k & 1][e][1];
+                    (void)u;
 #else
                     const uint2 mp = s_mono2[Pp + u], mn = s_mono2[Pn - u];
 #endif
