@@ -583,7 +583,10 @@ constexpr size_t boot_lds(bool full, bool lz) {
 template <bool MFULL, bool LZ>
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
-                        const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
+                        const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
+                        const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
+    // twAf / twAi = T.twA_fwd / T.twA_inv as restrict const arguments: the uniform A'-stage
+    // twiddles then come through the scalar cache (s_load) instead of vector loads
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_twBf = sm;
     uint32_t* s_twBi = sm + 992;
@@ -658,7 +661,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #if defined(FHE_ABL) && (FHE_ABL & 16)
         if (0)  // ablation: no inverse pass
 #endif
-        if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20, true, FHE_TW_PRE != 0>(dA, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
+        if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20, true, FHE_TW_PRE != 0>(dA, tile, l, twAi, s_twBi, T.w1R, T.oneR, m);
         else inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
         // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
         //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
@@ -668,7 +671,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #if defined(FHE_ABL) && (FHE_ABL & 32)
         // ablation: no forward passes
 #elif FHE_FWD_FUSED
-        fwd_pass2<LZ ? 1 : 0, FHE_TW_PRE != 0>(dA, dB, tile, l, T.twA_fwd, s_twBf, m);
+        fwd_pass2<LZ ? 1 : 0, FHE_TW_PRE != 0>(dA, dB, tile, l, twAf, s_twBf, m);
 #elif FHE_FWD_SHARED
         // one copy of the forward-pass code for both digit polynomials (instruction-cache
         // footprint): transform dA, swap, transform (old dB), swap back
@@ -883,17 +886,17 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
     if (g.ctmod == 2 * g.N) {
         if (lz)
             hipLaunchKernelGGL((k_blind_rotate_ginx<true, true>), dim3(blocks), dim3(256), boot_lds(true, true), s, g, t, k,
-                               idx, tvb, ext_a, ext_b);
+                               idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
         else
             hipLaunchKernelGGL((k_blind_rotate_ginx<true, false>), dim3(blocks), dim3(256), boot_lds(true, false), s, g, t,
-                               k, idx, tvb, ext_a, ext_b);
+                               k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
     } else {
         if (lz)
             hipLaunchKernelGGL((k_blind_rotate_ginx<false, true>), dim3(blocks), dim3(256), boot_lds(false, true), s, g, t,
-                               k, idx, tvb, ext_a, ext_b);
+                               k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
         else
             hipLaunchKernelGGL((k_blind_rotate_ginx<false, false>), dim3(blocks), dim3(256), boot_lds(false, false), s, g, t,
-                               k, idx, tvb, ext_a, ext_b);
+                               k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
     }
     return hipGetLastError();
 }
