@@ -1180,7 +1180,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
 
 // ---------------------------------------------------------------------------
 // Op-list preps, one wave per gate (a thread per gate serialises each gate's ~2000 steps on one
-// lane with its scratch in global memory: 2.1 ms for 8192 LMKCDEY gates, 0.1 ms this way).
+// lane with its scratch in global memory: 2.1 ms for 8192 LMKCDEY gates, 0.42 ms this way).
 // ---------------------------------------------------------------------------
 namespace {
 FHE_DEV uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
