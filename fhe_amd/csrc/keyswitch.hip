@@ -80,8 +80,17 @@ __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
     return r;
 }
 
-constexpr int kKsCols  = 64;                    // columns per workgroup (32 packed u32)
-constexpr int kKsRowB  = kKsCols * 2 + 16;      // LDS bytes per staged slice (+16 pad: conflict-light b128 reads)
+#ifndef FHE_KS_COLS
+#define FHE_KS_COLS 64  // 32: twice the workgroups, half the columns each
+#endif
+constexpr int kKsCols  = FHE_KS_COLS;           // columns per workgroup (packed u32 pairs)
+#ifndef FHE_KS_B64
+#define FHE_KS_B64 1
+#endif
+// LDS bytes per staged slice.  FHE_KS_B64: 136 B, read as 8-byte pieces: slice d's piece k sits in
+// 8-byte bank slot (17 d + k) mod 32, distinct for all 32 slices, so the random per-gate slice
+// choices never conflict (16-byte reads with a 144-B stride collide for slices d, d + 16).
+constexpr int kKsRowB  = kKsCols * 2 + (FHE_KS_B64 ? 8 : 16);
 constexpr int kKsParts = 32 * kKsCols * 2 / 16; // 16-byte parts staged per step (32 slices x 128 B)
 constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
 constexpr int kKsDigits = 3, kKsLogBase = 5;    // digitsKS, log2(baseKS)
@@ -118,9 +127,17 @@ __global__ void __launch_bounds__(G)
         const size_t row = ((size_t)i * (1u << kKsLogBase) + sd) * kKsDigits + j;
         return reinterpret_cast<const uint4*>(ksk + row * 512 + col0) + sp;
     };
-    auto slice_dst = [&](unsigned char* sb, int r) -> uint4* {
+    auto slice_dst = [&](unsigned char* sb, int r) -> unsigned char* {
         const uint32_t x = t + G * r;
-        return reinterpret_cast<uint4*>(sb + (x / kKsPartsPerSlice) * kKsRowB + (x % kKsPartsPerSlice) * 16);
+        return sb + (x / kKsPartsPerSlice) * kKsRowB + (x % kKsPartsPerSlice) * 16;
+    };
+    auto put = [&](unsigned char* dst, const uint4& v) {
+        if (FHE_KS_B64) {  // 8-byte aligned only
+            reinterpret_cast<uint2*>(dst)[0] = make_uint2(v.x, v.y);
+            reinterpret_cast<uint2*>(dst)[1] = make_uint2(v.z, v.w);
+        } else {
+            *reinterpret_cast<uint4*>(dst) = v;
+        }
     };
 
     uint32_t acc[kKsCols / 2];
@@ -128,10 +145,14 @@ __global__ void __launch_bounds__(G)
     for (int k = 0; k < kKsCols / 2; ++k) acc[k] = 0;
 
     uint4 st[kKsStep][P];
+    // threads past kKsParts (narrow column tiles) stage nothing: their slice index would run past
+    // the KSK rows of this i
+    const bool stager = kKsParts >= G || (int)t < kKsParts;
 #pragma unroll
     for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
-        for (int r = 0; r < P; ++r) st[q][r] = *slice_src(0, q, r);
+        for (int r = 0; r < P; ++r)
+            if (stager) st[q][r] = *slice_src(0, q, r);
     AV a0 = ga4[0], a1 = ga4[rounds > 1 ? 1 : 0], a2 = ga4[rounds > 2 ? 2 : 0];
 
     // one barrier per round: buffer buf is rewritten two rounds later, after every thread
@@ -141,13 +162,14 @@ __global__ void __launch_bounds__(G)
         for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
             for (int r = 0; r < P; ++r)
-                if (kKsParts >= G || (int)t < kKsParts) *slice_dst(s_buf[buf][q], r) = st[q][r];
+                if (stager) put(slice_dst(s_buf[buf][q], r), st[q][r]);
         __syncthreads();
         if (rd + 1 < rounds) {
 #pragma unroll
             for (int q = 0; q < kKsStep; ++q)
 #pragma unroll
-                for (int r = 0; r < P; ++r) st[q][r] = *slice_src(rd + 1, q, r);
+                for (int r = 0; r < P; ++r)
+                    if (stager) st[q][r] = *slice_src(rd + 1, q, r);
         }
         const AV av = a0;
         a0 = a1;
@@ -157,14 +179,31 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q) {
             const uint32_t dig = (as[q / kKsDigits] >> (kKsLogBase * (q % kKsDigits))) & ((1u << kKsLogBase) - 1);
-            const uint4* src = reinterpret_cast<const uint4*>(s_buf[buf][q] + dig * kKsRowB);
+            if (FHE_KS_B64) {
+                const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kKsRowB);
+                uint2 w[kKsCols / 4];
 #pragma unroll
-            for (int k = 0; k < kKsCols / 8; ++k) {
-                const uint4 w = src[k];
-                acc[4 * k + 0] = pk_sub_u16(acc[4 * k + 0], w.x);
-                acc[4 * k + 1] = pk_sub_u16(acc[4 * k + 1], w.y);
-                acc[4 * k + 2] = pk_sub_u16(acc[4 * k + 2], w.z);
-                acc[4 * k + 3] = pk_sub_u16(acc[4 * k + 3], w.w);
+                for (int k = 0; k < kKsCols / 4; ++k) {
+                    w[k] = src[k];
+                    // no ds_read2_b64 merge: its 16-lane groups bank mod 32, where slices d and
+                    // d + 16 collide again
+                    asm volatile("" ::: "memory");
+                }
+#pragma unroll
+                for (int k = 0; k < kKsCols / 4; ++k) {
+                    acc[2 * k + 0] = pk_sub_u16(acc[2 * k + 0], w[k].x);
+                    acc[2 * k + 1] = pk_sub_u16(acc[2 * k + 1], w[k].y);
+                }
+            } else {
+                const uint4* src = reinterpret_cast<const uint4*>(s_buf[buf][q] + dig * kKsRowB);
+#pragma unroll
+                for (int k = 0; k < kKsCols / 8; ++k) {
+                    const uint4 w = src[k];
+                    acc[4 * k + 0] = pk_sub_u16(acc[4 * k + 0], w.x);
+                    acc[4 * k + 1] = pk_sub_u16(acc[4 * k + 1], w.y);
+                    acc[4 * k + 2] = pk_sub_u16(acc[4 * k + 2], w.z);
+                    acc[4 * k + 3] = pk_sub_u16(acc[4 * k + 3], w.w);
+                }
             }
         }
     }
