@@ -13,7 +13,9 @@ scaling: B per GPU fixed).  Rank 0 prints one JSON line.
 Also measured in the same run and reported beside `value`:
   * roofline     -- dominant kernel of the step (blind rotation): algorithmic
                     bytes / launch time (HIP events on the launch stream) vs HBM
-                    peak, plus its integer-VALU utilisation (the binding limit);
+                    peak (tiny by construction: the BSK is reused by every gate);
+  * valu_roofline -- the same kernel against the bound that binds: modular
+                    multiplies per second vs the 32-bit integer multiply issue peak;
   * ntt_roofline -- BASELINE config 2: batched N=1024 NTT x 4096, GB/s vs HBM peak;
   * cpu_baseline -- the reference's own CPU path (oracle/_ref/libfhe_ref.so,
                     built from /root/reference) on the host cores, rank 0, N=1.
@@ -31,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "TFHE gate bootstraps/sec (STD128) at 1/2/4/8 MI355X; NTT GB/s vs HBM peak"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_MODMUL_PEAK_T = 256 * 4 * 16 * 2.4e9 / 3 / 1e12  # 13.1 T modmul/s (half-rate 32-bit multiplies)
 KEY_SEED = 0xBE4C0001
 # algorithmic bytes (reference u64 accounting)
 BSK_BYTES = {"ginx": 65_929_216, "lmkcdey": 29_655_040}
@@ -161,8 +164,18 @@ def main():
             "traffic_note": "2*FETCH_SIZE+WRITE_SIZE (profiles/*pmc_traffic.json); FETCH counts L2->fabric "
                             "requests incl. Infinity-Cache hits: the BSK is streamed once per XCD per wave "
                             "generation (8 XCDs x 4 generations at B=8192) from the 256 MiB cache",
-            "valu_note": "integer-VALU bound: modmul rate below",
+            "valu_note": "integer-VALU bound: see valu_roofline",
             "modmul_per_s": round(mm_per_gate * B / (br_ms * 1e-3) / 1e12, 3), "modmul_unit": "T/s",
+        }
+        # the bound that binds: 32-bit integer multiply issue (each modular multiply is three
+        # half-rate multiplies: v_mad_i64_i32, v_mul_lo_u32, v_mad_i64_i32)
+        mm_rate = mm_per_gate * B / (br_ms * 1e-3) / 1e12
+        valu_roofline = {
+            "kernel": f"k_blind_rotate_{args.method}", "bound": "valu-int-mul", "achieved": round(mm_rate, 3),
+            "peak": VALU_MODMUL_PEAK_T, "unit": "T modmul/s", "frac": round(mm_rate / VALU_MODMUL_PEAK_T, 4),
+            "basis": "SURVEY 8(a) modular multiplies per gate x gates / launch time; peak = 256 CUs x 4 SIMDs x "
+                     "16 lanes/clk (half-rate 32-bit multiplies) x 2.4 GHz / 3 multiplies per modmul; the measured "
+                     "multiply issue rate (profiles/r01_ubench_valu_rates.txt, 35.1 T lane-op/s) is 11.7 T modmul/s",
         }
         ntt = ntt_roofline(NttPlan, torch, dev, stream, args.ntt_count) if world == 1 else None
         cpu = None
@@ -181,6 +194,7 @@ def main():
                        "parallelism": f"shard{world}"},
             "verified": verified,
             "roofline": roofline,
+            "valu_roofline": valu_roofline,
             "ntt_roofline": ntt,
             "cpu_baseline": cpu,
         }
