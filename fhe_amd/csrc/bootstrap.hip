@@ -115,6 +115,15 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_INV_S
 #define FHE_INV_S 1     // LZ: signed inverse NTT
 #endif
+#ifndef FHE_DM_WAVES
+#define FHE_DM_WAVES 3   // waves per SIMD of the AP/DM op-list kernel
+#endif
+#ifndef FHE_LMK_TWPRE
+#define FHE_LMK_TWPRE 1  // LMKCDEY: per-lane B' twiddles requested together (FHE_TW_PRE)
+#endif
+#ifndef FHE_LMK_PIPE
+#define FHE_LMK_PIPE 1   // LMKCDEY: digit exchange one 4-slot group ahead of the external product
+#endif
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
@@ -938,7 +947,7 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
 // AddToAccLMKCDEY, rgsw-acc-dm.cpp:119-145) and no initial automorphism of acc1.
 // DM needs no automorphism path and fits 168 VGPRs: 3 waves per SIMD
 template <bool DM, bool LZ>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3 : FHE_LMK_WAVES)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? FHE_DM_WAVES : FHE_LMK_WAVES)))
     k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
                        const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b) {
@@ -1004,21 +1013,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
             // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass_s<20, LZ>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
+            inv_pass_s<20, LZ, !DM && FHE_LMK_TWPRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
-            fwd_pass2<FM>(dA, dB, tile, l, twAf, s_twBf, m);
+            fwd_pass2<FM, !DM && FHE_LMK_TWPRE>(dA, dB, tile, l, twAf, s_twBf, m);
 #if FHE_ROW_U4
             // one 16-byte vector per digit row and 4 slots (boot.h row_off)
             const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)op * (4 * 8 * 64);
             uint4 kq[2][4];
 #pragma unroll
             for (int d = 0; d < 4; ++d) kq[0][d] = kb4[(d * 8 + 0) * 64 + lane];
+            // LMKCDEY: the other half's digits of slots 4(kk+1).. requested before 4kk.. are consumed
+            constexpr bool PIPE = !DM && FHE_LMK_PIPE;
+            uint32_t xq[2][8];
+            auto issue = [&](int kk, int b) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    xq[b][2 * e]     = other_half(dA[4 * kk + e], xaddr);
+                    xq[b][2 * e + 1] = other_half(dB[4 * kk + e], xaddr);
+                }
+            };
+            if (PIPE) issue(0, 0);
 #pragma clang loop unroll(full)
             for (int kk = 0; kk < 8; ++kk) {
                 if (kk + 1 < 8) {  // request slots 4(kk+1).. while 4kk.. are consumed
 #pragma unroll
                     for (int d = 0; d < 4; ++d) kq[(kk + 1) & 1][d] = kb4[(d * 8 + kk + 1) * 64 + lane];
+                    if (PIPE) issue(kk + 1, (kk + 1) & 1);
                 }
                 asm volatile("" ::: "memory");
 #pragma unroll
@@ -1026,7 +1047,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
                     const int r = 4 * kk + e;
 #define KC(d) (e == 0 ? kq[kk & 1][d].x : e == 1 ? kq[kk & 1][d].y : e == 2 ? kq[kk & 1][d].z : kq[kk & 1][d].w)
 #if FHE_XCHG
-                    const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
+                    const uint32_t D0 = dA[r], D2 = dB[r];
+                    const uint32_t D1 = PIPE ? xq[kk & 1][2 * e] : other_half(dA[r], xaddr);
+                    const uint32_t D3 = PIPE ? xq[kk & 1][2 * e + 1] : other_half(dB[r], xaddr);
 #else
                     auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                     auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
@@ -1083,7 +1106,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
             automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass_s<20, LZ>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);  // half 0: COEF acc0'
+            inv_pass_s<20, LZ, FHE_LMK_TWPRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);  // half 0: COEF acc0'
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
                 decompose2<true>(dA[r], dec, dA[r], dB[r]);
@@ -1097,11 +1120,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
             uint4 ka[2][2];
             ka[0][0] = kb4[(0 * 8 + 0) * 64 + lane];
             ka[0][1] = kb4[(1 * 8 + 0) * 64 + lane];
+            uint32_t xa[2][4];
+            auto issue = [&](int kk, int b) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xa[b][e] = other_half(dA[4 * kk + e], xaddr);
+            };
+            if (FHE_LMK_PIPE) issue(0, 0);
 #pragma clang loop unroll(full)
             for (int kk = 0; kk < 8; ++kk) {
                 if (kk + 1 < 8) {
                     ka[(kk + 1) & 1][0] = kb4[(0 * 8 + kk + 1) * 64 + lane];
                     ka[(kk + 1) & 1][1] = kb4[(1 * 8 + kk + 1) * 64 + lane];
+                    if (FHE_LMK_PIPE) issue(kk + 1, (kk + 1) & 1);
                 }
                 asm volatile("" ::: "memory");
                 const uint4 k0 = ka[kk & 1][0], k1 = ka[kk & 1][1];
@@ -1109,7 +1139,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? 3
                 for (int e = 0; e < 4; ++e) {
                     const int r = 4 * kk + e;
 #if FHE_XCHG
-                    const uint32_t P0 = dA[r], P1 = other_half(dA[r], xaddr);
+                    const uint32_t P0 = dA[r], P1 = FHE_LMK_PIPE ? xa[kk & 1][e] : other_half(dA[r], xaddr);
 #else
                     auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
                     const uint32_t P0 = p[0], P1 = p[1];
