@@ -23,6 +23,7 @@ struct BootTables {
     const uint32_t* mono_full;  // kMonoTableWords: psi^e - 1, any m
     const uint32_t* monoP;       // plain (non-Montgomery) copies of mono / mono_full: the signed
     const uint32_t* monoP_full;  // accumulator multiplies the unreduced 64-bit digit-key sums by both
+    const uint32_t* tabI;        // TableI[0..1023] (the LMKCDEY automorphism's wave-wide inverse NTT)
     uint32_t Q, Q2, qinv;     // qinv = -Q^-1 mod 2^32
     // The resident keys carry a factor N^-1 (folded in at packing), so the EVALUATION accumulator
     // is N^-1 * acc and the last inverse stage needs no N^-1 multiply: it scales by TableI[1] only.

@@ -124,6 +124,9 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_PIPE
 #define FHE_LMK_PIPE 1   // LMKCDEY: digit exchange one 4-slot group ahead of the external product
 #endif
+#ifndef FHE_AUTO_WIDE
+#define FHE_AUTO_WIDE 1  // LMKCDEY automorphism: acc0' inverse-transformed across the whole wave
+#endif
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
@@ -941,6 +944,156 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
     }
     wave_lds_sync();
 }
+// ---- LMKCDEY automorphism op, acc0' inverse-transformed across the whole wave ---------------------
+// Only acc0' of an automorphism is decomposed, so instead of a half-wave pass per component (half 1
+// transforming acc1' for nothing) the wave transforms acc0' alone with 16 coefficients per lane,
+// in the three layouts of ntt.hip k_ntt1024w (x = EVAL slot or coefficient index):
+//   C: lane L = x7..x2, register r = (x9x8) << 2 | x1x0;   B: lane = (x9..x6) << 2 | x1x0,
+//   register = x5..x2;   A: lane = x5..x0, register = x9..x6.   LDS word of x: x + 4 (x >> 6).
+FHE_DEV int wt64(int x) { return x + ((x >> 6) << 2); }
+struct InvPlanWW {
+    bool red[10][16];  // reduce register r before stage s (C bit 0, C bit 1, B bits 0..3, A bits 0..2, last)
+    int fin[8];        // last-stage sum: |x + y| < 2^fin Q
+};
+template <int BIN, int LIM>
+constexpr InvPlanWW make_inv_plan_ww() {
+    InvPlanWW p{};
+    int B[16] = {};
+    for (int r = 0; r < 16; ++r) B[r] = BIN;
+    const int bits[10] = {0, 1, 0, 1, 2, 3, 0, 1, 2, 3};
+    for (int st = 0; st < 10; ++st) {
+        if (st == 2 || st == 6) {  // a transpose mixes every register
+            int U = 0;
+            for (int r = 0; r < 16; ++r) U = B[r] > U ? B[r] : U;
+            for (int r = 0; r < 16; ++r) B[r] = U;
+        }
+        const int bt = bits[st];
+        for (int r = 0; r < 16; ++r) {
+            if (r & (1 << bt)) continue;
+            const int q = r | (1 << bt);
+            while (B[r] + B[q] > LIM) {
+                const int e  = B[r] >= B[q] ? r : q;
+                B[e]         = 10;
+                p.red[st][e] = true;
+            }
+            if (st == 9) {
+                int f = 0;
+                while ((10 << f) < B[r] + B[q]) ++f;
+                p.fin[r] = f;
+            }
+            B[r] = B[r] + B[q];
+            B[q] = 10;
+        }
+    }
+    return p;
+}
+// EVAL (layout C, |v| < BIN Q / 10) -> canonical COEF (layout A); the keys carry N^-1, so the last
+// stage scales by TableI[1] only (as inv_pass_s).  tile: 1088 words of this wave; s_tabI: TableI.
+template <int BIN, bool LZ>
+FHE_DEV void inv_wave_s(uint32_t (&v)[16], uint32_t* tile, int L, const uint32_t* s_tabI, uint32_t w1R,
+                        uint32_t oneR, const Mod& m) {
+    constexpr InvPlanWW P = make_inv_plan_ww<BIN, lim_s(LZ)>();
+    auto redp = [&](int st) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (P.red[st][r]) v[r] = smont_mul(v[r], oneR, m);
+    };
+    auto gs = [&](uint32_t& x, uint32_t& y, uint32_t w) {
+        const uint32_t t = x + y;
+        y                = smont_mul(x - y, w, m);
+        x                = t;
+    };
+    const int G = L >> 2, jj = L & 3;
+    redp(0);
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh) {
+        const uint2 w0 = *reinterpret_cast<const uint2*>(s_tabI + 512 + (hh << 7) + (L << 1));
+        gs(v[4 * hh], v[4 * hh + 1], w0.x);
+        gs(v[4 * hh + 2], v[4 * hh + 3], w0.y);
+    }
+    redp(1);
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh) {
+        const uint32_t w1 = s_tabI[256 + (hh << 6) + L];
+        gs(v[4 * hh], v[4 * hh + 2], w1);
+        gs(v[4 * hh + 1], v[4 * hh + 3], w1);
+    }
+    // C -> B
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh)
+        *reinterpret_cast<uint4*>(tile + wt64((hh << 8) | (L << 2))) = make_uint4(v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]);
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = tile[wt64((G << 6) | (r << 2) | jj)];
+    wave_lds_sync();
+#pragma unroll
+    for (int b = 2; b <= 5; ++b) {
+        const int rb = b - 2;
+        redp(b);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & (1 << rb)) continue;
+            gs(v[r], v[r | (1 << rb)], s_tabI[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))]);
+        }
+    }
+    // B -> A
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[wt64((G << 6) | (r << 2) | jj)] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = tile[wt64((r << 6) | L)];
+    wave_lds_sync();
+#pragma unroll
+    for (int b = 6; b <= 8; ++b) {
+        const int rb = b - 6;
+        redp(b);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & (1 << rb)) continue;
+            gs(v[r], v[r | (1 << rb)], s_tabI[(1 << (9 - b)) + (r >> (rb + 1))]);
+        }
+    }
+    // bit 9 (transformnat-impl.h:599-623), canonical results as inv_pass_s
+    redp(9);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint32_t x = v[r], y = v[r | 8];
+        uint32_t s       = x + y + (m.Q << P.fin[r]);
+#pragma unroll
+        for (int f = P.fin[r]; f >= 0; --f) s = csub(s, m.Q << f);
+        const uint32_t d = smont_mul(x - y, w1R, m);
+        v[r]             = s;
+        v[r | 8]         = min(d, d + m.Q);
+    }
+}
+// automorphism X -> X^k of both components (as automorphism_eval: every half-wave gets its own
+// component back in layout B'), plus acc0' gathered into layout C for inv_wave_s
+FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* region, const uint32_t* region0,
+                               int l, int L, uint32_t k) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) region[l * 33 + r] = v[r];
+    wave_lds_sync();
+    const uint32_t cl = (2 * (__builtin_bitreverse32((uint32_t)l) >> 27) + 1) * k;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
+        const uint32_t t  = ((cl + sr) & 2047) >> 1;
+        const uint32_t sx = __builtin_bitreverse32(t) >> 22;
+        v[r]              = region[sx + (sx >> 5)];
+    }
+    // layout C: x = (H << 8) | (L << 2) | j, 2 brv10(x) + 1 = brv2(j) << 9 | brv6(L) << 3 | brv2(H) << 1 | 1
+    const uint32_t cL = (((__builtin_bitreverse32((uint32_t)L) >> 26) << 3) + 1) * k;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t H = (uint32_t)r >> 2, j = (uint32_t)r & 3;
+        const uint32_t su = ((((j & 1) << 1 | j >> 1) << 9) + (((H & 1) << 1 | H >> 1) << 1)) * k;  // uniform
+        const uint32_t t  = ((cL + su) & 2047) >> 1;
+        const uint32_t sx = __builtin_bitreverse32(t) >> 22;
+        a0[r]             = region0[sx + (sx >> 5)];
+    }
+    wave_lds_sync();
+}
+
 }  // namespace
 
 // DM: the AP/DM accumulator runs the same op loop with external products only (AddToAccDM ==
@@ -959,6 +1112,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         s_twBf[i] = T.twB_fwd[i];
         s_twBi[i] = T.twB_inv[i];
     }
+    uint32_t* s_tabI = s_tile + kWaves * 2 * kTile;  // FHE_AUTO_WIDE: TableI (1024 words)
+    if (!DM && FHE_AUTO_WIDE)
+        for (int i = threadIdx.x; i < 1024; i += 256) s_tabI[i] = T.tabI[i];
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
     const uint32_t gate = blockIdx.x * kWaves + wave;
@@ -1103,6 +1259,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
             }
             asm volatile("" : "+s"(kexp));  // no reuse of the prologue's (2N - 5) index math (spills)
+#if FHE_AUTO_WIDE
+            {
+                // acc0' across the wave: layout C -> canonical COEF layout A (16 per lane), its two
+                // digits scattered into the two tiles in A' order (digit A for half 0, B for half 1)
+                uint32_t a0[16];
+                automorphism_wide(acc, a0, tile, tileW, l, lane, kexp);
+                inv_wave_s<20, LZ>(a0, tileW, lane, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    uint32_t x, y;
+                    decompose2<true>(a0[r], dec, x, y);
+                    const uint32_t c = ((uint32_t)r << 6) | (uint32_t)lane;
+                    tileW[(c & 31) * 33 + (c >> 5)]         = x;
+                    tileW[kTile + (c & 31) * 33 + (c >> 5)] = y;
+                }
+                wave_lds_sync();
+#pragma unroll
+                for (int r = 0; r < 32; ++r) dA[r] = tile[l * 33 + r];
+                wave_lds_sync();
+            }
+#else
             automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
@@ -1114,6 +1291,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
                 dA[r]   = sw[0];
             }
+#endif
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
 #if FHE_ROW_U4
             const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
@@ -1392,7 +1570,7 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
                                    uint32_t* ext_a, uint32_t* ext_b, bool dm, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
-    const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile) * 4;
+    const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile + (!dm && FHE_AUTO_WIDE ? 1024 : 0)) * 4;
     const uint2* k  = reinterpret_cast<const uint2*>(bsk);
     const uint2* ak = reinterpret_cast<const uint2*>(autok);
     const bool lz   = t.Q < (1u << 27);

@@ -42,7 +42,7 @@ void Engine::build_tables() {
     const uint64_t Q = p_.Q;
     HostNtt h;
     h.init(p_.N, Q, p_.psi);
-    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2 * (kMonoHalfWords + kMonoTableWords), 0);
+    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2 * (kMonoHalfWords + kMonoTableWords) + 1024, 0);
     uint32_t* twAf = t.data();
     uint32_t* twAi = twAf + 32;
     uint32_t* twBf = twAi + 32;
@@ -51,6 +51,8 @@ void Engine::build_tables() {
     uint32_t* monoF = mono + kMonoHalfWords;
     uint32_t* monoP = monoF + kMonoTableWords;
     uint32_t* monoPF = monoP + kMonoHalfWords;
+    uint32_t* tabI = monoPF + kMonoTableWords;
+    for (uint32_t i = 0; i < 1024 && i < p_.N; ++i) tabI[i] = to_mont(h.tabI[i], Q);
     for (int i = 0; i < 32; ++i) {
         twAf[i] = to_mont(h.tab[i], Q);
         twAi[i] = to_mont(h.tabI[i], Q);
@@ -108,6 +110,7 @@ void Engine::build_tables() {
     tabs_.mono_full = tabs_.mono + kMonoHalfWords;  // kMonoTableWords words
     tabs_.monoP = tabs_.mono_full + kMonoTableWords;
     tabs_.monoP_full = tabs_.monoP + kMonoHalfWords;
+    tabs_.tabI = tabs_.monoP_full + kMonoTableWords;
     tabs_.Q = (uint32_t)Q;
     tabs_.Q2 = (uint32_t)(2 * Q);
     tabs_.qinv = neg_inv32((uint32_t)Q);
