@@ -1149,7 +1149,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 
     const Dec dec     = make_dec(m.Q, g.gbits);
     const uint16_t* gops = ops + (size_t)gate * maxops;
-    const uint32_t cnt   = nops[gate];
+    const uint32_t cnt   = __builtin_amdgcn_readfirstlane(nops[gate]);  // uniform: a scalar loop
     // Signed residues throughout (Q < 2^28): acc in (-2Q, 2Q) between ops (one signed Montgomery
     // reduction of the digit x key sum), signed inverse NTT to canonical COEF, balanced digits as
     // signed words, signed forward NTT (FM 1 for Q < 2^27, FM 2 above).
