@@ -166,6 +166,32 @@ def test_gpu_ragged_batches_vs_oracle(name, restatement):
 
 
 @pytest.mark.gpu
+def test_gpu_lmkcdey_on_std128_vs_oracle(restatement):
+    """the LMKCDEY accumulator on the STD128 parameter set (Q < 2^27: the op-list kernel's
+    lazy-reduction instantiation, which the STD128_LMKCDEY set (Q < 2^28) never runs), vs the
+    oracle restatement, on seeded keys and ragged batches.  (GINX on STD128_LMKCDEY is not a
+    valid pairing: its Gaussian secret has coefficients outside {-1, 0, 1}, which the CGGI
+    ternary keys cannot encode.)"""
+    from fhe_amd import binfhe as bf
+    from oracle_lib import Restatement
+    ps, m = bf.STD128, bf.LMKCDEY
+    keys = bf.keygen(ps, m, 0xC0550001)
+    O = Restatement(ps, m)
+    e = bf.GateEngine(ps, m)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    rng = np.random.default_rng(13)
+    for count, gate in ((1, 1), (5, 4), (11, 3), (33, 0)):
+        x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+        a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 300 + count)
+        a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 400 + count)
+        ao, bo = e.eval_gate(gate, a1, b1, a2, b2)
+        oa, ob = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, gate, a1, b1, a2, b2)
+        assert np.array_equal(ao, oa) and np.array_equal(bo, ob), (count, gate)
+        dec = bf.decrypt(ps, m, keys.sk, ao, bo)
+        assert np.array_equal(dec, TRUTH[gate](x1, x2).astype(np.int64))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", SETS)
 def test_gpu_keyswitch_kernels_vs_oracle(name, restatement):
     """both key-switch kernels (per-gate below 4096 ciphertexts, gate-tiled at and above,
