@@ -23,6 +23,16 @@ from ._lib import FheHipError, check, lib, ptr, sz, u64, vp
 
 # reference enum values (src/binfhe/include/binfhe-constants.h:49-126)
 TOY, STD128_AP, STD128, STD128_LMKCDEY = 0, 2, 3, 21
+LARGE = 1 << 30
+
+
+def large_paramset(paramset, arbFunc, logQ, N=0):
+    """paramset code of GenerateBinFHEContext(paramset, arbFunc, logQ, N, GINX, False)
+    (binfhecontext.cpp:55-104), the large-precision family (54-bit Q, N = 2048, qKS = 2^35)"""
+    logN = 0 if not N else N.bit_length() - 1
+    if N and N != 1 << logN:
+        raise ValueError("N must be a power of two")
+    return LARGE | (paramset << 16) | (int(bool(arbFunc)) << 15) | (logN << 8) | int(logQ)
 AP, GINX, LMKCDEY = 1, 2, 3
 OR, AND, NOR, NAND, XOR, XNOR, MAJORITY, AND3, OR3, AND4, OR4, XOR_FAST, XNOR_FAST, CMUX = range(14)
 GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR, "MAJORITY": MAJORITY,
@@ -31,9 +41,9 @@ MULTI_GATES = (MAJORITY, AND3, OR3, AND4, OR4)
 
 
 class _Params(ctypes.Structure):
-    _fields_ = [(f, ctypes.c_uint32) for f in ("paramset", "method", "n", "N", "q", "qKS", "baseKS", "digitsKS",
-                                               "baseG", "digitsG", "numAutoKeys", "keyDist")] + \
-               [(f, ctypes.c_uint64) for f in ("Q", "psi", "bsk_words", "ksk_rows")]
+    _fields_ = [(f, ctypes.c_uint32) for f in ("paramset", "method", "n", "N", "q", "baseKS", "digitsKS",
+                                               "baseG", "digitsG", "numAutoKeys", "keyDist", "reserved")] + \
+               [(f, ctypes.c_uint64) for f in ("Q", "psi", "qKS", "bsk_words", "ksk_rows")]
 
 
 def _setup(L):
@@ -108,15 +118,16 @@ class Params:
     n: int
     N: int
     q: int
-    qKS: int
     baseKS: int
     digitsKS: int
     baseG: int
     digitsG: int
     numAutoKeys: int
     keyDist: int
+    reserved: int
     Q: int
     psi: int
+    qKS: int
     bsk_words: int
     ksk_rows: int
 
@@ -548,7 +559,20 @@ class BinFHEContext:
         self._ctr = 0
         self.engine = None
 
-    def GenerateBinFHEContext(self, paramset=STD128, method=GINX):
+    def GenerateBinFHEContext(self, paramset=STD128, method=GINX, *args, logQ=None, N=0, timeOptimization=False):
+        """GenerateBinFHEContext(set, method) (binfhecontext.cpp:106-179), or the large-precision
+        overload GenerateBinFHEContext(set, arbFunc, logQ = 11, N = 0, method = GINX,
+        timeOptimization = False) (:55-104) when the second argument is a bool"""
+        if isinstance(method, bool):
+            arb = method
+            rest = list(args)
+            logQ = rest.pop(0) if rest else (11 if logQ is None else logQ)
+            N = rest.pop(0) if rest else N
+            method = rest.pop(0) if rest else GINX
+            timeOptimization = rest.pop(0) if rest else timeOptimization
+            if timeOptimization:
+                raise FheHipError(-2, "timeOptimization (dynamic baseG) is not supported")
+            paramset = large_paramset(paramset, arb, logQ, N)
         self.paramset, self.method = paramset, method
         self.params = params(paramset, method)
         self.engine = GateEngine(paramset, method, self.device)

@@ -72,6 +72,9 @@ struct GateArgs {
     uint32_t xor_double;              // XOR/XNOR: 2 (ct1 + ct2)
     uint32_t msb_out;                 // 1: write ctExt mod-switched to qKS; 0: raw ctExt mod Q
     uint32_t gbits;                   // log2(baseG)
+    // the large-precision family (boot_wide.h): the same window / test vector / b with 64-bit Q
+    uint64_t lv64, uv64, b64;
+    const uint64_t* tv64;
 };
 
 // The LWE ciphertext a gate bootstraps: ct = sum_j (-1)^{neg_j} ct_j + (0, boff) mod q, then

@@ -1,0 +1,333 @@
+// bootstrap_wide.hip -- gate / functional bootstrapping of the large-precision family
+// (boot_wide.h): 64-bit accumulator residues, N = 2048 (or 1024).
+//
+// One workgroup of N/4 threads per bootstrap.  Thread t owns the EVALUATION slots
+// j = t + (N/4) r, r < 4, of both accumulator polynomials in registers; the transforms run
+// radix-2 through one 2N-word LDS buffer (two polynomials at once).  Per accumulator index i
+// (rgsw-acc-cggi.cpp:59-151), skipped when its monomial exponent is 0 (X^0 - 1 = 0):
+//   1. both accumulators to COEF (inverse NTT, the N^-1 folded into the coefficient reads);
+//   2. SignedDigitDecompose (rgsw-acc.cpp:54-91) kept as a running signed 64-bit state per
+//      coefficient, one gadget level at a time: level L's two digit polynomials (from acc0 and
+//      acc1) are written to LDS and forward-transformed;
+//   3. every slot accumulates digit x key products for the 2 signs x 2 components in 128 bits
+//      (keys stored in Montgomery form K 2^64 mod Q: one reduction per sum);
+//   4. acc_c += S+_c (X^m - 1) + S-_c (X^-m - 1), the monomials EVAL(X^m) = psi^((2 brv(j)+1) m)
+//      from one 2N-entry power table.
+// Keys are read straight from HBM, coalesced (consecutive threads, consecutive slots).
+#include "boot_wide.h"
+
+namespace fhe_amd {
+
+namespace {
+#define WD __device__ __forceinline__
+
+struct U128 {
+    uint64_t lo, hi;
+};
+
+WD void mac(U128& s, uint64_t a, uint64_t b) {
+    const uint64_t lo = a * b, hi = __umul64hi(a, b);
+    s.lo += lo;
+    s.hi += hi + (s.lo < lo ? 1 : 0);
+}
+// t < Q 2^64  ->  t 2^-64 mod Q in [0, Q)
+WD uint64_t redc(const U128& t, uint64_t Q, uint64_t qinv) {
+    const uint64_t u = t.lo * qinv;
+    const uint64_t r = t.hi + __umul64hi(u, Q) + (t.lo != 0 ? 1 : 0);
+    return r >= Q ? r - Q : r;
+}
+// x w mod Q for w < Q, ws = floor(w 2^64 / Q), any 64-bit x
+WD uint64_t mul_shoup(uint64_t x, uint64_t w, uint64_t ws, uint64_t Q) {
+    const uint64_t r = x * w - __umul64hi(x, ws) * Q;
+    return r >= Q ? r - Q : r;
+}
+WD uint64_t add_q(uint64_t a, uint64_t b, uint64_t Q) {
+    const uint64_t s = a + b;
+    return s >= Q ? s - Q : s;
+}
+WD uint64_t sub_q(uint64_t a, uint64_t b, uint64_t Q) { return a >= b ? a - b : a + Q - b; }
+
+// RoundqQ(v, q, Q) = floor(0.5 + double(v) double(q) / double(Q)) mod q (lwe-pke.cpp:41-46), in
+// IEEE double like the reference (no contraction: the product is divided before the add)
+WD uint64_t round_qQ(uint64_t v, uint64_t q, uint64_t Q) {
+#pragma clang fp contract(off)
+    const double x = (double)v * (double)q / (double)Q;
+    return (uint64_t)floor(0.5 + x) % q;
+}
+
+// Merged Cooley-Tukey forward transform in place on NB polynomials at buf + p N (bit-reversed
+// output, ForwardTransformToBitReverseInPlace transformnat-impl.h:302-373); all threads, synced.
+template <int LOGN, int NB>
+WD void ntt_fwd(uint64_t* buf, const WideTables& tb) {
+    constexpr int N = 1 << LOGN, T = N / 4;
+    const uint64_t Q = tb.Q;
+#pragma unroll 1
+    for (int s = 0; s < LOGN; ++s) {
+        const int logt = LOGN - 1 - s, t = 1 << logt;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int b = (int)threadIdx.x + T * k;
+            const int i = b >> logt;
+            const int j = (i << (logt + 1)) | (b & (t - 1));
+            const uint64_t w = tb.tab[(1 << s) + i], ws = tb.tabS[(1 << s) + i];
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                const uint64_t U = buf[p * N + j];
+                const uint64_t V = mul_shoup(buf[p * N + j + t], w, ws, Q);
+                buf[p * N + j]     = add_q(U, V, Q);
+                buf[p * N + j + t] = sub_q(U, V, Q);
+            }
+        }
+        __syncthreads();
+    }
+}
+// Gentleman-Sande inverse (InverseTransformFromBitReverseInPlace :511-624) WITHOUT the final
+// N^-1 scaling (the readers apply it)
+template <int LOGN, int NB>
+WD void ntt_inv(uint64_t* buf, const WideTables& tb) {
+    constexpr int N = 1 << LOGN, T = N / 4;
+    const uint64_t Q = tb.Q;
+#pragma unroll 1
+    for (int s = 0; s < LOGN; ++s) {
+        const int logt = s, t = 1 << logt, m = N >> (s + 1);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int b = (int)threadIdx.x + T * k;
+            const int i = b >> logt;
+            const int j = (i << (logt + 1)) | (b & (t - 1));
+            const uint64_t w = tb.tabI[m + i], ws = tb.tabIS[m + i];
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                const uint64_t U = buf[p * N + j], V = buf[p * N + j + t];
+                buf[p * N + j]     = add_q(U, V, Q);
+                buf[p * N + j + t] = mul_shoup(sub_q(U, V, Q), w, ws, Q);
+            }
+        }
+        __syncthreads();
+    }
+}
+}  // namespace
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 4)
+    k_blind_rotate_wide(WideArgs g, WideTables tb, const uint64_t* __restrict__ bsk, const uint16_t* __restrict__ idx,
+                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b) {
+    constexpr int N = 1 << LOGN, T = N / 4, S = 4;
+    __shared__ uint64_t buf[2 * N];
+    const uint32_t gate = blockIdx.x, t = threadIdx.x;
+    const uint64_t Q = tb.Q, QHalf = Q >> 1;
+    const uint32_t dG2 = (g.digitsG - 1) * 2, gb = g.gbits, sh = 64 - gb;
+
+    // test vector (BootstrapGateCore binfhe-base-scheme.cpp:556-575 / BootstrapFuncCore :596-608):
+    // acc1 = NTT(m), acc0 = 0
+    uint64_t acc0[S], acc1[S];
+    {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const uint32_t x = t + T * r;
+            uint64_t v = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            buf[x] = v;
+        }
+        __syncthreads();
+        ntt_fwd<LOGN, 1>(buf, tb);
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            acc0[r] = 0;
+            acc1[r] = buf[t + T * r];
+        }
+    }
+
+    const uint16_t* gi = idx + (size_t)gate * g.n;
+    const size_t key_stride = (size_t)2 * dG2 * 2 * N;  // [2 signs][dG2][2][N] per index
+#pragma unroll 1
+    for (uint32_t i = 0; i < g.n; ++i) {
+        const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)gi[i]);
+        if (m == 0) continue;  // AddToAccCGGI with X^0 - 1 = 0 leaves acc unchanged
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            buf[t + T * r]     = acc0[r];
+            buf[N + t + T * r] = acc1[r];
+        }
+        __syncthreads();
+        ntt_inv<LOGN, 2>(buf, tb);
+        // SignedDigitDecompose state: centred value, lowest digit dropped
+        int64_t d[2][S];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                const uint64_t v = mul_shoup(buf[p * N + t + T * r], tb.ninv, tb.ninvS, Q);
+                int64_t x = v < QHalf ? (int64_t)v : (int64_t)v - (int64_t)Q;
+                const int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
+                d[p][r] = (x - r0) >> gb;
+            }
+        U128 acc[2][2][S];  // [sign][component][slot]
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < S; ++r) acc[sg][c][r] = U128{0, 0};
+        const uint64_t* key = bsk + (size_t)i * key_stride;
+#pragma unroll 1
+        for (uint32_t L = 0; 2 * L < dG2; ++L) {
+            __syncthreads();  // previous readers of buf are done
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int r = 0; r < S; ++r) {
+                    const int64_t x = d[p][r];
+                    int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
+                    d[p][r] = (x - r0) >> gb;
+                    if (r0 < 0) r0 += (int64_t)Q;
+                    buf[p * N + t + T * r] = (uint64_t)r0;
+                }
+            __syncthreads();
+            ntt_fwd<LOGN, 2>(buf, tb);
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                const uint32_t j = t + T * r;
+                const uint64_t x0 = buf[j], x1 = buf[N + j];
+#pragma unroll
+                for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const uint64_t* k0 = key + ((size_t)(sg * dG2 + 2 * L) * 2 + c) * N;
+                        mac(acc[sg][c][r], x0, k0[j]);
+                        mac(acc[sg][c][r], x1, k0[2 * N + j]);  // row 2L + 1
+                    }
+            }
+        }
+        // acc_c += S+_c (X^m - 1) + S-_c (X^-m - 1)
+        const uint32_t mneg = 2 * N - m, emask = 2 * N - 1;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const uint32_t j = t + T * r;
+            const uint32_t e = 2 * (__brev(j) >> (32 - LOGN)) + 1;
+            const uint64_t mp = sub_q(tb.psiM[(e * m) & emask], tb.oneM, Q);
+            const uint64_t mn = sub_q(tb.psiM[(e * mneg) & emask], tb.oneM, Q);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                U128 z{0, 0};
+                mac(z, redc(acc[0][c][r], Q, tb.qinv), mp);
+                mac(z, redc(acc[1][c][r], Q, tb.qinv), mn);
+                const uint64_t add = redc(z, Q, tb.qinv);
+                if (c == 0) acc0[r] = add_q(acc0[r], add, Q);
+                else acc1[r] = add_q(acc1[r], add, Q);
+            }
+        }
+    }
+
+    // extraction (binfhe-base-scheme.cpp:110-121, :616-626): Transpose(acc0) then COEF: coefficient
+    // k of acc0(X^-1) is -a_(N-k) (k >= 1), a_0 for k = 0; b = b_const + acc1[0]
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        buf[t + T * r]     = acc0[r];
+        buf[N + t + T * r] = acc1[r];
+    }
+    __syncthreads();
+    ntt_inv<LOGN, 2>(buf, tb);
+    uint64_t* oa = ext_a + (size_t)gate * N;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const uint32_t x = t + T * r;
+        const uint64_t c = mul_shoup(buf[x == 0 ? 0 : N - x], tb.ninv, tb.ninvS, Q);
+        const uint64_t v = (x == 0 || c == 0) ? c : Q - c;
+        oa[x] = g.msb_out ? round_qQ(v, g.qKS, Q) : v;
+    }
+    if (t == 0) {
+        const uint64_t bb = add_q(g.b_const % Q, mul_shoup(buf[N], tb.ninv, tb.ninvS, Q), Q);
+        ext_b[gate] = g.msb_out ? round_qQ(bb, g.qKS, Q) : bb;
+    }
+}
+
+hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
+                                    const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if ((g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 || g.factor == 0 ||
+        g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
+        return hipErrorInvalidValue;
+    if (g.N == 2048)
+        hipLaunchKernelGGL(k_blind_rotate_wide<11>, dim3(g.count), dim3(512), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_wide<10>, dim3(g.count), dim3(256), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// KeySwitch mod qKS = 2^k (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out): one workgroup per
+// ciphertext, thread t owns columns t + blockDim c of the n-wide A rows (u64, read coalesced)
+// and thread 0 also the B column; the 2^35 values of N digitsKS rows sum below 2^64 unreduced.
+// ---------------------------------------------------------------------------
+constexpr int kKsWideCols = 8;
+
+__global__ void __launch_bounds__(256)
+    k_keyswitch_wide(uint32_t n, uint32_t N, uint32_t logBase, uint32_t digitsKS, uint64_t qKS,
+                     const uint64_t* __restrict__ A, const uint64_t* __restrict__ B, const uint64_t* __restrict__ ms_a,
+                     const uint64_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
+                     uint64_t* __restrict__ b_out) {
+    __shared__ uint64_t s_a[2048];
+    const uint32_t gate = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    for (uint32_t i = t; i < N; i += nt) s_a[i] = ms_a[(size_t)gate * N + i];
+    __syncthreads();
+    const uint64_t mask = (1ull << logBase) - 1;
+    uint64_t acc[kKsWideCols] = {};
+    uint64_t accb = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < N; ++i) {
+        const uint64_t ai = s_a[i];
+#pragma unroll 1
+        for (uint32_t j = 0; j < digitsKS; ++j) {
+            const uint64_t row = ((uint64_t)i << logBase | ((ai >> (logBase * j)) & mask)) * digitsKS + j;
+            const uint64_t* Ar = A + row * n;
+#pragma unroll
+            for (int c = 0; c < kKsWideCols; ++c) {
+                const uint32_t k = t + nt * c;
+                if (k < n) acc[c] += Ar[k];
+            }
+            if (t == 0) accb += B[row];
+        }
+    }
+    const uint64_t qm = qKS - 1;
+    uint64_t* oa = a_out + (size_t)gate * n;
+#pragma unroll
+    for (int c = 0; c < kKsWideCols; ++c) {
+        const uint32_t k = t + nt * c;
+        if (k < n) {
+            const uint64_t v = (0 - acc[c]) & qm;
+            oa[k] = q_out ? round_qQ(v, q_out, qKS) : v;
+        }
+    }
+    if (t == 0) {
+        const uint64_t v = (ms_b[gate] - accb) & qm;
+        b_out[gate] = q_out ? round_qQ(v, q_out, qKS) : v;
+    }
+}
+
+hipError_t launch_keyswitch_wide(size_t count, uint32_t n, uint32_t N, uint32_t baseKS, uint32_t digitsKS, uint64_t qKS,
+                                 const uint64_t* A, const uint64_t* B, const uint64_t* ms_a, const uint64_t* ms_b,
+                                 uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (N > 2048 || (qKS & (qKS - 1)) || (baseKS & (baseKS - 1)) || baseKS < 2 || count > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    uint32_t logBase = 0;
+    while ((1u << logBase) < baseKS) ++logBase;
+    uint32_t nt = (n + 63) / 64 * 64;
+    if (nt > 256) nt = 256;
+    if ((size_t)nt * kKsWideCols < n) return hipErrorInvalidValue;
+    // the digits must cover log2(qKS) bits and the unreduced column sums must fit 64 bits
+    if ((uint64_t)logBase * digitsKS < 64 && (qKS >> (logBase * digitsKS)) > 1) return hipErrorInvalidValue;
+    if ((double)N * digitsKS * (double)qKS >= 18446744073709551616.0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_keyswitch_wide, dim3((uint32_t)count), dim3(nt), 0, s, n, N, logBase, digitsKS, qKS, A, B,
+                       ms_a, ms_b, q_out, a_out, b_out);
+    return hipGetLastError();
+}
+
+}  // namespace fhe_amd

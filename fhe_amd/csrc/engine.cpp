@@ -18,6 +18,19 @@ inline uint32_t neg_inv32(uint32_t Q) {  // -Q^-1 mod 2^32 (Newton)
 }  // namespace
 
 Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, method)), device_(device) {
+    if (is_large(paramset)) {  // 64-bit accumulator (bootstrap_wide.hip)
+        wide_ = true;
+        if (p_.N != 1024 && p_.N != 2048)
+            throw std::invalid_argument("device path supports N = 1024 / 2048 for the large-precision family");
+        if ((double)p_.digitsG2 * (double)p_.Q >= 18446744073709551616.0)
+            throw std::invalid_argument("device path: digitsG2 * Q must stay below 2^64");
+        if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
+        if (p_.n > 2048) throw std::invalid_argument("device path supports n <= 2048");
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        build_tables_wide();
+        return;
+    }
     if (p_.N != 1024) throw std::invalid_argument("device path supports ring dimension N = 1024 (STD128 sets)");
     if (p_.Q >= (1ull << 28)) throw std::invalid_argument("device path needs Q < 2^28");
     if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
@@ -33,7 +46,8 @@ Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_})
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
+                      d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_})
         if (ptr) (void)hipFree(ptr);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -119,9 +133,61 @@ void Engine::build_tables() {
     tabs_.oneR = to_mont(1, Q);
 }
 
+void Engine::build_tables_wide() {
+    const uint64_t Q = p_.Q;
+    const uint32_t N = p_.N;
+    HostNtt h;
+    h.init(N, Q, p_.psi);
+    std::vector<uint64_t> t(6 * (size_t)N);
+    for (uint32_t i = 0; i < N; ++i) {
+        t[i] = h.tab[i];
+        t[N + i] = shoup64(h.tab[i], Q);
+        t[2 * N + i] = h.tabI[i];
+        t[3 * N + i] = shoup64(h.tabI[i], Q);
+    }
+    const uint64_t R = (uint64_t)(((u128)1 << 64) % Q);  // Montgomery 1
+    uint64_t x = 1;
+    for (uint32_t e = 0; e < 2 * N; ++e) {
+        t[4 * N + e] = mulmod(x, R, Q);
+        x = mulmod(x, p_.psi, Q);
+    }
+    FHE_HIP_CHECK(hipMalloc(&d_wtables_, t.size() * 8));
+    FHE_HIP_CHECK(hipMemcpy(d_wtables_, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    const uint64_t* d = static_cast<const uint64_t*>(d_wtables_);
+    wtabs_.tab = d;
+    wtabs_.tabS = d + N;
+    wtabs_.tabI = d + 2 * N;
+    wtabs_.tabIS = d + 3 * N;
+    wtabs_.psiM = d + 4 * N;
+    wtabs_.Q = Q;
+    uint64_t inv = Q;  // Q^-1 mod 2^64 (Newton)
+    for (int i = 0; i < 6; ++i) inv *= 2 - Q * inv;
+    wtabs_.qinv = 0 - inv;
+    wtabs_.ninv = h.ninv;
+    wtabs_.ninvS = shoup64(h.ninv, Q);
+    wtabs_.oneM = R;
+}
+
 void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     if (!bsk) throw std::invalid_argument("bsk is null");
     if (words != p_.bsk_words()) throw std::invalid_argument("bsk has wrong length");
+    if (wide_) {  // raw layout [n][2][dG2][2][N], Montgomery form K 2^64 mod Q (bootstrap_wide.hip)
+        const uint64_t Q = p_.Q;
+        std::vector<uint64_t> dev(words);
+        bool bad = false;
+#pragma omp parallel for schedule(static) reduction(|| : bad)
+        for (int64_t i = 0; i < (int64_t)words; ++i) {
+            bad = bad || bsk[i] >= Q;
+            dev[i] = (uint64_t)(((u128)(bsk[i] % Q) << 64) % Q);
+        }
+        if (bad) throw std::invalid_argument("bsk coefficient not reduced mod Q");
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        if (d_bsk_) FHE_HIP_CHECK(hipFree(d_bsk_));
+        d_bsk_ = nullptr;
+        FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * 8));
+        FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), words * 8, hipMemcpyHostToDevice));
+        return;
+    }
     const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
     const uint64_t Q = p_.Q;
     if (dG2 != 4) throw std::invalid_argument("device path expects digitsG = 3");
@@ -190,6 +256,20 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
     if (!A || !B) throw std::invalid_argument("ksk is null");
     const size_t rows = p_.ksk_rows();
     if (nA != rows * p_.n || nB != rows) throw std::invalid_argument("ksk has wrong length");
+    if (wide_) {  // u64 A [rows][n] ++ B [rows] as given
+        bool bad = false;
+#pragma omp parallel for schedule(static) reduction(|| : bad)
+        for (int64_t r = 0; r < (int64_t)nA; ++r) bad = bad || A[r] >= p_.qKS;
+        for (size_t r = 0; r < nB; ++r) bad = bad || B[r] >= p_.qKS;
+        if (bad) throw std::invalid_argument("ksk value not reduced mod qKS");
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        if (d_wksk_) FHE_HIP_CHECK(hipFree(d_wksk_));
+        d_wksk_ = nullptr;
+        FHE_HIP_CHECK(hipMalloc(&d_wksk_, (nA + nB) * 8));
+        FHE_HIP_CHECK(hipMemcpy(d_wksk_, A, nA * 8, hipMemcpyHostToDevice));
+        FHE_HIP_CHECK(hipMemcpy(d_wksk_ + nA, B, nB * 8, hipMemcpyHostToDevice));
+        return;
+    }
     std::vector<uint16_t> dev(rows * 512, 0);
     bool bad = false;
 #pragma omp parallel for schedule(static) reduction(|| : bad)
@@ -215,6 +295,16 @@ void Engine::keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t
     if (!sk) throw std::invalid_argument("secret key is null");
     if (n != p_.n) throw std::invalid_argument("secret key has wrong length");
     const std::vector<uint64_t> s(sk, sk + n);
+    if (wide_) {  // large-precision family: the host generator (keygen.cpp), then the upload
+        KeySet ks;
+        keygen_bootstrap(p_, s, seed, ks);
+        load_bsk(ks.bsk.data(), ks.bsk.size());
+        load_ksk(ks.kskA.data(), ks.kskA.size(), ks.kskB.data(), ks.kskB.size());
+        if (bsk_out) std::copy(ks.bsk.begin(), ks.bsk.end(), bsk_out);
+        if (kskA_out) std::copy(ks.kskA.begin(), ks.kskA.end(), kskA_out);
+        if (kskB_out) std::copy(ks.kskB.begin(), ks.kskB.end(), kskB_out);
+        return;
+    }
     const size_t words = p_.bsk_words(), rows = p_.ksk_rows();
     FHE_HIP_CHECK(hipSetDevice(device_));
     if (d_bsk_) FHE_HIP_CHECK(hipFree(d_bsk_));
@@ -284,6 +374,10 @@ GateArgs Engine::gate_args(int gate, size_t count, uint32_t p, bool multi) const
     g.factor = (uint32_t)(p_.N / qHalf);
     // b = Q/8 + 1 for 2-input gates (:118, hardcoded p = 4), Q/(2p) + 1 for ctvector gates (:162)
     g.b_const = (uint32_t)(multi ? Q / (2 * p) + 1 : (Q >> 3) + 1);
+    g.lv64 = swap ? Q2p : Q2pNeg;
+    g.uv64 = swap ? Q2pNeg : Q2p;
+    g.b64 = multi ? Q / (2 * p) + 1 : (Q >> 3) + 1;
+    g.tv64 = nullptr;
     g.xor_double = (gate == G_XOR || gate == G_XNOR || gate == G_XOR_FAST || gate == G_XNOR_FAST) ? 1 : 0;
     g.msb_out = 1;
     g.gbits = p_.gBits;
@@ -294,13 +388,19 @@ void Engine::ensure_work(size_t count) {
     if (count <= cap_) return;
     FHE_HIP_CHECK(hipSetDevice(device_));
     FHE_HIP_CHECK(hipStreamSynchronize(stream_));
-    for (void* ptr : {(void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_, (void*)d_ext_b_})
+    for (void* ptr : {(void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_, (void*)d_ext_b_, (void*)d_wext_a_, (void*)d_wext_b_})
         if (ptr) FHE_HIP_CHECK(hipFree(ptr));
     d_idx_ = nullptr; d_tvb_ = nullptr; d_ext_a_ = nullptr; d_ext_b_ = nullptr; cap_ = 0;
+    d_wext_a_ = nullptr; d_wext_b_ = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d_idx_, count * p_.n * sizeof(uint16_t)));
     FHE_HIP_CHECK(hipMalloc(&d_tvb_, count * sizeof(uint32_t)));
-    FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
-    FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
+    if (wide_) {
+        FHE_HIP_CHECK(hipMalloc(&d_wext_a_, count * p_.N * sizeof(uint64_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_wext_b_, count * sizeof(uint64_t)));
+    } else {
+        FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
+    }
     if (p_.method == M_LMKCDEY || p_.method == M_AP) {
         for (void* ptr : {(void*)d_ops_, (void*)d_nops_})
             if (ptr) FHE_HIP_CHECK(hipFree(ptr));
@@ -338,6 +438,27 @@ void Engine::prep_device(const GateArgs& g, const GateInputs& in, size_t offset,
 }
 
 void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
+    if (wide_) {
+        WideArgs w{};
+        w.count = g.count;
+        w.n = g.n;
+        w.N = g.N;
+        w.ctmod = g.ctmod;
+        w.factor = g.factor;
+        w.lb = g.lb;
+        w.ub = g.ub;
+        w.digitsG = p_.digitsG;
+        w.gbits = p_.gBits;
+        w.msb_out = g.msb_out;
+        w.lv = g.lv64;
+        w.uv = g.uv64;
+        w.b_const = g.b64;
+        w.qKS = p_.qKS;
+        w.tv = g.tv64;
+        FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_), d_idx_, d_tvb_,
+                                               d_wext_a_, d_wext_b_, s));
+        return;
+    }
     // the kernels' digit decomposition (bootstrap.hip decompose2) works on d + C in 32 bits
     const uint64_t h = 1ull << (g.gbits - 1);
     if (g.gbits < 2 || h * (1 + (1ull << g.gbits) + (1ull << (2 * g.gbits))) + p_.Q >= (1ull << 32))
@@ -418,12 +539,38 @@ void Engine::eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* 
 }
 
 void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
-    if (!d_ksk_) throw std::logic_error("key-switching key not loaded");
+    if (!d_ksk_ && !d_wksk_) throw std::logic_error("key-switching key not loaded");
     if (count == 0) return;
     if (count > cap_) throw std::logic_error("workspace holds fewer ciphertexts than requested");
-    GateArgs g = gate_args(G_AND, count);
     FHE_HIP_CHECK(hipSetDevice(device_));
-    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, p_.q, a_out, b_out, s));
+    keyswitch_ext(count, p_.q, a_out, b_out, s);
+}
+
+void Engine::keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    if (wide_) {
+        const size_t rows = p_.ksk_rows();
+        FHE_HIP_CHECK(launch_keyswitch_wide(count, p_.n, p_.N, p_.baseKS, p_.digitsKS, p_.qKS, d_wksk_,
+                                            d_wksk_ + rows * p_.n, d_wext_a_, d_wext_b_, q_out, a_out, b_out, s));
+        return;
+    }
+    GateArgs g = gate_args(G_AND, count);
+    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, q_out, a_out, b_out, s));
+}
+
+void Engine::copy_ext_host(size_t count, uint64_t* ext_a, uint64_t* ext_b) {
+    const size_t N = p_.N;
+    if (wide_) {
+        FHE_HIP_CHECK(hipMemcpyAsync(ext_a, d_wext_a_, count * N * 8, hipMemcpyDeviceToHost, stream_));
+        FHE_HIP_CHECK(hipMemcpyAsync(ext_b, d_wext_b_, count * 8, hipMemcpyDeviceToHost, stream_));
+        FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+        return;
+    }
+    std::vector<uint32_t> ha(count * N), hb(count);
+    FHE_HIP_CHECK(hipMemcpyAsync(ha.data(), d_ext_a_, count * N * 4, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(hb.data(), d_ext_b_, count * 4, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (size_t i = 0; i < count * N; ++i) ext_a[i] = ha[i];
+    for (size_t i = 0; i < count; ++i) ext_b[i] = hb[i];
 }
 
 void Engine::eval_gate_device(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
@@ -471,20 +618,32 @@ void Engine::bootstrap_extended_host(int gate, size_t count, const uint64_t* a1,
     FHE_HIP_CHECK(hipMemcpyAsync(da2, a2, count * n * 8, hipMemcpyHostToDevice, stream_));
     FHE_HIP_CHECK(hipMemcpyAsync(db2, b2, count * 8, hipMemcpyHostToDevice, stream_));
     bootstrap_device(gate, count, da1, db1, da2, db2, false, stream_);
-    std::vector<uint32_t> ha(count * N), hb(count);
-    FHE_HIP_CHECK(hipMemcpyAsync(ha.data(), d_ext_a_, count * N * 4, hipMemcpyDeviceToHost, stream_));
-    FHE_HIP_CHECK(hipMemcpyAsync(hb.data(), d_ext_b_, count * 4, hipMemcpyDeviceToHost, stream_));
-    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
-    for (size_t i = 0; i < count * N; ++i) ext_a[i] = ha[i];
-    for (size_t i = 0; i < count; ++i) ext_b[i] = hb[i];
+    (void)N;
+    copy_ext_host(count, ext_a, ext_b);
 }
 
 void Engine::keyswitch_host(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out) {
-    if (!d_ksk_) throw std::logic_error("key-switching key not loaded");
+    if (!d_ksk_ && !d_wksk_) throw std::logic_error("key-switching key not loaded");
     if (count == 0) return;
     ensure_work(count);
     ensure_host_stage(count);
     const size_t N = p_.N;
+    if (wide_) {
+        for (size_t i = 0; i < count * N; ++i)
+            if (a[i] >= p_.qKS) throw std::invalid_argument("keyswitch input not reduced mod qKS");
+        for (size_t i = 0; i < count; ++i)
+            if (b[i] >= p_.qKS) throw std::invalid_argument("keyswitch input not reduced mod qKS");
+        uint64_t* dao = d_io_;
+        uint64_t* dbo = dao + count * p_.n;
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        FHE_HIP_CHECK(hipMemcpyAsync(d_wext_a_, a, count * N * 8, hipMemcpyHostToDevice, stream_));
+        FHE_HIP_CHECK(hipMemcpyAsync(d_wext_b_, b, count * 8, hipMemcpyHostToDevice, stream_));
+        keyswitch_ext(count, 0, dao, dbo, stream_);
+        FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * p_.n * 8, hipMemcpyDeviceToHost, stream_));
+        FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+        FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+        return;
+    }
     std::vector<uint32_t> ha(count * N), hb(count);
     for (size_t i = 0; i < count * N; ++i) {
         if (a[i] >= p_.qKS) throw std::invalid_argument("keyswitch input not reduced mod qKS");
@@ -543,12 +702,8 @@ void Engine::eval_gate_multi_host(int gate, size_t count, uint32_t k, const uint
         return;
     }
     eval_gate_multi_device(gate, count, k, da, db, p, nullptr, nullptr, stream_);
-    std::vector<uint32_t> ha(count * N), hb(count);
-    FHE_HIP_CHECK(hipMemcpyAsync(ha.data(), d_ext_a_, count * N * 4, hipMemcpyDeviceToHost, stream_));
-    FHE_HIP_CHECK(hipMemcpyAsync(hb.data(), d_ext_b_, count * 4, hipMemcpyDeviceToHost, stream_));
-    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
-    for (size_t i = 0; i < count * N; ++i) a_out[i] = ha[i];
-    for (size_t i = 0; i < count; ++i) b_out[i] = hb[i];
+    (void)N;
+    copy_ext_host(count, a_out, b_out);
 }
 
 void Engine::eval_cmux_host(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1,

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "boot.h"
+#include "boot_wide.h"
 #include "params.h"
 
 namespace fhe_amd {
@@ -42,7 +43,9 @@ public:
     const Params& params() const { return p_; }
     int device() const { return device_; }
     hipStream_t stream() const { return stream_; }
-    bool ready() const { return d_bsk_ && d_ksk_; }
+    bool ready() const { return d_bsk_ && (d_ksk_ || d_wksk_); }
+    // the large-precision family (64-bit accumulator, boot_wide.h)
+    bool wide() const { return wide_; }
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -123,6 +126,11 @@ private:
     void ensure_work(size_t count);
     void ensure_host_stage(size_t count);
     void build_tables();
+    void build_tables_wide();
+    // KeySwitch + ModSwitch(qKS -> q_out) of workspace slots [0, count) (q_out = 0: none)
+    void keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // ctExt of workspace slots [0, count) to host u64 arrays
+    void copy_ext_host(size_t count, uint64_t* ext_a, uint64_t* ext_b);
 
     Params p_;
     int device_;
@@ -152,6 +160,14 @@ private:
     // staging for host entry points: up to 4 inputs + one ctExt-sized output
     size_t hcap_ = 0;
     uint64_t* d_io_ = nullptr;
+    // large-precision family: u64 keys (Montgomery BSK, raw KSK A ++ B), tables, u64 ctExt
+    bool wide_ = false;
+    WideTables wtabs_{};
+    void* d_wtables_ = nullptr;
+    uint64_t* d_wksk_ = nullptr;
+    uint64_t* d_wext_a_ = nullptr;
+    uint64_t* d_wext_b_ = nullptr;
+    uint64_t* d_wtv_ = nullptr;
 };
 
 }  // namespace fhe_amd

@@ -78,16 +78,25 @@ void Engine::bootstrap_func_device(size_t count, const uint64_t* a, const uint64
     if (count > 0x7fffffffull) throw std::invalid_argument("batch too large");
     ensure_work(count);
     FHE_HIP_CHECK(hipSetDevice(device_));
-    if (!d_tv_) FHE_HIP_CHECK(hipMalloc(&d_tv_, 2 * (size_t)p_.N * 4));
+    if (wide_) {
+        if (!d_wtv_) FHE_HIP_CHECK(hipMalloc(&d_wtv_, 2 * (size_t)p_.N * 8));
+    } else if (!d_tv_) {
+        FHE_HIP_CHECK(hipMalloc(&d_tv_, 2 * (size_t)p_.N * 4));
+    }
     // BootstrapFuncCore (:596-608): m[j * 2N/ctmod] = (Q / fmod) f((b - j) mod ctmod)
-    std::vector<uint32_t> tv(ctmod);
+    std::vector<uint64_t> tv(ctmod);
     const uint64_t scale = p_.Q / fmod;
     for (uint32_t x = 0; x < ctmod; ++x) {
         if (f[x] > fmod) throw std::invalid_argument("BootstrapFunc: f(x) exceeds fmod");
-        tv[x] = (uint32_t)(scale * f[x]);
+        tv[x] = scale * f[x];  // <= Q
     }
-    // stream-ordered: the copy runs after every earlier launch on s that reads d_tv_
-    FHE_HIP_CHECK(hipMemcpyAsync(d_tv_, tv.data(), ctmod * 4, hipMemcpyHostToDevice, s));
+    // stream-ordered: the copy runs after every earlier launch on s that reads the table
+    if (wide_) {
+        FHE_HIP_CHECK(hipMemcpyAsync(d_wtv_, tv.data(), ctmod * 8, hipMemcpyHostToDevice, s));
+    } else {
+        std::vector<uint32_t> tv32(tv.begin(), tv.end());
+        FHE_HIP_CHECK(hipMemcpyAsync(d_tv_, tv32.data(), ctmod * 4, hipMemcpyHostToDevice, s));
+    }
     GateArgs g{};
     g.count = (uint32_t)count;
     g.n = p_.n;
@@ -97,13 +106,14 @@ void Engine::bootstrap_func_device(size_t count, const uint64_t* a, const uint64
     g.ctmod = ctmod;
     g.factor = 2 * p_.N / ctmod;
     g.tv = d_tv_;
+    g.tv64 = d_wtv_;
     g.b_const = 0;  // ctExt = (acc0, acc1[0]) (:624-626)
     g.msb_out = 1;
     g.gbits = p_.gBits;
     GateInputs in{{a, nullptr, nullptr, nullptr}, {b, nullptr, nullptr, nullptr}, 1, 0, 0};
     prep_device(g, in, 0, s);
     rotate_device(g, s);
-    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, fmod, a_out, b_out, s));
+    keyswitch_ext(count, fmod, a_out, b_out, s);
 }
 
 // EvalFunc (:241-337)

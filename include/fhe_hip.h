@@ -83,9 +83,15 @@ void* fhe_hip_ntt_plan_stream(fhe_hip_ntt_plan* plan);
 typedef struct fhe_hip_ctx fhe_hip_ctx;
 
 typedef struct {
-    uint32_t paramset, method, n, N, q, qKS, baseKS, digitsKS, baseG, digitsG, numAutoKeys, keyDist;
-    uint64_t Q, psi, bsk_words, ksk_rows;
+    uint32_t paramset, method, n, N, q, baseKS, digitsKS, baseG, digitsG, numAutoKeys, keyDist, reserved;
+    uint64_t Q, psi, qKS, bsk_words, ksk_rows;
 } fhe_hip_params;
+/* The large-precision family GenerateBinFHEContext(set, arbFunc, logQ, N, GINX, false)
+ * (binfhecontext.cpp:55-104: Q = LastPrime(54, 2N), N = 2048, qKS = 2^35, n = 1305 (TOY: 32),
+ * baseG 2^14 / 2^18 / 2^27 by logQ) is addressed by the paramset code
+ *   FHE_HIP_LARGE | set << 16 | arbFunc << 15 | log2(N) << 8 (0: minimum N) | logQ
+ * in every entry point that takes a paramset. */
+#define FHE_HIP_LARGE (1 << 30)
 
 /* parameters of a set (host only; GenerateBinFHEContext, binfhecontext.cpp:107-179) */
 int fhe_hip_params_get(int paramset, int method, fhe_hip_params* out);

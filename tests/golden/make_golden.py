@@ -194,6 +194,70 @@ def make_fb(names=("std128", "lmkcdey")):
         print(name, "fb ok", sorted(k for k in out if k.endswith("_a")))
 
 
+# the large-precision family GenerateBinFHEContext(set, arbFunc, logQ, N, GINX) (binfhecontext.cpp:55-104):
+# name -> (set, arbFunc, logQ); covers every baseG regime (2^27 / 2^18 / 2^14 at N = 2048) and
+# logQ = 11 (27-bit Q, N = 1024, baseG = 2^5); one STD128 (n = 1305) case
+LARGE_SETS = {"toy12arb": (0, True, 12), "toy17": (0, False, 17), "toy29": (0, False, 29), "toy11": (0, False, 11),
+              "std29": (3, False, 29)}
+
+
+def large_inputs(name):
+    """keys (seeded host keygen) and the inputs of each large-family fixture: gate bits (mod q),
+    and values mod 2^logQ with plaintext modulus P = 2^logQ / (q / (2 beta)) around P/2"""
+    from fhe_amd import binfhe as bf
+    st, arb, logQ = LARGE_SETS[name]
+    ps = bf.large_paramset(st, arb, logQ)
+    key_seed = 0xB1600000 + logQ + (st << 8) + (int(arb) << 7)
+    keys = bf.keygen(ps, GINX, key_seed)
+    P = bf.params(ps, GINX)
+    cnt = 2 if st == 3 else 4
+    rng = np.random.default_rng(key_seed)
+    bits1, bits2 = rng.integers(0, 2, cnt), rng.integers(0, 2, cnt)
+    g1 = bf.encrypt(ps, GINX, keys.sk, bits1, key_seed + 1)
+    g2 = bf.encrypt(ps, GINX, keys.sk, bits2, key_seed + 2)
+    mod = 1 << logQ
+    PL = mod // (P.q // 256) if mod > P.q else P.q // 256
+    xs = np.array([PL // 2 - 1, PL // 2, 3, PL - 3, PL // 4, 0][:cnt + (2 if st != 3 else 0)])
+    la, lb = bf.encrypt(ps, GINX, keys.sk, xs, key_seed + 3, PL, mod)
+    return ps, key_seed, keys, P, bits1, bits2, g1, g2, mod, PL, xs, la, lb
+
+
+def make_large(names=tuple(LARGE_SETS)):
+    for name in names:
+        ps, key_seed, keys, P, bits1, bits2, (a1, b1), (a2, b2), mod, PL, xs, la, lb = large_inputs(name)
+        ref = Ref(ps, GINX)
+        assert (ref.n, ref.N, ref.q, ref.Q, ref.qKS, ref.baseG) == (P.n, P.N, P.q, P.Q, P.qKS, P.baseG)
+        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        out = {"paramset": ps, "key_seed": np.uint64(key_seed), "bits1": bits1, "bits2": bits2, "xs": xs,
+               "mod": np.uint64(mod), "PL": np.uint64(PL),
+               "in_sha": np.array(sha(a1) + sha(b1) + sha(a2) + sha(b2) + sha(la) + sha(lb))}
+        if name != "std29":
+            out["keys_sha"] = np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB))
+        for gname, g in (("AND", 1), ("XOR", 4)):
+            ao, bo = ref.eval_gate(g, a1, b1, a2, b2)
+            out[f"{gname}_a"], out[f"{gname}_b"] = ao, bo
+            ea, eb = ref.eval_gate(g, a1, b1, a2, b2, extended=True)
+            out[f"{gname}_ext_a"], out[f"{gname}_ext_b"] = ea, eb
+        if mod > P.q:
+            ao, bo = ref.eval_floor(la, lb, mod, 0)
+            out["floor_a"], out["floor_b"] = ao, bo
+            ao, bo = ref.eval_sign(la, lb, mod, False)
+            out["sign_a"], out["sign_b"] = ao, bo
+            if name != "std29":
+                ao, bo = ref.eval_decomp(la, lb, mod)
+                out["decomp_a"], out["decomp_b"] = ao, bo
+        if P.q <= P.N:   # arbitrary-function LUT (eval-function.cpp): x^3 mod p on inputs mod q
+            p = P.q // 256
+            lut = np.array([(P.q // p) * (((i * p) // P.q) ** 3 % p) for i in range(P.q)], np.uint64)
+            ms = np.arange(p)
+            fa, fb = __import__("fhe_amd.binfhe", fromlist=["x"]).encrypt(ps, GINX, keys.sk, ms, key_seed + 4, p)
+            ao, bo = ref.eval_func(fa, fb, P.q, lut)
+            out["func_in_sha"] = np.array(sha(fa) + sha(fb))
+            out["func_ms"], out["func_a"], out["func_b"] = ms, ao, bo
+        np.savez_compressed(os.path.join(HERE, f"large_{name}.npz"), **out)
+        print(name, "large ok", sorted(k for k in out if k.endswith("_a")))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("ntt", "all"):
@@ -204,5 +268,7 @@ if __name__ == "__main__":
         make_multi(sys.argv[2:] or ("std128", "lmkcdey"))
     if what == "fb":   # one parameter set per process (see tests/test_fb.py)
         make_fb(sys.argv[2:] or ("std128",))
+    if what == "large":
+        make_large(sys.argv[2:] or tuple(LARGE_SETS))
     sys.stdout.flush()
     os._exit(0)   # skip interpreter teardown: two OpenMP runtimes (reference + fhe_amd) in one process

@@ -1,0 +1,149 @@
+"""The large-precision parameter family GenerateBinFHEContext(set, arbFunc, logQ, N, GINX)
+(binfhecontext.cpp:55-104): 54-bit Q, N = 2048, qKS = 2^35 (27-bit Q, N = 1024 at logQ = 11).
+fhe_amd (bootstrap_wide.hip) vs golden vectors the reference produced on the same seeded keys
+and inputs (tests/golden/make_golden.py large)."""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TOY = ["toy12arb", "toy17", "toy29", "toy11"]
+TRUTH = {"AND": lambda a, b: a & b, "XOR": lambda a, b: a ^ b}
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.uint64).tobytes()).hexdigest()
+
+
+_cache = {}
+
+
+def fixture(name):
+    if name not in _cache:
+        sys.path.insert(0, GOLD)
+        from make_golden import large_inputs
+        g = np.load(os.path.join(GOLD, f"large_{name}.npz"))
+        _cache[name] = (g, large_inputs(name))
+    return _cache[name]
+
+
+# ----------------------------------------------------------------- CPU ----
+def test_large_params_match_reference_table():
+    """derived constants of the family (binfhecontext.cpp:55-104) for every logQ regime"""
+    from fhe_amd import binfhe as bf
+    for logQ, bg, dG, N, Qbits in ((11, 1 << 5, 6, 1024, 27), (12, 1 << 27, 2, 2048, 54), (17, 1 << 18, 3, 2048, 54),
+                                   (26, 1 << 14, 4, 2048, 54), (29, 1 << 14, 4, 2048, 54)):
+        for st, n in ((bf.TOY, 32), (bf.STD128, 1305)):
+            for arb in (False, True):
+                P = bf.params(bf.large_paramset(st, arb, logQ), bf.GINX)
+                assert (P.n, P.N, P.q, P.qKS, P.baseKS, P.digitsKS, P.baseG, P.digitsG) == \
+                    (n, N, N if arb else 2 * N, 1 << 35, 32, 7, bg, dG)
+                assert P.Q.bit_length() == Qbits and P.Q % (2 * N) == 1
+    with pytest.raises(Exception):
+        bf.params(bf.large_paramset(bf.TOY, False, 30), bf.GINX)
+    with pytest.raises(Exception):
+        bf.params(bf.large_paramset(bf.TOY, False, 17), bf.LMKCDEY)
+
+
+@pytest.mark.parametrize("name", TOY)
+def test_large_keys_and_inputs_deterministic(name):
+    g, (ps, seed, keys, P, b1, b2, (a1, bb1), (a2, bb2), mod, PL, xs, la, lb) = fixture(name)
+    assert sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB) == str(g["keys_sha"])
+    assert sha(a1) + sha(bb1) + sha(a2) + sha(bb2) + sha(la) + sha(lb) == str(g["in_sha"])
+
+
+@pytest.mark.parametrize("name", TOY)
+def test_large_reference_outputs_decrypt(name):
+    """the reference, on our keys, computes what the operations promise (our keys are valid)"""
+    from fhe_amd import binfhe as bf
+    g, (ps, seed, keys, P, b1, b2, _, _, mod, PL, xs, la, lb) = fixture(name)
+    for gname, f in TRUTH.items():
+        dec = bf.decrypt(ps, bf.GINX, keys.sk, g[f"{gname}_a"], g[f"{gname}_b"])
+        assert np.array_equal(dec, f(b1, b2)), gname
+    if "sign_a" in g:
+        # EvalSign is the MSB of x rounded to the bootstrapping precision: PL/2 - 1 reads 1 and
+        # PL - 3 wraps to 0 there, so only the values away from the rounding edges are checked
+        dec = bf.decrypt(ps, bf.GINX, keys.sk, g["sign_a"], g["sign_b"], mod=P.q, p=2)
+        assert list(dec[[1, 2, 4, 5]]) == [1, 0, 0, 0]
+
+
+# ----------------------------------------------------------------- GPU ----
+_engines = {}
+
+
+def engine(name):
+    from fhe_amd import binfhe as bf
+    if name not in _engines:
+        g, (ps, seed, keys, *_) = fixture(name)
+        e = bf.GateEngine(ps, bf.GINX)
+        e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        _engines[name] = e
+    return _engines[name]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", TOY)
+def test_gpu_large_gates_bit_exact(name):
+    g, (ps, seed, keys, P, b1, b2, (a1, bb1), (a2, bb2), *_) = fixture(name)
+    e = engine(name)
+    for gname, gate in (("AND", 1), ("XOR", 4)):
+        ea, eb = e.eval_gate_extended(gate, a1, bb1, a2, bb2)
+        assert np.array_equal(ea, g[f"{gname}_ext_a"]) and np.array_equal(eb, g[f"{gname}_ext_b"]), gname
+        ao, bo = e.eval_gate(gate, a1, bb1, a2, bb2)
+        assert np.array_equal(ao, g[f"{gname}_a"]) and np.array_equal(bo, g[f"{gname}_b"]), gname
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in TOY if n != "toy11"])
+def test_gpu_large_functional_bit_exact(name):
+    """EvalFloor / EvalSign / EvalDecomp on ciphertexts mod 2^logQ, EvalFunc (arbitrary LUT)"""
+    g, (ps, seed, keys, P, b1, b2, _, _, mod, PL, xs, la, lb) = fixture(name)
+    e = engine(name)
+    ao, bo = e.eval_floor(la, lb, mod)
+    assert np.array_equal(ao, g["floor_a"]) and np.array_equal(bo, g["floor_b"])
+    ao, bo = e.eval_sign(la, lb, mod)
+    assert np.array_equal(ao, g["sign_a"]) and np.array_equal(bo, g["sign_b"])
+    ao, bo = e.eval_decomp(la, lb, mod)
+    assert np.array_equal(ao, g["decomp_a"]) and np.array_equal(bo, g["decomp_b"])
+    if "func_a" in g:
+        from fhe_amd import binfhe as bf
+        p = P.q // 256
+        lut = np.array([(P.q // p) * (((i * p) // P.q) ** 3 % p) for i in range(P.q)], np.uint64)
+        fa, fb = bf.encrypt(ps, bf.GINX, keys.sk, g["func_ms"], seed + 4, p)
+        ao, bo = e.eval_func(fa, fb, P.q, lut)
+        assert np.array_equal(ao, g["func_a"]) and np.array_equal(bo, g["func_b"])
+
+
+@pytest.mark.gpu
+def test_gpu_large_std128_bit_exact():
+    """STD128 large-precision set (n = 1305, 4.8 GB key-switching key): gates and EvalSign"""
+    if not os.path.exists(os.path.join(GOLD, "large_std29.npz")):
+        pytest.skip("large_std29 fixture not generated")
+    name = "std29"
+    g, (ps, seed, keys, P, b1, b2, (a1, bb1), (a2, bb2), mod, PL, xs, la, lb) = fixture(name)
+    e = engine(name)
+    for gname, gate in (("AND", 1), ("XOR", 4)):
+        ao, bo = e.eval_gate(gate, a1, bb1, a2, bb2)
+        assert np.array_equal(ao, g[f"{gname}_a"]) and np.array_equal(bo, g[f"{gname}_b"]), gname
+    ao, bo = e.eval_sign(la, lb, mod)
+    assert np.array_equal(ao, g["sign_a"]) and np.array_equal(bo, g["sign_b"])
+    _engines.pop(name)
+    _cache.pop(name)
+
+
+@pytest.mark.gpu
+def test_gpu_large_context_api():
+    """BinFHEContext large-precision overload (eval-sign.cpp flow): EvalSign of values mod 2^29"""
+    from fhe_amd import binfhe as bf
+    cc = bf.BinFHEContext()
+    cc.GenerateBinFHEContext(bf.TOY, False, 29, 0, bf.GINX, False)
+    sk = cc.KeyGen()
+    cc.BTKeyGen(sk)
+    Q = 1 << 29
+    P = Q // (cc.params.q // 256)
+    for x in (0, 5, P // 4, P // 2, 3 * P // 4):
+        ct = cc.Encrypt(sk, x, p=P, mod=Q)
+        assert cc.Decrypt(sk, cc.EvalSign(ct), p=2) == int(x >= P // 2), x
