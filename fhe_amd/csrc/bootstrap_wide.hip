@@ -16,6 +16,11 @@
 // Keys are read straight from HBM, coalesced (consecutive threads, consecutive slots).
 #include "boot_wide.h"
 
+// waves per SIMD the blind-rotation kernel is compiled for (VGPR budget 512 / waves)
+#ifndef FHE_WIDE_WAVES
+#define FHE_WIDE_WAVES 4
+#endif
+
 namespace fhe_amd {
 
 namespace {
@@ -106,10 +111,117 @@ WD void ntt_inv(uint64_t* buf, const WideTables& tb) {
         __syncthreads();
     }
 }
+
+// Radix-4 passes of the same transforms: each thread takes whole 4-element units through two
+// stages between barriers (LOGN / 2 barriers instead of LOGN), an odd last stage radix-2.
+template <int LOGN, int NB>
+WD void ntt_fwd4(uint64_t* buf, const WideTables& tb) {
+    constexpr int N = 1 << LOGN, T = N / 4;
+    const uint64_t Q = tb.Q;
+    const int u = (int)threadIdx.x;  // one unit per thread per polynomial
+#pragma unroll 1
+    for (int s = 0; s + 1 < LOGN; s += 2) {
+        const int logt = LOGN - 1 - s, t = 1 << logt, th = t >> 1, m = 1 << s;
+        const int i = u >> (logt - 1), k = u & (th - 1);
+        const int j0 = (i << (logt + 1)) + k;
+        const uint64_t w = tb.tab[m + i], ws = tb.tabS[m + i];
+        const uint64_t w1 = tb.tab[2 * m + 2 * i], w1s = tb.tabS[2 * m + 2 * i];
+        const uint64_t w2 = tb.tab[2 * m + 2 * i + 1], w2s = tb.tabS[2 * m + 2 * i + 1];
+#pragma unroll
+        for (int p = 0; p < NB; ++p) {
+            uint64_t* b = buf + p * N + j0;
+            uint64_t x0 = b[0], x1 = b[th], x2 = b[t], x3 = b[t + th];
+            uint64_t V = mul_shoup(x2, w, ws, Q);
+            x2 = sub_q(x0, V, Q);
+            x0 = add_q(x0, V, Q);
+            V = mul_shoup(x3, w, ws, Q);
+            x3 = sub_q(x1, V, Q);
+            x1 = add_q(x1, V, Q);
+            V = mul_shoup(x1, w1, w1s, Q);
+            b[0] = add_q(x0, V, Q);
+            b[th] = sub_q(x0, V, Q);
+            V = mul_shoup(x3, w2, w2s, Q);
+            b[t] = add_q(x2, V, Q);
+            b[t + th] = sub_q(x2, V, Q);
+        }
+        __syncthreads();
+    }
+    if (LOGN & 1) {  // last stage: t = 1, m = N / 2
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int bf = u + T * k;
+            const uint64_t w = tb.tab[N / 2 + bf], ws = tb.tabS[N / 2 + bf];
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                uint64_t* b = buf + p * N + 2 * bf;
+                const uint64_t U = b[0], V = mul_shoup(b[1], w, ws, Q);
+                b[0] = add_q(U, V, Q);
+                b[1] = sub_q(U, V, Q);
+            }
+        }
+        __syncthreads();
+    }
+}
+template <int LOGN, int NB>
+WD void ntt_inv4(uint64_t* buf, const WideTables& tb) {
+    constexpr int N = 1 << LOGN, T = N / 4;
+    const uint64_t Q = tb.Q;
+    const int u = (int)threadIdx.x;
+#pragma unroll 1
+    for (int s = 0; s + 1 < LOGN; s += 2) {
+        const int t = 1 << s, m = N >> (s + 1);
+        const int i = u >> s, k = u & (t - 1);
+        const int e0 = (i << (s + 2)) + k;
+        const uint64_t wa = tb.tabI[m + 2 * i], was = tb.tabIS[m + 2 * i];
+        const uint64_t wb = tb.tabI[m + 2 * i + 1], wbs = tb.tabIS[m + 2 * i + 1];
+        const uint64_t w2 = tb.tabI[(m >> 1) + i], w2s = tb.tabIS[(m >> 1) + i];
+#pragma unroll
+        for (int p = 0; p < NB; ++p) {
+            uint64_t* b = buf + p * N + e0;
+            const uint64_t x0 = b[0], x1 = b[t], x2 = b[2 * t], x3 = b[3 * t];
+            const uint64_t y0 = add_q(x0, x1, Q), y1 = mul_shoup(sub_q(x0, x1, Q), wa, was, Q);
+            const uint64_t y2 = add_q(x2, x3, Q), y3 = mul_shoup(sub_q(x2, x3, Q), wb, wbs, Q);
+            b[0] = add_q(y0, y2, Q);
+            b[2 * t] = mul_shoup(sub_q(y0, y2, Q), w2, w2s, Q);
+            b[t] = add_q(y1, y3, Q);
+            b[3 * t] = mul_shoup(sub_q(y1, y3, Q), w2, w2s, Q);
+        }
+        __syncthreads();
+    }
+    if (LOGN & 1) {  // last stage: t = N / 2, m = 1
+        const uint64_t w = tb.tabI[1], ws = tb.tabIS[1];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int j = u + T * k;
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                uint64_t* b = buf + p * N + j;
+                const uint64_t U = b[0], V = b[N / 2];
+                b[0] = add_q(U, V, Q);
+                b[N / 2] = mul_shoup(sub_q(U, V, Q), w, ws, Q);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+#ifndef FHE_WIDE_R4
+#define FHE_WIDE_R4 1
+#endif
+template <int LOGN, int NB>
+WD void fwd(uint64_t* buf, const WideTables& tb) {
+    if (FHE_WIDE_R4) ntt_fwd4<LOGN, NB>(buf, tb);
+    else ntt_fwd<LOGN, NB>(buf, tb);
+}
+template <int LOGN, int NB>
+WD void inv(uint64_t* buf, const WideTables& tb) {
+    if (FHE_WIDE_R4) ntt_inv4<LOGN, NB>(buf, tb);
+    else ntt_inv<LOGN, NB>(buf, tb);
+}
 }  // namespace
 
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 4)
+__global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
     k_blind_rotate_wide(WideArgs g, WideTables tb, const uint64_t* __restrict__ bsk, const uint16_t* __restrict__ idx,
                         const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b) {
     constexpr int N = 1 << LOGN, T = N / 4, S = 4;
@@ -134,7 +246,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4)
             buf[x] = v;
         }
         __syncthreads();
-        ntt_fwd<LOGN, 1>(buf, tb);
+        fwd<LOGN, 1>(buf, tb);
 #pragma unroll
         for (int r = 0; r < S; ++r) {
             acc0[r] = 0;
@@ -155,7 +267,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4)
             buf[N + t + T * r] = acc1[r];
         }
         __syncthreads();
-        ntt_inv<LOGN, 2>(buf, tb);
+        inv<LOGN, 2>(buf, tb);
         // SignedDigitDecompose state: centred value, lowest digit dropped
         int64_t d[2][S];
 #pragma unroll
@@ -189,7 +301,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4)
                     buf[p * N + t + T * r] = (uint64_t)r0;
                 }
             __syncthreads();
-            ntt_fwd<LOGN, 2>(buf, tb);
+            fwd<LOGN, 2>(buf, tb);
 #pragma unroll
             for (int r = 0; r < S; ++r) {
                 const uint32_t j = t + T * r;
@@ -233,7 +345,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4)
         buf[N + t + T * r] = acc1[r];
     }
     __syncthreads();
-    ntt_inv<LOGN, 2>(buf, tb);
+    inv<LOGN, 2>(buf, tb);
     uint64_t* oa = ext_a + (size_t)gate * N;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
