@@ -1,26 +1,35 @@
 #!/usr/bin/env python3
 """bench.py -- TFHE gate bootstraps/sec (STD128) on MI355X, driver contract.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--method ginx|lmkcdey]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--total T | --batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A step = one EvalBinGate(AND) pass over a batch of B independent gate pairs per
-GPU (default B = 8192 = BASELINE.json config 4's per-GPU shard of 65536), inputs
-resident in HBM: blind rotation (k_blind_rotate_*) then key switch
-(k_keyswitch).  Ranks shard gates with no data-path collective ("weak"
-scaling: B per GPU fixed).  Rank 0 prints one JSON line.
+A step = one EvalBinGate(AND) pass over BASELINE config 4's global batch of T = 65,536
+independent STD128 GINX gate pairs, sharded contiguously over the N ranks (strong
+scaling: T / N gates per GPU, no data-path collective), inputs resident in HBM:
+gate prep + blind rotation (k_blind_rotate_ginx), then key switch + ModSwitch
+(k_keyswitch_tiled).  Rank 0 prints ONE JSON line.  In the same line:
 
-Also measured in the same run and reported beside `value`:
-  * roofline     -- dominant kernel of the step (blind rotation): algorithmic
-                    bytes / launch time (HIP events on the launch stream) vs HBM
-                    peak (tiny by construction: the BSK is reused by every gate);
-  * valu_roofline -- the same kernel against the bound that binds: modular
-                    multiplies per second vs the 32-bit integer multiply issue peak;
-  * ntt_roofline -- BASELINE config 2: batched N=1024 NTT x 4096, GB/s vs HBM peak;
-  * cpu_baseline -- the reference's own CPU path (oracle/_ref/libfhe_ref.so,
-                    built from /root/reference) on the host cores, rank 0, N=1.
+  * roofline       -- the dominant kernel (blind rotation): algorithmic bytes / launch
+                      time (HIP events on the launch stream) vs HBM peak; tiny by
+                      construction (the BSK is reused by every gate of the batch);
+  * valu_roofline  -- the same kernel against the bound that binds: modular multiplies/s
+                      vs the half-rate 32-bit integer multiply issue peak;
+  * lmkcdey        -- BASELINE config 5: the same step on STD128_LMKCDEY (T gates,
+                      same sharding), with its own roofline / valu_roofline / cpu_baseline;
+  * config3        -- BASELINE config 3: B = 1024 GINX gates on one GPU (N = 1 only);
+  * ntt_roofline   -- BASELINE config 2: 4096-polynomial N = 1024 NTT and iNTT passes,
+                      27-bit STD128 modulus (k_ntt1024w) and 60-bit poly-benchmark prime
+                      (k_ntt1024<u64>), GB/s vs HBM peak;
+  * cpu_baseline   -- the reference's own CPU path (oracle/_ref/libfhe_ref.so, built
+                      from /root/reference) on this host, rank 0, N = 1 only: all cores
+                      available to the job and 1 core, host model recorded; config-1
+                      single-NTT time.
+  * bit_exact_vs_reference -- the whole step's outputs hashed against the reference's
+                      outputs for the same 65,536 gates (tests/golden/full_*.npz).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -34,12 +43,17 @@ sys.path.insert(0, ROOT)
 METRIC = "TFHE gate bootstraps/sec (STD128) at 1/2/4/8 MI355X; NTT GB/s vs HBM peak"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_MODMUL_PEAK_T = 256 * 4 * 16 * 2.4e9 / 3 / 1e12  # 13.1 T modmul/s (half-rate 32-bit multiplies)
-KEY_SEED = 0xBE4C0001
 # algorithmic bytes (reference u64 accounting)
 BSK_BYTES = {"ginx": 65_929_216, "lmkcdey": 29_655_040}
+KSK_BYTES = {"ginx": 396_361_728, "lmkcdey": 352_321_536}
 IN_BYTES_PER_GATE = {"ginx": 2 * 504 * 8, "lmkcdey": 2 * 448 * 8}  # two LWE inputs (n+1 u64)
+OUT_BYTES_PER_GATE = {"ginx": 504 * 8, "lmkcdey": 448 * 8}
 EXT_BYTES_PER_GATE = 1025 * 8                                       # ctExt (N+1 u64)
 NTT_BYTES_PER_POLY = 2 * 1024 * 8                                   # read + write u64
+MODMUL_PER_GATE = {"ginx": 25.8e6, "lmkcdey": 24.7e6}              # SURVEY.md 8(a) cost table
+K1_NAME = {"ginx": "k_blind_rotate_ginx", "lmkcdey": "k_blind_rotate_lmk"}
+PREP_NAME = {"ginx": "k_prep_ginx", "lmkcdey": "k_prep_lmk_w"}
+FULL_SHARD = 8192
 
 
 def log(*a):
@@ -51,13 +65,136 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8192, help="gates per GPU per step")
-    ap.add_argument("--method", default="ginx", choices=["ginx", "lmkcdey"])
+    ap.add_argument("--total", type=int, default=65536, help="global gates per step (strong scaling)")
+    ap.add_argument("--batch", type=int, default=0, help="gates per GPU per step (weak scaling; overrides --total)")
+    ap.add_argument("--method", default="ginx", choices=["ginx", "lmkcdey"], help="method of the main line")
+    ap.add_argument("--no-lmkcdey", action="store_true", help="skip the config-5 sub-object")
+    ap.add_argument("--no-config3", action="store_true")
     ap.add_argument("--ntt-count", type=int, default=4096)
-    ap.add_argument("--cpu-sample", type=int, default=3072, help="gates in the CPU-baseline sample (~12 s of host work)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=2048, help="gates in the all-cores CPU sample")
+    ap.add_argument("--cpu-sample-1core", type=int, default=24, help="gates in the 1-core CPU sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core available to this job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------
+# inputs: the seeded batch of tests/golden/make_golden.py full_inputs(), so the outputs can be
+# checked against the reference's hashes for the same 65,536 gates
+# ---------------------------------------------------------------------------------------------
+def make_inputs(bf, ps, method, total):
+    key_seed = 0xB0070000 + ps
+    keys = bf.keygen(ps, method, key_seed)
+    rng = np.random.default_rng(0xF011 + ps)
+    x1, x2 = rng.integers(0, 2, total), rng.integers(0, 2, total)
+    a1, b1 = bf.encrypt(ps, method, keys.sk, x1, 0xF0110000 + ps)
+    a2, b2 = bf.encrypt(ps, method, keys.sk, x2, 0xF0120000 + ps)
+    return keys, x1, x2, a1, b1, a2, b2
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.uint64).tobytes()).hexdigest()
+
+
+def golden_check(name, lo, hi, total, ao, bo):
+    """True/False when [lo, hi) of the 65,536-gate batch is covered by the reference hashes of
+    tests/golden/full_<name>.npz (whole batch or whole 8192-gate shards), else None."""
+    f = os.path.join(ROOT, "tests", "golden", f"full_{name}.npz")
+    if not os.path.exists(f):
+        return None
+    g = np.load(f)
+    if total != int(g["count"]):
+        return None
+    if lo == 0 and hi == total:
+        return _sha(ao) + _sha(bo) == str(g["out_sha"])
+    S = int(g["shard"])
+    if lo % S or (hi - lo) % S:
+        return None
+    shards = [str(s) for s in g["shard_sha"]]
+    return all(_sha(ao[s - lo:s - lo + S]) + _sha(bo[s - lo:s - lo + S]) == shards[s // S] for s in range(lo, hi, S))
+
+
+def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=True):
+    """Times K steps of EvalBinGate(AND) over gates [lo, hi) of a `total`-gate batch on this
+    rank; returns the per-rank measurements (elapsed is max-reduced by the caller)."""
+    from fhe_amd.dist import barrier
+    dev, stream, sp = ctx["dev"], ctx["stream"], ctx["stream"].cuda_stream
+    ps, method = (bf.STD128, bf.GINX) if method_name == "ginx" else (bf.STD128_LMKCDEY, bf.LMKCDEY)
+    P = bf.params(ps, method)
+    B = hi - lo
+    t0 = time.time()
+    keys, x1, x2, a1, b1, a2, b2 = make_inputs(bf, ps, method, total)
+    eng = bf.GateEngine(ps, method, device=dev.index)
+    eng.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    to_dev = lambda x: torch.from_numpy(np.ascontiguousarray(x[lo:hi]).view(np.int64)).to(dev)  # noqa: E731
+    d_in = [to_dev(x) for x in (a1, b1, a2, b2)]
+    d_ao = torch.empty((B, P.n), dtype=torch.int64, device=dev)
+    d_bo = torch.empty((B,), dtype=torch.int64, device=dev)
+    ptrs = [t.data_ptr() for t in d_in]
+    log(f"[{method_name}] setup {time.time() - t0:.1f}s (keygen + upload), gates [{lo}, {hi}) of {total}")
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        eng.blind_rotate_device(bf.AND, B, *ptrs, stream=sp)
+        if ev:
+            ev[1].record(stream)
+        eng.keyswitch_workspace_device(B, d_ao.data_ptr(), d_bo.data_ptr(), stream=sp)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    br_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    ks_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ao = d_ao.cpu().numpy().view(np.uint64)
+    bo = d_bo.cpu().numpy().view(np.uint64)
+    dec = bf.decrypt(ps, method, keys.sk, ao, bo)
+    verified = bool(np.array_equal(dec, (x1[lo:hi] & x2[lo:hi]).astype(np.int64)))
+    exact = golden_check("std128" if method_name == "ginx" else "lmkcdey", lo, hi, total, ao, bo) if golden else None
+    eng.close()
+    return {"elapsed": elapsed, "br_ms": br_ms, "ks_ms": ks_ms, "verified": verified, "exact": exact, "B": B,
+            "keys": keys, "inputs": (a1[lo:hi], b1[lo:hi], a2[lo:hi], b2[lo:hi]), "out": (ao, bo), "ps": ps,
+            "method": method}
+
+
+def rooflines(method_name, B, br_ms, ks_ms):
+    """roofline (HBM) and valu_roofline of the blind-rotation kernel at B gates per launch."""
+    alg_bytes = BSK_BYTES[method_name] + B * (IN_BYTES_PER_GATE[method_name] + EXT_BYTES_PER_GATE)
+    achieved = alg_bytes / (br_ms * 1e-3) / 1e9
+    mm_rate = MODMUL_PER_GATE[method_name] * B / (br_ms * 1e-3) / 1e12
+    k1 = K1_NAME[method_name]
+    roofline = {
+        "kernel": k1, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(k1, B),
+        "launch_ms": round(br_ms, 4), "launch_note": f"HIP events around {PREP_NAME[method_name]} + {k1} "
+                                                     "(the prep kernel is <1% of it)",
+        "keyswitch_ms": round(ks_ms, 4),
+        "alg_bytes_per_launch": alg_bytes,
+        "alg_bytes_basis": "BSK (reference u64 accounting) + B x (two LWE inputs + ctExt), SURVEY 8(d)",
+        "traffic_note": "2*FETCH_SIZE+WRITE_SIZE per launch from the committed rocprofv3 PMC summary "
+                        "(profiles/*pmc_traffic.json, gfx950 FETCH correction), scaled to this batch; FETCH "
+                        "counts L2->fabric requests incl. Infinity-Cache hits",
+        "valu_note": "integer-VALU bound: see valu_roofline",
+    }
+    valu = {
+        "kernel": k1, "bound": "valu-int-mul", "achieved": round(mm_rate, 3),
+        "peak": round(VALU_MODMUL_PEAK_T, 4), "unit": "T modmul/s", "frac": round(mm_rate / VALU_MODMUL_PEAK_T, 4),
+        "basis": "SURVEY 8(a) modular multiplies per gate x gates / launch time; peak = 256 CUs x 4 SIMDs x "
+                 "16 lanes/clk (half-rate 32-bit multiplies) x 2.4 GHz / 3 multiplies per modmul; the measured "
+                 "multiply issue rate (profiles/r01_ubench_valu_rates.txt, 35.1 T lane-op/s) is 11.7 T modmul/s",
+    }
+    return roofline, valu
 
 
 def main():
@@ -65,8 +202,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from fhe_amd.dist import barrier, env, max_over_ranks
-    rank, world, local = env()
+    from fhe_amd.dist import max_over_ranks, shard
+    rank, world, local = env_rank()
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} differs from --gpus={args.gpus}; using WORLD_SIZE")
     # rehearsal knobs (not used by the driver): FHE_BENCH_DEVICE_MAP="0,0" puts ranks on
@@ -83,134 +220,105 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else None
+    stream = torch.cuda.Stream(dev)     # a real (non-null) stream: our kernels launch on it and
+    assert stream.cuda_stream, "need a non-default stream handle"   # the timing events are recorded on it
+    ctx = {"dev": dev, "stream": stream}
 
     from fhe_amd import binfhe as bf
     from fhe_amd import NttPlan
 
-    ps, method = (bf.STD128, bf.GINX) if args.method == "ginx" else (bf.STD128_LMKCDEY, bf.LMKCDEY)
-    P = bf.params(ps, method)
-    B = args.batch
+    if args.batch:
+        total, scaling = args.batch * world, "weak"
+    else:
+        total, scaling = args.total, "strong"
+    lo, hi = shard(total, rank, world)
 
-    # ---- setup (untimed): keys replicated on every GPU, inputs resident in HBM
-    t0 = time.time()
-    keys = bf.keygen(ps, method, KEY_SEED)
-    eng = bf.GateEngine(ps, method, device=local)
-    eng.load_keys(keys.bsk, keys.kskA, keys.kskB)
-    rng = np.random.default_rng(1000 + rank)
-    x1, x2 = rng.integers(0, 2, B), rng.integers(0, 2, B)
-    a1, b1 = bf.encrypt(ps, method, keys.sk, x1, 2000 + rank)
-    a2, b2 = bf.encrypt(ps, method, keys.sk, x2, 3000 + rank)
-    to_dev = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)  # noqa: E731
-    d_in = [to_dev(x) for x in (a1, b1, a2, b2)]
-    d_ao = torch.empty((B, P.n), dtype=torch.int64, device=dev)
-    d_bo = torch.empty((B,), dtype=torch.int64, device=dev)
-    ptrs = [t.data_ptr() for t in d_in]
-    stream = torch.cuda.Stream(dev)      # a real (non-null) stream: our kernels launch on it and
-    sp = stream.cuda_stream              # the timing events are recorded on it
-    assert sp, "need a non-default stream handle"
-    log(f"[rank {rank}] setup {time.time() - t0:.1f}s (keygen + upload), batch {B}")
+    def measure(method_name):
+        r = run_config(args, bf, torch, ctx, method_name, total, lo, hi)
+        el, bad, inexact, unknown = max_over_ranks(
+            [r["elapsed"], 0.0 if r["verified"] else 1.0, 1.0 if r["exact"] is False else 0.0,
+             1.0 if r["exact"] is None else 0.0], device=red_dev)
+        r["elapsed"] = el
+        r["verified"] = bad == 0.0
+        r["exact"] = None if unknown else inexact == 0.0
+        return r
 
-    def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        eng.blind_rotate_device(bf.AND, B, *ptrs, stream=sp)
-        if ev:
-            ev[1].record(stream)
-        eng.keyswitch_workspace_device(B, d_ao.data_ptr(), d_bo.data_ptr(), stream=sp)
-        if ev:
-            ev[2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    br_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    ks_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-
-    # correctness of the last step (host decrypt of the whole shard)
-    ao = d_ao.cpu().numpy().view(np.uint64)
-    bo = d_bo.cpu().numpy().view(np.uint64)
-    verified = bool(np.array_equal(bf.decrypt(ps, method, keys.sk, ao, bo), (x1 & x2).astype(np.int64)))
-
-    elapsed, bad = max_over_ranks([elapsed, 0.0 if verified else 1.0], device=red_dev)
-    verified = bad == 0.0
-
-    total_gates = B * world * args.steps
-    value = total_gates / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
+    main_r = measure(args.method)
+    lmk_r = measure("lmkcdey") if (args.method == "ginx" and not args.no_lmkcdey) else None
 
     result = None
     if rank == 0:
-        # ---- roofline of the dominant kernel (blind rotation), live HIP-event timing
-        alg_bytes = BSK_BYTES[args.method] + B * (IN_BYTES_PER_GATE[args.method] + EXT_BYTES_PER_GATE)
-        achieved = alg_bytes / (br_ms * 1e-3) / 1e9
-        # integer-VALU view: modular multiplies per gate (SURVEY.md 8(a) cost table)
-        mm_per_gate = 25.8e6 if args.method == "ginx" else 24.7e6
-        roofline = {
-            "kernel": f"k_blind_rotate_{args.method}",
-            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(f"k_blind_rotate_{args.method}", B),
-            "launch_ms": round(br_ms, 4), "keyswitch_ms": round(ks_ms, 4),
-            "alg_bytes_per_launch": alg_bytes,
-            "traffic_note": "2*FETCH_SIZE+WRITE_SIZE (profiles/*pmc_traffic.json); FETCH counts L2->fabric "
-                            "requests incl. Infinity-Cache hits: the BSK is streamed once per XCD per wave "
-                            "generation (8 XCDs x 4 generations at B=8192) from the 256 MiB cache",
-            "valu_note": "integer-VALU bound: see valu_roofline",
-            "modmul_per_s": round(mm_per_gate * B / (br_ms * 1e-3) / 1e12, 3), "modmul_unit": "T/s",
-        }
-        # the bound that binds: 32-bit integer multiply issue (each modular multiply is three
-        # half-rate multiplies: v_mad_i64_i32, v_mul_lo_u32, v_mad_i64_i32)
-        mm_rate = mm_per_gate * B / (br_ms * 1e-3) / 1e12
-        valu_roofline = {
-            "kernel": f"k_blind_rotate_{args.method}", "bound": "valu-int-mul", "achieved": round(mm_rate, 3),
-            "peak": VALU_MODMUL_PEAK_T, "unit": "T modmul/s", "frac": round(mm_rate / VALU_MODMUL_PEAK_T, 4),
-            "basis": "SURVEY 8(a) modular multiplies per gate x gates / launch time; peak = 256 CUs x 4 SIMDs x "
-                     "16 lanes/clk (half-rate 32-bit multiplies) x 2.4 GHz / 3 multiplies per modmul; the measured "
-                     "multiply issue rate (profiles/r01_ubench_valu_rates.txt, 35.1 T lane-op/s) is 11.7 T modmul/s",
-        }
-        ntt = ntt_roofline(NttPlan, torch, dev, stream, args.ntt_count) if world == 1 else None
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(ps, method, keys, a1, b1, a2, b2, ao, bo, args)
+        roofline, valu = rooflines(args.method, main_r["B"], main_r["br_ms"], main_r["ks_ms"])
+        value = total * args.steps / main_r["elapsed"]
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "bootstraps/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: seeded keys (fhe_amd keygen), random bit encryptions",
-            "config": {"workload": f"STD128{'' if args.method == 'ginx' else '_LMKCDEY'} "
-                                   f"{args.method.upper()} EvalBinGate(AND), {B} gates per GPU per step "
-                                   f"(BASELINE config {'4' if args.method == 'ginx' else '5'} shard)",
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(main_r["elapsed"] / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: seeded keys (fhe_amd keygen) and seeded random-bit encryptions, the batch of "
+                    "tests/golden/full_*.npz",
+            "config": {"workload": f"STD128{'' if args.method == 'ginx' else '_LMKCDEY'} {args.method.upper()} "
+                                   f"EvalBinGate(AND), {total} gates per step over {world} GPU(s) "
+                                   f"({hi - lo} per GPU; BASELINE config {'4' if args.method == 'ginx' else '5'})",
                        "paramset": "STD128" if args.method == "ginx" else "STD128_LMKCDEY",
-                       "method": args.method.upper(), "batch_per_gpu": B, "global_batch": B * world,
+                       "method": args.method.upper(), "global_batch": total, "batch_per_gpu": hi - lo,
                        "parallelism": f"shard{world}"},
-            "verified": verified,
+            "verified": main_r["verified"],
+            "bit_exact_vs_reference": main_r["exact"],
             "roofline": roofline,
-            "valu_roofline": valu_roofline,
-            "ntt_roofline": ntt,
-            "cpu_baseline": cpu,
+            "valu_roofline": valu,
         }
+        if lmk_r is not None:
+            lr, lv = rooflines("lmkcdey", lmk_r["B"], lmk_r["br_ms"], lmk_r["ks_ms"])
+            result["lmkcdey"] = {
+                "config": f"BASELINE config 5: STD128_LMKCDEY EvalBinGate(AND), {total} gates per step over "
+                          f"{world} GPU(s) ({hi - lo} per GPU)",
+                "value": round(total * args.steps / lmk_r["elapsed"], 1), "unit": "bootstraps/s",
+                "ms_per_step": round(lmk_r["elapsed"] / args.steps * 1e3, 3),
+                "verified": lmk_r["verified"], "bit_exact_vs_reference": lmk_r["exact"],
+                "roofline": lr, "valu_roofline": lv, "cpu_baseline": None,
+            }
+    if world == 1 and not args.no_config3 and args.method == "ginx":
+        c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden=False)
+        r3, v3 = rooflines("ginx", 1024, c3["br_ms"], c3["ks_ms"])
+        alg3 = BSK_BYTES["ginx"] + KSK_BYTES["ginx"] + 1024 * (IN_BYTES_PER_GATE["ginx"] + OUT_BYTES_PER_GATE["ginx"])
+        step_s = c3["elapsed"] / args.steps
+        result["config3"] = {
+            "config": "BASELINE config 3: STD128 GINX EvalBinGate(AND), 1024 gates, 1 GPU",
+            "value": round(1024 / step_s, 1), "unit": "bootstraps/s", "ms_per_step": round(step_s * 1e3, 3),
+            "verified": c3["verified"], "valu_roofline": v3, "blind_rotate_ms": r3["launch_ms"],
+            "keyswitch_ms": r3["keyswitch_ms"],
+            "hbm_frac_compulsory": round(alg3 / step_s / 1e9 / HBM_PEAK_GBS, 6),
+            "hbm_basis": "SURVEY 8(d) config 3: BSK + KSK + 1024 x I/O = 474,677,248 B per batch / step time",
+        }
+    if rank == 0 and world == 1:
+        result["ntt_roofline"] = ntt_rooflines(NttPlan, torch, dev, stream, args.ntt_count)
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(main_r, args)
+            if lmk_r is not None:
+                result["lmkcdey"]["cpu_baseline"] = cpu_baseline(lmk_r, args)
+        result["cpu_baseline"] = cpu
+    if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        from fhe_amd.dist import barrier
         barrier()
         dist.destroy_process_group()
     return result
 
 
+def env_rank():
+    from fhe_amd.dist import env
+    return env()
+
+
 def pmc_traffic(kernel, batch):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json,
-    written by tools/pmc_traffic.py), scaled to this batch; None if not measured."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc_traffic.json,
+    written by tools/pmc_traffic.py), scaled to this batch; None if not measured.  The newest
+    summary (by file name: r02 after r01) wins."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         try:
             d = json.load(open(f))
         except Exception:
@@ -221,53 +329,122 @@ def pmc_traffic(kernel, batch):
     return None if best is None else round(best)
 
 
-def ntt_roofline(NttPlan, torch, dev, stream, count, reps=20):
-    Q = 134215681
-    plan = NttPlan(Q, device=dev.index)
-    x = torch.randint(0, Q, (count, 1024), dtype=torch.int64, device=dev)
+def ntt_rooflines(NttPlan, torch, dev, stream, count, reps=20):
+    """BASELINE config 2: forward and inverse passes over `count` polynomials for the STD128 modulus
+    (27-bit, k_ntt1024w SignedA) and the poly-benchmark 60-bit prime (k_ntt1024<uint64_t>)."""
+    out = []
     sp = stream.cuda_stream
-    for _ in range(3):
-        plan.run_device(x.data_ptr(), x.data_ptr(), count, False, stream=sp)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(reps):
-        plan.run_device(x.data_ptr(), x.data_ptr(), count, False, stream=sp)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / reps
-    ach = count * NTT_BYTES_PER_POLY / (ms * 1e-3) / 1e9
-    plan.close()
-    return {"kernel": "k_ntt1024w<fwd, SignedA>", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_ntt1024w", count),
-            "launch_us": round(ms * 1e3, 3), "polys": count, "Q": Q}
+    for Q, kname in ((134215681, "k_ntt1024w<{}, SignedA>"), (1152921504606830593, "k_ntt1024<uint64_t, {}>")):
+        plan = NttPlan(Q, device=dev.index)
+        x = torch.randint(0, min(Q, 2**62), (count, 1024), dtype=torch.int64, device=dev)
+        y = torch.empty_like(x)
+        for inv in (False, True):
+            for _ in range(3):
+                plan.run_device(x.data_ptr(), y.data_ptr(), count, inv, stream=sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                plan.run_device(x.data_ptr(), y.data_ptr(), count, inv, stream=sp)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / reps
+            ach = count * NTT_BYTES_PER_POLY / (ms * 1e-3) / 1e9
+            name = kname.format("inv" if inv else "fwd")
+            out.append({"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": pmc_traffic(name, count), "launch_us": round(ms * 1e3, 3), "polys": count,
+                        "Q": Q, "alg_bytes_per_launch": count * NTT_BYTES_PER_POLY})
+        plan.close()
+    return out
 
 
-def cpu_baseline(ps, method, keys, a1, b1, a2, b2, ao, bo, args):
-    """The reference's CPU path timed on this host: EvalBinGateBatch semantics (OpenMP
-    parallel-for over BinFHEContext::EvalBinGate, batch.cpp:197-200) on a bounded sample."""
+def host_info():
+    """CPU facts of this host: the whole machine and what this job may use."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity"] = None
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except Exception:
+        pass
+    info["cgroup_cpus"] = quota
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    avail = info["affinity"] or info["nproc"] or 1
+    if quota:
+        avail = max(1, min(avail, int(quota)))
+    info["usable"] = avail
+    return info
+
+
+def cpu_baseline(r, args):
+    """The reference's CPU path on this host: EvalBinGateBatch semantics (OpenMP parallel-for over
+    BinFHEContext::EvalBinGate, batch.cpp:197-200) on bounded samples of the same batch, on every
+    core available to the job and on 1 core; plus the config-1 single-NTT time."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Ref, Restatement, ref_available, restatement_available
-    S = min(args.cpu_sample, len(b1))
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    sl = slice(0, S)
+    hi = host_info()
+    threads = args.cpu_threads or hi["usable"]
+    ps, method, keys = r["ps"], r["method"], r["keys"]
+    a1, b1, a2, b2 = r["inputs"]
+    ao, bo = r["out"]
+    label = "GINX" if method == 2 else "LMKCDEY"
+    S_all = min(args.cpu_sample if method == 2 else args.cpu_sample // 2, len(b1))
+    S_one = min(args.cpu_sample_1core if method == 2 else max(1, args.cpu_sample_1core * 2 // 3), len(b1))
     if ref_available():
         ref = Ref(ps, method)
         ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
-        t, ra, rb = ref.time_gates(1, a1[sl], b1[sl], a2[sl], b2[sl], nthreads=threads)
+        ref.time_gates(1, a1[:2], b1[:2], a2[:2], b2[:2], nthreads=min(2, threads))   # warm-up (tables)
+        t_all, ra, rb = ref.time_gates(1, a1[:S_all], b1[:S_all], a2[:S_all], b2[:S_all], nthreads=threads)
+        off = S_all
+        S_one = min(S_one, len(b1) - off) if len(b1) > off else S_one
+        sl1 = slice(off, off + S_one) if len(b1) > off else slice(0, S_one)
+        t_one, ra1, rb1 = ref.time_gates(1, a1[sl1], b1[sl1], a2[sl1], b2[sl1], nthreads=1)
         kind = "reference"
     elif restatement_available():
         O = Restatement(ps, method)
         t0 = time.perf_counter()
-        ra, rb = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, 1, a1[sl], b1[sl], a2[sl], b2[sl], nthreads=threads)
-        t = time.perf_counter() - t0
+        ra, rb = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, 1, a1[:S_all], b1[:S_all], a2[:S_all], b2[:S_all],
+                             nthreads=threads)
+        t_all = time.perf_counter() - t0
+        sl1 = slice(0, S_one)
+        t0 = time.perf_counter()
+        ra1, rb1 = O.eval_gate(keys.bsk, keys.kskA, keys.kskB, 1, a1[sl1], b1[sl1], a2[sl1], b2[sl1], nthreads=1)
+        t_one = time.perf_counter() - t0
+        ref = None
         kind = "port"
     else:
         return None
-    match = bool(np.array_equal(ra, ao[sl]) and np.array_equal(rb, bo[sl]))
-    return {"value": round(S / t, 2), "unit": "bootstraps/s", "cores": threads, "kind": kind,
-            "sample": f"{S} STD128 {'GINX' if method == 2 else 'LMKCDEY'} AND gates of the same batch, "
-                      f"OpenMP parallel-for over EvalBinGate, {threads} threads, {t:.2f} s wall",
-            "bit_exact_vs_gpu": match}
+    match = bool(np.array_equal(ra, ao[:S_all]) and np.array_equal(rb, bo[:S_all])
+                 and np.array_equal(ra1, ao[sl1]) and np.array_equal(rb1, bo[sl1]))
+    out = {"value": round(S_all / t_all, 2), "unit": "bootstraps/s", "cores": threads, "kind": kind,
+           "sample": f"{S_all} STD128{'' if method == 2 else '_LMKCDEY'} {label} AND gates of the same batch, "
+                     f"OpenMP parallel-for over EvalBinGate on {threads} threads ({t_all:.2f} s wall); 1-core leg: "
+                     f"{S_one} gates ({t_one:.2f} s)",
+           "value_1core": round(S_one / t_one, 3), "ms_per_gate_1core": round(t_one / S_one * 1e3, 2),
+           "host": hi, "bit_exact_vs_gpu": match}
+    if method == 2 and ref is not None:
+        # config 1 (poly-benchmark Native_ntt body, poly-benchmark.h:213-221): one N = 1024 forward
+        # NTT on one core, 60-bit and STD128 moduli; config 2 CPU cost = 4096 x that
+        ntt = {}
+        rng = np.random.default_rng(0x5EED0001)
+        for nm, Q in (("q60", 1152921504606830593), ("std128", 134215681)):
+            x = rng.integers(0, Q, size=1024, dtype=np.uint64)
+            ns = ref.L.ref_ntt_bench(Q, 1024, x.ctypes.data, 20000)
+            ntt[nm] = {"Q": Q, "us_per_ntt_1core": round(ns / 1e3, 3),
+                       "config2_us_4096_1core": round(ns * 4096 / 1e3, 1)}
+        out["ntt_config1"] = ntt
+    return out
 
 
 if __name__ == "__main__":

@@ -1607,13 +1607,21 @@ hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops
 // ---------------------------------------------------------------------------
 // ModSwitch on u64 vectors (standalone entry point)
 // ---------------------------------------------------------------------------
+// RoundqQ exactly as the reference writes it (lwe-pke.cpp:41-46): IEEE double, the product divided
+// before the add (no contraction).  Any moduli: the GPU's double divide is correctly rounded.
+FHE_DEV uint64_t round_qQ_double(uint64_t v, uint64_t to, uint64_t from) {
+#pragma clang fp contract(off)
+    const double x = (double)v * (double)to / (double)from;
+    return (uint64_t)floor(0.5 + x) % to;
+}
+
 __global__ void k_modswitch(uint64_t from, uint64_t to, uint32_t len, uint32_t count, const uint64_t* __restrict__ a,
                             const uint64_t* __restrict__ b, uint64_t* __restrict__ ao, uint64_t* __restrict__ bo) {
     const uint64_t total = (uint64_t)len * count;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x)
-        ao[t] = mod_switch(a[t], from, to);
+        ao[t] = round_qQ_double(a[t], to, from);
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < count; t += (uint64_t)gridDim.x * blockDim.x)
-        bo[t] = mod_switch(b[t], from, to);
+        bo[t] = round_qQ_double(b[t], to, from);
 }
 
 hipError_t launch_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, uint32_t count, const uint64_t* a,

@@ -61,6 +61,13 @@ static void fill_params(const Params& p, fhe_hip_params* o) {
     o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows();
 }
 
+// The stream a context's call runs on: the caller's (or the context's own).  A context has one
+// workspace, so a call on a different stream than the previous call first waits for that
+// stream's work (Engine::use_stream): calls on one context are always ordered.
+static hipStream_t ctx_stream(fhe_hip_ctx* ctx, void* stream) {
+    return ctx->eng.use_stream(static_cast<hipStream_t>(stream));
+}
+
 struct fhe_hip_multi {
     MultiEngine eng;
     fhe_hip_multi(int ps, int m, const int* d, int n) : eng(ps, m, d, n) {}
@@ -272,6 +279,7 @@ int fhe_hip_eval_bingate_packed(fhe_hip_ctx* ctx, int gate, const uint8_t* in1, 
         std::vector<uint64_t> a1(c1 * n), b1(c1), a2(c1 * n), b2(c1), ao(c1 * n), bo(c1);
         unpack_lwe_batch(in1, size1, &n1, &c1, a1.data(), b1.data());
         unpack_lwe_batch(in2, size2, &n2, &c2, a2.data(), b2.data());
+        ctx_stream(ctx, nullptr);
         ctx->eng.eval_gate_host(gate, c1, a1.data(), b1.data(), a2.data(), b2.data(), ao.data(), bo.data());
         pack_lwe_batch(n, c1, ao.data(), bo.data(), out_flags, out);
         return FHE_HIP_OK;
@@ -392,6 +400,7 @@ int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const u
                                const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !io_ok(count, a1, b1, a2, b2, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.eval_gate_host(gate, count, a1, b1, a2, b2, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -403,8 +412,10 @@ int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, 
     if (!ctx || !io_ok(count, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out))
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
         ctx->eng.eval_gate_device(gate, count, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
-                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+                                  s);
+        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -413,8 +424,10 @@ int fhe_hip_blind_rotate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, 
                                       const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2, void* stream) {
     if (!ctx || !io_ok(count, d_a1, d_b1, d_a2, d_b2, d_a1, d_b1)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
         ctx->eng.bootstrap_device(gate, count, d_a1, d_b1, d_a2, d_b2, true,
-                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+                                  s);
+        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -423,8 +436,10 @@ int fhe_hip_keyswitch_workspace_device(fhe_hip_ctx* ctx, size_t count, uint64_t*
                                        void* stream) {
     if (!ctx || (count && (!d_a_out || !d_b_out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
         ctx->eng.keyswitch_workspace_device(count, d_a_out, d_b_out,
-                                            stream ? (hipStream_t)stream : ctx->eng.stream());
+                                            s);
+        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -433,6 +448,7 @@ int fhe_hip_eval_bingate_extended(fhe_hip_ctx* ctx, int gate, size_t count, cons
                                   const uint64_t* a2, const uint64_t* b2, uint64_t* ext_a, uint64_t* ext_b) {
     if (!ctx || !io_ok(count, a1, b1, a2, b2, ext_a, ext_b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.bootstrap_extended_host(gate, count, a1, b1, a2, b2, ext_a, ext_b);
         return FHE_HIP_OK;
     });
@@ -444,6 +460,7 @@ int fhe_hip_eval_gate_multi_batch(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32
     if (!ctx || (count && (!a_in || !b_in || !a_out || !b_out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (k < 2 || k > 4) return fail(FHE_HIP_ERR_INVALID_PARAM, "k must be 2..4");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.eval_gate_multi_host(gate, count, k, a_in, b_in, ptmod, a_out, b_out, extended != 0);
         return FHE_HIP_OK;
     });
@@ -456,8 +473,10 @@ int fhe_hip_eval_gate_multi_batch_device(fhe_hip_ctx* ctx, int gate, uint32_t k,
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (k < 2 || k > 4) return fail(FHE_HIP_ERR_INVALID_PARAM, "k must be 2..4");
     return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
         ctx->eng.eval_gate_multi_device(gate, count, k, d_a_in, d_b_in, ptmod, d_a_out, d_b_out,
-                                        stream ? (hipStream_t)stream : ctx->eng.stream());
+                                        s);
+        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -468,6 +487,7 @@ int fhe_hip_eval_cmux_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a0, 
     if (!ctx || !io_ok(count, a0, b0, a1, b1, a_out, b_out) || (count && (!a2 || !b2)))
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.eval_cmux_host(count, a0, b0, a1, b1, a2, b2, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -479,8 +499,10 @@ int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
     if (!ctx || !io_ok(count, d_a0, d_b0, d_a1, d_b1, d_a_out, d_b_out) || (count && (!d_a2 || !d_b2)))
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
         ctx->eng.eval_cmux_device(count, d_a0, d_b0, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
-                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+                                  s);
+        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -491,6 +513,7 @@ int fhe_hip_eval_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, c
     if (!ctx || !lut || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.fb_host(0, count, a, b, q_in, 0, 0, lut, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -503,8 +526,10 @@ int fhe_hip_eval_func_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
     return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
         ctx->eng.eval_func_device(count, d_a, d_b, q_in, lut, d_a_out, d_b_out,
-                                  stream ? (hipStream_t)stream : ctx->eng.stream());
+                                  s);
+        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -513,6 +538,7 @@ int fhe_hip_eval_floor_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, 
                              uint32_t roundbits, uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.fb_host(1, count, a, b, mod, 0, roundbits, nullptr, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -522,6 +548,7 @@ int fhe_hip_eval_sign_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, c
                             int scheme_switch, uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.fb_host(2, count, a, b, mod, 0, scheme_switch ? 1u : 0u, nullptr, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -539,6 +566,7 @@ int fhe_hip_eval_decomp_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a,
                               uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.fb_host(3, count, a, b, mod, 0, 0, nullptr, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -548,6 +576,7 @@ int fhe_hip_bootstrap_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t*
                                  uint32_t ctmod, const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !f || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.fb_host(4, count, a, b, ctmod, fmod, 0, f, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -557,6 +586,7 @@ int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, c
                             uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
         ctx->eng.keyswitch_host(count, a, b, a_out, b_out);
         return FHE_HIP_OK;
     });
@@ -565,8 +595,7 @@ int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, c
 int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, uint32_t len, size_t count,
                             const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
-    if (q_from == 0 || q_to == 0 || q_from >= (1ull << 40) || q_to >= (1ull << 20))
-        return fail(FHE_HIP_ERR_INVALID_PARAM, "modswitch: moduli out of the exact-integer range");
+    if (q_from == 0 || q_to == 0) return fail(FHE_HIP_ERR_INVALID_PARAM, "modswitch: zero modulus");
     return guarded([&]() -> int {
         if (count == 0) return FHE_HIP_OK;
         const size_t words = count * (size_t)len;
@@ -575,7 +604,7 @@ int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, ui
         uint64_t* d = nullptr;
         FHE_HIP_CHECK(hipSetDevice(ctx->eng.device()));
         FHE_HIP_CHECK(hipMalloc(&d, (2 * words + 2 * count) * 8));
-        hipStream_t s = ctx->eng.stream();
+        hipStream_t s = ctx_stream(ctx, nullptr);
         hipError_t e = hipMemcpyAsync(d, a, words * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(d + words, b, count * 8, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)

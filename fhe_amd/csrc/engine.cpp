@@ -49,7 +49,31 @@ Engine::~Engine() {
                       (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_})
         if (ptr) (void)hipFree(ptr);
+    if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+hipStream_t Engine::use_stream(hipStream_t s) {
+    if (!s) s = stream_;
+    if (pending_ && s != last_stream_) {  // order after the previous call's work on its stream
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        FHE_HIP_CHECK(hipStreamWaitEvent(s, order_ev_, 0));
+    }
+    last_stream_ = s;
+    return s;
+}
+
+void Engine::end_call(hipStream_t s) {
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    if (!order_ev_) FHE_HIP_CHECK(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming));
+    FHE_HIP_CHECK(hipEventRecord(order_ev_, s));
+    pending_ = true;
+}
+
+void Engine::sync_streams() {
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (pending_) FHE_HIP_CHECK(hipEventSynchronize(order_ev_));
 }
 
 void Engine::build_tables() {
@@ -386,11 +410,10 @@ GateArgs Engine::gate_args(int gate, size_t count, uint32_t p, bool multi) const
 
 void Engine::ensure_work(size_t count) {
     if (count <= cap_) return;
-    FHE_HIP_CHECK(hipSetDevice(device_));
-    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+    sync_streams();
     for (void* ptr : {(void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_, (void*)d_ext_b_, (void*)d_wext_a_, (void*)d_wext_b_})
         if (ptr) FHE_HIP_CHECK(hipFree(ptr));
-    d_idx_ = nullptr; d_tvb_ = nullptr; d_ext_a_ = nullptr; d_ext_b_ = nullptr; cap_ = 0;
+    d_idx_ = nullptr; d_tvb_ = nullptr; d_ext_a_ = nullptr; d_ext_b_ = nullptr; cap_ = 0; rot_count_ = 0;
     d_wext_a_ = nullptr; d_wext_b_ = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d_idx_, count * p_.n * sizeof(uint16_t)));
     FHE_HIP_CHECK(hipMalloc(&d_tvb_, count * sizeof(uint32_t)));
@@ -413,8 +436,7 @@ void Engine::ensure_work(size_t count) {
 
 void Engine::ensure_host_stage(size_t count) {
     if (count <= hcap_) return;
-    FHE_HIP_CHECK(hipSetDevice(device_));
-    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+    sync_streams();
     if (d_io_) FHE_HIP_CHECK(hipFree(d_io_));
     d_io_ = nullptr;
     hcap_ = 0;
@@ -438,6 +460,7 @@ void Engine::prep_device(const GateArgs& g, const GateInputs& in, size_t offset,
 }
 
 void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
+    rot_count_ = g.count;
     if (wide_) {
         WideArgs w{};
         w.count = g.count;
@@ -541,7 +564,8 @@ void Engine::eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* 
 void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
     if (!d_ksk_ && !d_wksk_) throw std::logic_error("key-switching key not loaded");
     if (count == 0) return;
-    if (count > cap_) throw std::logic_error("workspace holds fewer ciphertexts than requested");
+    if (count > rot_count_)
+        throw std::invalid_argument("key switch of more ciphertexts than the last blind rotation produced");
     FHE_HIP_CHECK(hipSetDevice(device_));
     keyswitch_ext(count, p_.q, a_out, b_out, s);
 }

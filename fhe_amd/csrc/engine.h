@@ -43,6 +43,12 @@ public:
     const Params& params() const { return p_; }
     int device() const { return device_; }
     hipStream_t stream() const { return stream_; }
+    // The stream a call runs on (nullptr: the context's own).  All calls share one workspace, so
+    // a call on a different stream than the previous call first waits for that stream's work.
+    // (end_call records the point a later call on another stream waits for).
+    hipStream_t use_stream(hipStream_t s);
+    void end_call(hipStream_t s);
+    void sync_streams();  // waits for the context's stream and the last asynchronous call
     bool ready() const { return d_bsk_ && (d_ksk_ || d_wksk_); }
     // the large-precision family (64-bit accumulator, boot_wide.h)
     bool wide() const { return wide_; }
@@ -144,8 +150,13 @@ private:
     uint16_t* d_ops_ = nullptr;
     uint32_t* d_nops_ = nullptr;
     uint16_t* d_ksk_ = nullptr;
-    // workspace
+    // cross-stream ordering (use_stream)
+    hipStream_t last_stream_ = nullptr;
+    hipEvent_t order_ev_ = nullptr;
+    bool pending_ = false;
+    // workspace; rot_count_ = ciphertexts the last blind rotation left in it
     size_t cap_ = 0;
+    size_t rot_count_ = 0;
     uint16_t* d_idx_ = nullptr;
     uint32_t* d_tvb_ = nullptr;
     uint32_t* d_ext_a_ = nullptr;

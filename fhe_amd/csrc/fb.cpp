@@ -140,11 +140,11 @@ void Engine::eval_func_device(size_t count, const uint64_t* a, const uint64_t* b
         // ct1 = ct with a's modulus raised to dq (values unchanged); ct2 = ct1 + beta mod dq
         FHE_HIP_CHECK(hipMemcpyAsync(ua, ta, count * n * 8, hipMemcpyDeviceToDevice, s));
         FHE_HIP_CHECK(hipMemcpyAsync(ub, tb, count * 8, hipMemcpyDeviceToDevice, s));
-        FHE_HIP_CHECK(launch_lwe_addb(ub, kBeta, dq, count, s));
+        FHE_HIP_CHECK(launch_lwe_addb(ub, kBeta % dq, dq, count, s));
         auto f0 = tv_values(TV_HALF, nullptr, 0, dq, dq);
         bootstrap_func_device(count, ua, ub, (uint32_t)dq, f0.data(), dq, ca, cb, s);  // ct3
         FHE_HIP_CHECK(launch_lwe_sub(ta, tb, ca, cb, ca, cb, dq, (uint32_t)n, count, s));  // EvalSubEq2(ct1, ct3)
-        FHE_HIP_CHECK(launch_lwe_addb(cb, kBeta, dq, count, s));
+        FHE_HIP_CHECK(launch_lwe_addb(cb, kBeta % dq, dq, count, s));
         FHE_HIP_CHECK(launch_lwe_addb(cb, dq - (q_in >> 1), dq, count, s));              // - q/2
         auto f2 = tv_values(TV_LUT_ANTI, lut, q_in, dq, dq);                              // LUT2 = LUT || LUT
         bootstrap_func_device(count, ca, cb, (uint32_t)dq, f2.data(), dq, ua, ub, s);  // ct4

@@ -16,11 +16,21 @@
 namespace fhe_amd {
 
 namespace {
-// RoundqQ(v, q_out, qKS) = floor(0.5 + v q_out / qKS) mod q_out (lwe-pke.cpp:41-46) as the exact
-// integer floor((2 v q_out + qKS) / (2 qKS)) mod q_out: qKS is a power of two, so the double
-// expression is exact (v q_out < 2^14 2^32 < 2^53) and so is this one.
+// the reference's RoundqQ expression itself (lwe-pke.cpp:41-46): IEEE double, no contraction
+FHE_DEV uint64_t round_qQ_ref(uint64_t v, uint64_t q, uint64_t Q) {
+#pragma clang fp contract(off)
+    const double x = (double)v * (double)q / (double)Q;
+    return (uint64_t)floor(0.5 + x) % q;
+}
+// RoundqQ(v, q_out, qKS) = floor(0.5 + v q_out / qKS) mod q_out (lwe-pke.cpp:41-46).  qKS is a power
+// of two, so while qKS q_out <= 2^52 every step of the double expression is exact (the product
+// v q_out < 2^52, the division by 2^k, and the add of 0.5 to a value with < 2^52 units of 2^-k)
+// and it equals the integer floor((2 v q_out + qKS) / (2 qKS)).  Larger q_out (BootstrapFunc's
+// fmod can reach 2^40) take the reference's double expression itself.  q_out is uniform.
 FHE_DEV uint64_t mod_switch_up(uint64_t v, uint32_t qKS, uint64_t q_out) {
-    return ((2 * v * q_out + qKS) / (2 * (uint64_t)qKS)) % q_out;
+    if ((unsigned __int128)qKS * q_out <= ((unsigned __int128)1 << 52))
+        return ((2 * v * q_out + qKS) / (2 * (uint64_t)qKS)) % q_out;
+    return round_qQ_ref(v, q_out, qKS);
 }
 }  // namespace
 

@@ -12,7 +12,10 @@
  *     no C++ exception ever crosses this boundary (c_api.cpp:224-235);
  *   - the caller owns host buffers; a context owns its device copies;
  *   - host-buffer calls are synchronous; *_device calls are asynchronous on the
- *     given HIP stream (NULL = the context's own stream);
+ *     given HIP stream (NULL = the context's own stream).  A context has one
+ *     device workspace: a call on a different stream than the context's previous
+ *     asynchronous call first waits for that call's work (an event recorded on its
+ *     stream), so the calls on one context always execute in issue order;
  *   - a context is bound to one device and is not thread-safe: use one per
  *     host thread / device (BinFHEContext is likewise used per process).
  * Integers are the reference's u64 words (NativeInteger, NATIVEINT=64).
@@ -156,10 +159,10 @@ int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const u
 int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
                                       const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2,
                                       uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
-/* The two stages of fhe_hip_eval_bingate_batch_device, separately launchable
- * (Backend::BlindRotateBatch, then KeySwitchBatch + ModSwitchBatch):
+/* The two stages of fhe_hip_eval_bingate_batch_device, separately launchable:
  * blind_rotate leaves the mod-switched ctExt (N+1 values mod qKS per gate) in
- * the context's workspace; keyswitch consumes it. */
+ * the context's workspace; keyswitch consumes it (count must not exceed the
+ * count of the last blind rotation: FHE_HIP_ERR_INVALID_PARAM otherwise). */
 int fhe_hip_blind_rotate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* d_a1,
                                       const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2, void* stream);
 int fhe_hip_keyswitch_workspace_device(fhe_hip_ctx* ctx, size_t count, uint64_t* d_a_out, uint64_t* d_b_out,
@@ -216,7 +219,8 @@ int fhe_hip_bootstrap_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t*
 /* LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372): (N, qKS) -> (n, qKS) */
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
                             uint64_t* b_out);
-/* LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:254-261) */
+/* LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:254-261): RoundqQ in IEEE double exactly as the
+ * reference evaluates it (lwe-pke.cpp:41-46), for any nonzero moduli */
 int fhe_hip_modswitch_batch(fhe_hip_ctx* ctx, uint64_t q_from, uint64_t q_to, uint32_t len, size_t count,
                             const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
 

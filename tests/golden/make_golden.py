@@ -258,8 +258,51 @@ def make_large(names=tuple(LARGE_SETS)):
         print(name, "large ok", sorted(k for k in out if k.endswith("_a")))
 
 
+# BASELINE configs 4 and 5 at their stated size: 65,536 AND gates through one context (the
+# global batch of the 8-GPU run); hashes of the reference's outputs, whole and per 8192-gate shard
+FULL_GATES = 65536
+FULL_SHARD = 8192
+
+
+def full_inputs(name, count=FULL_GATES):
+    """keys (same seed as gates_<name>.npz) and `count` seeded AND-gate input pairs"""
+    from fhe_amd import binfhe as bf
+    ps, m = GATE_SETS[name]
+    key_seed = 0xB0070000 + ps
+    keys = bf.keygen(ps, m, key_seed)
+    rng = np.random.default_rng(0xF011 + ps)
+    bits1, bits2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+    a1, b1 = bf.encrypt(ps, m, keys.sk, bits1, 0xF0110000 + ps)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, bits2, 0xF0120000 + ps)
+    return ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2
+
+
+def make_full(names=("std128", "lmkcdey"), nthreads=8):
+    import time
+    for name in names:
+        ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2 = full_inputs(name)
+        ref = Ref(ps, m)
+        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        t0 = time.time()
+        ao, bo = ref.eval_gate(GATES["AND"], a1, b1, a2, b2, nthreads=nthreads)
+        dt = time.time() - t0
+        dec = np.array([ref.decrypt(keys.sk, ao[i], bo[i], ref.q) for i in range(0, FULL_GATES, 97)])
+        assert np.array_equal(dec, (bits1 & bits2)[::97]), "reference AND outputs do not decrypt"
+        shards = [sha(ao[s:s + FULL_SHARD]) + sha(bo[s:s + FULL_SHARD]) for s in range(0, FULL_GATES, FULL_SHARD)]
+        np.savez_compressed(os.path.join(HERE, f"full_{name}.npz"), paramset=ps, method=m,
+                            key_seed=np.uint64(key_seed), count=FULL_GATES, shard=FULL_SHARD, gate=GATES["AND"],
+                            out_sha=np.array(sha(ao) + sha(bo)), shard_sha=np.array(shards),
+                            out_a_head=ao[:16].astype(np.uint16), out_b_head=bo[:16].astype(np.uint16),
+                            keys_sha=np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB)),
+                            in_sha=np.array(sha(a1) + sha(b1) + sha(a2) + sha(b2)),
+                            ref_seconds=dt, ref_threads=nthreads)
+        print(name, "full ok", FULL_GATES, f"{dt:.0f} s on {nthreads} threads", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "full":   # ~15 min per set on 8 cores
+        make_full(sys.argv[2:] or ("std128", "lmkcdey"))
     if what in ("ntt", "all"):
         make_ntt()
     if what in ("gates", "all"):
