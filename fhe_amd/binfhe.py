@@ -103,6 +103,13 @@ def _setup(L):
     L.fhe_hip_multi_destroy.restype = None
     L.fhe_hip_multi_load_keys.argtypes = [vp, vp, sz, vp, sz, vp, sz]
     L.fhe_hip_multi_eval_bingate_batch.argtypes = [vp, ctypes.c_int, sz, vp, vp, vp, vp, vp, vp]
+    L.fhe_hip_blind_rotate_acc_batch.argtypes = [vp, sz, vp, u64, vp]
+    L.fhe_hip_blind_rotate_acc_batch_device.argtypes = [vp, sz, vp, u64, vp, vp]
+    L.fhe_hip_external_product_batch.argtypes = [vp, sz, vp, vp, vp]
+    L.fhe_hip_external_product_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.fhe_hip_max_batch_size.argtypes = [vp, vp]
+    L.fhe_hip_device_memory.argtypes = [ctypes.c_int, vp, vp]
+    L.fhe_hip_unpack_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, vp, sz, vp, vp]
     L._binfhe_ready = True
     return L
 
@@ -452,6 +459,30 @@ class GateEngine:
         bo = np.zeros(cnt, np.uint64)
         check(L().fhe_hip_keyswitch_batch(self._h, cnt, ptr(a), ptr(b), ptr(ao), ptr(bo)))
         return ao, bo
+
+    # ---- the Backend seam (backend.h:131-192) ----
+    def blind_rotate_acc(self, a, ctmod, acc):
+        """Backend::BlindRotateBatch = EvalAcc: a [count][n] mod ctmod, acc [count][2][N] EVALUATION
+        (canonical mod Q) -> the rotated accumulators (a new array)."""
+        a = _u64(np.atleast_2d(a))
+        out = np.array(acc, dtype=np.uint64, copy=True, order="C").reshape(len(a), 2, self.params.N)
+        check(L().fhe_hip_blind_rotate_acc_batch(self._h, len(a), ptr(a), ctmod, ptr(out)))
+        return out
+
+    def external_product(self, rgsw, rlwe):
+        """Backend::ExternalProductBatch: rgsw [count][digitsG2][2][N], rlwe [count][2][N] (EVALUATION)
+        -> rgsw (x) rlwe [count][2][N]."""
+        N, d2 = self.params.N, 2 * (self.params.digitsG - 1)
+        rgsw = _u64(rgsw).reshape(-1, d2, 2, N)
+        rlwe = _u64(rlwe).reshape(-1, 2, N)
+        out = np.zeros_like(rlwe)
+        check(L().fhe_hip_external_product_batch(self._h, len(rlwe), ptr(rgsw), ptr(rlwe), ptr(out)))
+        return out
+
+    def max_batch_size(self):
+        v = ctypes.c_size_t()
+        check(L().fhe_hip_max_batch_size(self._h, ctypes.byref(v)))
+        return v.value
 
     def modswitch(self, q_from, q_to, a, b):
         a, b = _u64(a), _u64(b)

@@ -30,6 +30,7 @@ struct BootTables {
     uint32_t ninvR;  // N^-1 (Montgomery): scales the initial accumulator
     uint32_t w1R;    // TableI[1] (Montgomery) for the last iNTT stage
     uint32_t oneR;   // 2^32 mod Q (Montgomery 1): x -> x mod Q by one signed Montgomery product
+    uint32_t nR;     // N (Montgomery): undoes the N^-1 scaling when the accumulator is written out
 };
 
 // Digit exchange between the half-waves in the external products: 1 = ds_bpermute of the other
@@ -75,6 +76,12 @@ struct GateArgs {
     // the large-precision family (boot_wide.h): the same window / test vector / b with 64-bit Q
     uint64_t lv64, uv64, b64;
     const uint64_t* tv64;
+    // Backend::BlindRotate / ExternalProduct seam (backend.h:131-146, 177-192): non-null selects the
+    // accumulator-I/O instantiation of the blind-rotation kernels.  The initial accumulator is read
+    // from acc_io[count][2][N] (EVALUATION, bit-reversed as the reference stores it, canonical mod Q)
+    // instead of being built from the test vector, and the final one is written back there in the
+    // same form instead of the extraction / ModSwitch epilogue.
+    uint64_t* acc_io;
 };
 
 // The LWE ciphertext a gate bootstraps: ct = sum_j (-1)^{neg_j} ct_j + (0, boff) mod q, then
@@ -106,6 +113,13 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
 // (q - a_i) mod q (rgsw-acc-dm.cpp:62-77), + test-vector b
 hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops, uint32_t* nops, uint32_t* tvb,
                           uint32_t maxops, uint32_t baseR, uint32_t digitsR, hipStream_t s);
+// ExternalProduct seam: raw RGSW keys [count][dG2 = 4][2][N] (EVAL, u64) -> the op-list kernel's
+// resident layout (row_off, half-swapped rows, Montgomery with N^-1 folded in), key g at
+// out + g * 4 * 2 * N words
+hipError_t launch_pack_rgsw(const uint64_t* raw, size_t count, uint32_t N, uint32_t Q, uint32_t ninv_mont,
+                            uint32_t* out, hipStream_t s);
+// one op per item: ops[g * maxops] = g, nops[g] = 1 (ExternalProduct through the DM op loop)
+hipError_t launch_single_ops(uint16_t* ops, uint32_t* nops, uint32_t count, uint32_t maxops, hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out) (:254-261), KSK as u16 rows of 512;
 // q_out = 0: no final switch (output mod qKS)
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,

@@ -546,6 +546,25 @@ FHE_DEV uint32_t mod_switch(uint64_t v, uint64_t from, uint64_t to) {
     return (uint32_t)(r % to);
 }
 
+// accumulator I/O of the seam instantiations (GateArgs::acc_io): lane (h, l) register r holds
+// EVAL slot (l << 5) | r of component h.  In: canonical u64 -> N^-1-scaled residue (the keys carry
+// N^-1, BootTables::ninvR).  Out: any |acc| < 2^31 -> acc N mod Q, canonical u64.
+FHE_DEV void acc_load(uint32_t (&acc)[32], const GateArgs& g, uint32_t gate, int h, int l, uint32_t ninvR,
+                      const Mod& m) {
+    const uint64_t* src = g.acc_io + ((size_t)gate * 2 + h) * g.N + ((uint32_t)l << 5);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) acc[r] = csub(mont_mul((uint32_t)src[r], ninvR, m), m.Q);
+}
+FHE_DEV void acc_store(const uint32_t (&acc)[32], const GateArgs& g, uint32_t gate, int h, int l, uint32_t nR,
+                       const Mod& m) {
+    uint64_t* dst = g.acc_io + ((size_t)gate * 2 + h) * g.N + ((uint32_t)l << 5);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const int32_t v = (int32_t)smont_mul(acc[r], nR, m);
+        dst[r] = (uint64_t)(uint32_t)(v < 0 ? v + (int32_t)m.Q : v);
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -592,7 +611,9 @@ constexpr size_t boot_lds(bool full, bool lz) {
 // MFULL: full-resolution monomial table (ciphertext modulus 2N, any exponent); otherwise the
 // half-resolution table (even exponents: every gate), where slots r and r ^ 1 share a monomial
 // and the compiler drops half of the table reads.
-template <bool MFULL, bool LZ>
+// ACCIO: Backend::BlindRotate seam -- the accumulator is read from and written back to g.acc_io
+// (GateArgs) instead of the test vector / extraction (EvalAcc itself, rgsw-acc-cggi.cpp:59-68)
+template <bool MFULL, bool LZ, bool ACCIO = false>
 __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     k_blind_rotate_ginx(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint16_t* __restrict__ idx,
                         const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
@@ -634,7 +655,9 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 
     // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[32];
-    {
+    if (ACCIO) {
+        acc_load(acc, g, gate, h, l, T.ninvR, m);
+    } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
@@ -853,6 +876,10 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #undef ki
     }
 
+    if (ACCIO) {
+        acc_store(acc, g, gate, h, l, T.nR, m);
+        return;
+    }
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
     // 2N-1), both to COEF; ctExt = (acc0 coefficients, (Q>>3)+1 + acc1[0]); then ModSwitch to qKS.
     // In COEF, Transpose maps coefficient k to -a_(N-k) (k >= 1), a_0 to itself.
@@ -895,21 +922,19 @@ hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, cons
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
     const uint2* k = reinterpret_cast<const uint2*>(bsk);
     const bool lz  = t.Q < (1u << 27);
-    if (g.ctmod == 2 * g.N) {
-        if (lz)
-            hipLaunchKernelGGL((k_blind_rotate_ginx<true, true>), dim3(blocks), dim3(256), boot_lds(true, true), s, g, t, k,
-                               idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
-        else
-            hipLaunchKernelGGL((k_blind_rotate_ginx<true, false>), dim3(blocks), dim3(256), boot_lds(true, false), s, g, t,
-                               k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+    const bool full = g.ctmod == 2 * g.N;
+#define FHE_LAUNCH_GINX(MF, LZ_, IO)                                                                        \
+    hipLaunchKernelGGL((k_blind_rotate_ginx<MF, LZ_, IO>), dim3(blocks), dim3(256), boot_lds(MF, LZ_), s, g, t, k, \
+                       idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
+    if (g.acc_io) {
+        if (full) { if (lz) FHE_LAUNCH_GINX(true, true, true); else FHE_LAUNCH_GINX(true, false, true); }
+        else { if (lz) FHE_LAUNCH_GINX(false, true, true); else FHE_LAUNCH_GINX(false, false, true); }
+    } else if (full) {
+        if (lz) FHE_LAUNCH_GINX(true, true, false); else FHE_LAUNCH_GINX(true, false, false);
     } else {
-        if (lz)
-            hipLaunchKernelGGL((k_blind_rotate_ginx<false, true>), dim3(blocks), dim3(256), boot_lds(false, true), s, g, t,
-                               k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
-        else
-            hipLaunchKernelGGL((k_blind_rotate_ginx<false, false>), dim3(blocks), dim3(256), boot_lds(false, false), s, g, t,
-                               k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+        if (lz) FHE_LAUNCH_GINX(false, true, false); else FHE_LAUNCH_GINX(false, false, false);
     }
+#undef FHE_LAUNCH_GINX
     return hipGetLastError();
 }
 
@@ -1099,7 +1124,8 @@ FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* 
 // DM: the AP/DM accumulator runs the same op loop with external products only (AddToAccDM ==
 // AddToAccLMKCDEY, rgsw-acc-dm.cpp:119-145) and no initial automorphism of acc1.
 // DM needs no automorphism path and fits 168 VGPRs: 3 waves per SIMD
-template <bool DM, bool LZ>
+// ACCIO: Backend::BlindRotate / ExternalProduct seam (GateArgs::acc_io), as in k_blind_rotate_ginx
+template <bool DM, bool LZ, bool ACCIO = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? FHE_DM_WAVES : FHE_LMK_WAVES)))
     k_blind_rotate_lmk(GateArgs g, BootTables T, const uint2* __restrict__ bsk, const uint2* __restrict__ autok,
                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
@@ -1126,7 +1152,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
     const uint32_t M = 2 * g.N;
 
     uint32_t acc[32];
-    {
+    if (ACCIO) {
+        acc_load(acc, g, gate, h, l, T.ninvR, m);
+        // acc1 <- acc1(X^(2N-5)) (:99) on half 1 only: X^1 (the identity) on half 0
+        if (!DM) automorphism_eval(acc, tile, l, h ? M - 5 : 1u);
+    } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
@@ -1362,6 +1392,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #endif
         }
     }
+    if (ACCIO) {
+        acc_store(acc, g, gate, h, l, T.nR, m);
+        return;
+    }
     // extraction, identical to GINX
     inv_pass_s<20, LZ>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m.oneR, m);
     wave_lds_sync();
@@ -1575,18 +1609,18 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
     const uint2* ak = reinterpret_cast<const uint2*>(autok);
     const bool lz   = t.Q < (1u << 27);
     if (t.Q >= (1u << 28)) return hipErrorInvalidValue;  // signed residue bounds
-    if (dm && lz)
-        hipLaunchKernelGGL((k_blind_rotate_lmk<true, true>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
-                           maxops, tvb, ext_a, ext_b);
-    else if (dm)
-        hipLaunchKernelGGL((k_blind_rotate_lmk<true, false>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
-                           maxops, tvb, ext_a, ext_b);
-    else if (lz)
-        hipLaunchKernelGGL((k_blind_rotate_lmk<false, true>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
-                           maxops, tvb, ext_a, ext_b);
-    else
-        hipLaunchKernelGGL((k_blind_rotate_lmk<false, false>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops,
-                           maxops, tvb, ext_a, ext_b);
+#define FHE_LAUNCH_LMK(DM_, LZ_, IO)                                                                          \
+    hipLaunchKernelGGL((k_blind_rotate_lmk<DM_, LZ_, IO>), dim3(blocks), dim3(256), lds, s, g, t, k, ak, ops, nops, \
+                       maxops, tvb, ext_a, ext_b)
+    if (g.acc_io) {
+        if (dm) { if (lz) FHE_LAUNCH_LMK(true, true, true); else FHE_LAUNCH_LMK(true, false, true); }
+        else { if (lz) FHE_LAUNCH_LMK(false, true, true); else FHE_LAUNCH_LMK(false, false, true); }
+    } else if (dm) {
+        if (lz) FHE_LAUNCH_LMK(true, true, false); else FHE_LAUNCH_LMK(true, false, false);
+    } else {
+        if (lz) FHE_LAUNCH_LMK(false, true, false); else FHE_LAUNCH_LMK(false, false, false);
+    }
+#undef FHE_LAUNCH_LMK
     return hipGetLastError();
 }
 
@@ -1601,6 +1635,63 @@ hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops
     if (digitsR > 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_prep_dm_w, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, in, g,
                        ops, nops, tvb, maxops, baseR, digitsR);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ExternalProduct seam (Backend::ExternalProduct[Batch], backend.h:141-146, 187-192): per-item
+// RGSW keys in the reference's raw EVAL layout [dG2 = 4][2][N] packed into the op-list kernel's
+// resident layout (the layout Engine::load_bsk writes), then one EXT op per item.
+// ---------------------------------------------------------------------------
+__global__ void k_pack_rgsw(const uint64_t* __restrict__ raw, uint32_t count, uint32_t N, uint32_t Q,
+                            uint32_t ninv_mont, uint32_t* __restrict__ out) {
+    // ninv_mont = N^-1 2^32 mod Q: out = raw N^-1 2^32 mod Q (Montgomery form of raw N^-1)
+    const uint64_t words = (uint64_t)count * 4 * 2 * N;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
+        // t enumerates destination words of key g: (d, k, lane, e) in row_off order
+        const uint64_t g = t / (8 * N), w = t % (8 * N);
+        uint32_t d, k, lane, e;
+        if (kRowU4) {   // (((d * 8 + k/2) * 64 + lane) * 4 + (k & 1) * 2 + e
+            const uint32_t q4 = (uint32_t)(w >> 2), sub = (uint32_t)(w & 3);
+            lane = q4 & 63;
+            const uint32_t dk = q4 >> 6;
+            d = dk >> 3;
+            k = ((dk & 7) << 1) | (sub >> 1);
+            e = sub & 1;
+        } else {
+            e = (uint32_t)(w & 1);
+            lane = (uint32_t)(w >> 1) & 63;
+            k = (uint32_t)(w >> 7) & 15;
+            d = (uint32_t)(w >> 11);
+        }
+        const uint32_t h = lane >> 5, l = lane & 31;
+        const uint32_t row = kBskHalfSwap ? d ^ h : d;
+        const uint64_t src = raw[g * 8 * N + ((uint64_t)row * 2 + h) * N + l * 32 + 2 * k + e];
+        out[g * 8 * N + row_off(d, k, lane, e)] = (uint32_t)((src % Q) * ninv_mont % Q);
+    }
+}
+
+__global__ void k_single_ops(uint16_t* __restrict__ ops, uint32_t* __restrict__ nops, uint32_t count, uint32_t maxops) {
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < count; g += gridDim.x * blockDim.x) {
+        ops[(size_t)g * maxops] = (uint16_t)g;
+        nops[g] = 1;
+    }
+}
+
+hipError_t launch_pack_rgsw(const uint64_t* raw, size_t count, uint32_t N, uint32_t Q, uint32_t ninv_mont,
+                            uint32_t* out, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (N != 1024 || count > 0x7fffffffull) return hipErrorInvalidValue;
+    const uint64_t words = (uint64_t)count * 8 * N;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((words + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_pack_rgsw, dim3(blocks), dim3(256), 0, s, raw, (uint32_t)count, N, Q, ninv_mont, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_single_ops(uint16_t* ops, uint32_t* nops, uint32_t count, uint32_t maxops, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (count > 0x8000u) return hipErrorInvalidValue;   // op codes: key index < 0x8000
+    hipLaunchKernelGGL(k_single_ops, dim3((count + 255) / 256), dim3(256), 0, s, ops, nops, count, maxops);
     return hipGetLastError();
 }
 

@@ -47,6 +47,22 @@ int guarded(F&& f) {
         return fail(FHE_HIP_ERR_INVALID_PARAM, "unknown exception");
     }
 }
+// device scratch for a synchronous host-buffer call (freed on every exit path)
+struct DeviceScratch {
+    uint64_t* p = nullptr;
+    DeviceScratch(int device, size_t bytes) {
+        FHE_HIP_CHECK(hipSetDevice(device));
+        FHE_HIP_CHECK(hipMalloc(&p, bytes));
+    }
+    ~DeviceScratch() {
+        if (p) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+        }
+    }
+    DeviceScratch(const DeviceScratch&) = delete;
+    DeviceScratch& operator=(const DeviceScratch&) = delete;
+};
 }  // namespace
 
 struct fhe_hip_ctx {
@@ -503,6 +519,113 @@ int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
         ctx->eng.eval_cmux_device(count, d_a0, d_b0, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
                                   s);
         ctx->eng.end_call(s);
+        return FHE_HIP_OK;
+    });
+}
+
+// ---- the Backend seam (backend.h:73-247) ----
+int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, uint64_t ctmod, uint64_t* acc) {
+    if (!ctx || (count && (!a || !acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (ctmod == 0 || ctmod > 0xffffffffull) return fail(FHE_HIP_ERR_INVALID_PARAM, "bad ciphertext modulus");
+    return guarded([&]() -> int {
+        if (count == 0) return FHE_HIP_OK;
+        const Params& p = ctx->eng.params();
+        const size_t aw = count * p.n, accw = count * 2 * (size_t)p.N;
+        for (size_t i = 0; i < aw; ++i)
+            if (a[i] >= ctmod) return fail(FHE_HIP_ERR_INVALID_PARAM, "a not reduced mod the ciphertext modulus");
+        for (size_t i = 0; i < accw; ++i)
+            if (acc[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "accumulator not reduced mod Q");
+        hipStream_t s = ctx_stream(ctx, nullptr);
+        DeviceScratch d(ctx->eng.device(), (aw + accw) * 8);
+        FHE_HIP_CHECK(hipMemcpyAsync(d.p, a, aw * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(d.p + aw, acc, accw * 8, hipMemcpyHostToDevice, s));
+        ctx->eng.blind_rotate_acc_device(count, d.p, (uint32_t)ctmod, d.p + aw, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(acc, d.p + aw, accw * 8, hipMemcpyDeviceToHost, s));
+        FHE_HIP_CHECK(hipStreamSynchronize(s));
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_blind_rotate_acc_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, uint64_t ctmod,
+                                          uint64_t* d_acc, void* stream) {
+    if (!ctx || (count && (!d_a || !d_acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (ctmod == 0 || ctmod > 0xffffffffull) return fail(FHE_HIP_ERR_INVALID_PARAM, "bad ciphertext modulus");
+    return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
+        ctx->eng.blind_rotate_acc_device(count, d_a, (uint32_t)ctmod, d_acc, s);
+        ctx->eng.end_call(s);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_external_product_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* rgsw, const uint64_t* rlwe,
+                                   uint64_t* result) {
+    if (!ctx || (count && (!rgsw || !rlwe || !result))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        if (count == 0) return FHE_HIP_OK;
+        const Params& p = ctx->eng.params();
+        const size_t kw = count * (size_t)p.digitsG2 * 2 * p.N, rw = count * 2 * (size_t)p.N;
+        for (size_t i = 0; i < kw; ++i)
+            if (rgsw[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "RGSW key not reduced mod Q");
+        for (size_t i = 0; i < rw; ++i)
+            if (rlwe[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "RLWE ciphertext not reduced mod Q");
+        hipStream_t s = ctx_stream(ctx, nullptr);
+        DeviceScratch d(ctx->eng.device(), (kw + rw) * 8);
+        FHE_HIP_CHECK(hipMemcpyAsync(d.p, rgsw, kw * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(d.p + kw, rlwe, rw * 8, hipMemcpyHostToDevice, s));
+        ctx->eng.external_product_device(count, d.p, d.p + kw, d.p + kw, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(result, d.p + kw, rw * 8, hipMemcpyDeviceToHost, s));
+        FHE_HIP_CHECK(hipStreamSynchronize(s));
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_external_product_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_rgsw,
+                                          const uint64_t* d_rlwe, uint64_t* d_result, void* stream) {
+    if (!ctx || (count && (!d_rgsw || !d_rlwe || !d_result))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        hipStream_t s = ctx_stream(ctx, stream);
+        ctx->eng.external_product_device(count, d_rgsw, d_rlwe, d_result, s);
+        ctx->eng.end_call(s);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_max_batch_size(fhe_hip_ctx* ctx, size_t* max_count) {
+    if (!ctx || !max_count) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        *max_count = ctx->eng.max_batch();
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_device_memory(int device, size_t* free_bytes, size_t* total_bytes) {
+    if (!free_bytes && !total_bytes) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    size_t fr = 0, tot = 0;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMemGetInfo(&fr, &tot);
+    if (e != hipSuccess) return hip_fail(e, "hipMemGetInfo");
+    if (free_bytes) *free_bytes = fr;
+    if (total_bytes) *total_bytes = tot;
+    return FHE_HIP_OK;
+}
+
+int fhe_hip_unpack_keys(int paramset, int method, const uint8_t* bsk_packed, size_t bsk_size, uint64_t* bsk,
+                        const uint8_t* ksk_packed, size_t ksk_size, uint64_t* kskA, uint64_t* kskB) {
+    if ((!bsk_packed || !bsk) && (!ksk_packed || !kskA || !kskB)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const Params p = make_params(paramset, method);
+        if (bsk_packed && bsk) {
+            size_t words = 0;
+            const uint64_t* raw = unpack_bsk(p, bsk_packed, bsk_size, &words);
+            std::copy(raw, raw + words, bsk);
+        }
+        if (ksk_packed && kskA && kskB) {
+            const uint64_t *A = nullptr, *B = nullptr;
+            unpack_ksk(p, ksk_packed, ksk_size, &A, &B);
+            std::copy(A, A + p.ksk_rows() * p.n, kskA);
+            std::copy(B, B + p.ksk_rows(), kskB);
+        }
         return FHE_HIP_OK;
     });
 }

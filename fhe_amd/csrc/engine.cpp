@@ -47,7 +47,8 @@ Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
                       (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
-                      d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_})
+                      d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
+                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_})
         if (ptr) (void)hipFree(ptr);
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -155,6 +156,7 @@ void Engine::build_tables() {
     tabs_.ninvR = to_mont(h.ninv, Q);
     tabs_.w1R = to_mont(h.tabI[1], Q);
     tabs_.oneR = to_mont(1, Q);
+    tabs_.nR = to_mont(p_.N, Q);
 }
 
 void Engine::build_tables_wide() {
@@ -505,6 +507,90 @@ void Engine::bootstrap_device(int gate, size_t count, const uint64_t* a1, const 
     GateInputs in{{a1, a2, nullptr, nullptr}, {b1, b2, nullptr, nullptr}, 2, 0, 0};
     prep_device(g, in, 0, s);
     rotate_device(g, s);
+}
+
+void Engine::blind_rotate_acc_device(size_t count, const uint64_t* a, uint32_t ctmod, uint64_t* acc, hipStream_t s) {
+    if (!d_bsk_) throw std::logic_error("bootstrapping key not loaded");
+    if (wide_) throw std::invalid_argument("BlindRotate seam: 32-bit parameter sets only");
+    if (ctmod < 2 || (ctmod & (ctmod - 1)) || ctmod > 2 * p_.N)
+        throw std::invalid_argument("BlindRotate: ciphertext modulus must be a power of two <= 2N");
+    if (p_.method == M_AP && ctmod != p_.q)  // EvalAcc DM reads a_i modulo q (rgsw-acc-dm.cpp:64-69)
+        throw std::invalid_argument("BlindRotate (AP): ciphertext modulus must be q");
+    if (p_.method == M_LMKCDEY && ctmod != 2 * p_.N)  // a_i are taken mod M = 2N (rgsw-acc-lmkcdey.cpp:84-86)
+        throw std::invalid_argument("BlindRotate (LMKCDEY): ciphertext modulus must be 2N");
+    if (count == 0) return;
+    if (!a || !acc) throw std::invalid_argument("null argument");
+    if (count > 0x7fffffffull) throw std::invalid_argument("batch too large");
+    ensure_work(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    GateArgs g{};
+    g.count = (uint32_t)count;
+    g.n = p_.n;
+    g.N = p_.N;
+    g.q = p_.q;
+    g.qKS = p_.qKS;
+    g.ctmod = ctmod;
+    g.factor = 2 * p_.N / ctmod;
+    g.gbits = p_.gBits;
+    g.acc_io = acc;
+    // the prep kernels read one input ciphertext; its b only feeds the (unused) test vector
+    GateInputs in{{a, nullptr, nullptr, nullptr}, {a, nullptr, nullptr, nullptr}, 1, 0, 0};
+    prep_device(g, in, 0, s);
+    rotate_device(g, s);
+    rot_count_ = 0;  // no ctExt left in the workspace
+}
+
+void Engine::external_product_device(size_t count, const uint64_t* rgsw, const uint64_t* rlwe, uint64_t* result,
+                                     hipStream_t s) {
+    if (wide_) throw std::invalid_argument("ExternalProduct seam: 32-bit parameter sets only");
+    if (p_.digitsG2 != 4) throw std::invalid_argument("device path expects digitsG = 3");
+    if (count == 0) return;
+    if (!rgsw || !rlwe || !result) throw std::invalid_argument("null argument");
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    constexpr size_t kChunk = 0x8000;   // op codes hold key indices < 0x8000
+    const size_t keyw = (size_t)p_.digitsG2 * 2 * p_.N;
+    const size_t cap = std::min(count, kChunk);
+    if (cap > epcap_) {
+        sync_streams();
+        for (void* ptr : {(void*)d_epk_, (void*)d_epops_, (void*)d_epn_})
+            if (ptr) FHE_HIP_CHECK(hipFree(ptr));
+        d_epk_ = nullptr; d_epops_ = nullptr; d_epn_ = nullptr; epcap_ = 0;
+        FHE_HIP_CHECK(hipMalloc(&d_epk_, cap * keyw * sizeof(uint32_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_epops_, cap * sizeof(uint16_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_epn_, cap * sizeof(uint32_t)));
+        epcap_ = cap;
+    }
+    const uint32_t ninv_mont = to_mont(invmod(p_.N, p_.Q), p_.Q);
+    for (size_t off = 0; off < count; off += kChunk) {
+        const size_t c = std::min(kChunk, count - off);
+        if (result + off * 2 * p_.N != rlwe + off * 2 * p_.N)
+            FHE_HIP_CHECK(hipMemcpyAsync(result + off * 2 * p_.N, rlwe + off * 2 * p_.N, c * 2 * p_.N * 8,
+                                         hipMemcpyDeviceToDevice, s));
+        FHE_HIP_CHECK(launch_pack_rgsw(rgsw + off * keyw, c, p_.N, (uint32_t)p_.Q, ninv_mont, d_epk_, s));
+        FHE_HIP_CHECK(launch_single_ops(d_epops_, d_epn_, (uint32_t)c, 1, s));
+        GateArgs g{};
+        g.count = (uint32_t)c;
+        g.n = p_.n;
+        g.N = p_.N;
+        g.q = p_.q;
+        g.qKS = p_.qKS;
+        g.ctmod = p_.q;
+        g.factor = 1;
+        g.gbits = p_.gBits;
+        g.acc_io = result + off * 2 * p_.N;
+        // the DM op loop: each item's list is the one external product with its own key
+        FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_epk_, nullptr, d_epops_, d_epn_, 1, nullptr, nullptr,
+                                              nullptr, true, s));
+    }
+}
+
+size_t Engine::max_batch() const {
+    size_t fr = 0, tot = 0;
+    if (hipSetDevice(device_) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+    // workspace per gate: monomial indices / op list, ctExt, test-vector b, staged I/O
+    const size_t per = (size_t)p_.n * 2 + (size_t)maxops_ * 2 + ((size_t)p_.N + 1) * (wide_ ? 8 : 4) + 4 +
+                       (4 * ((size_t)p_.n + 1) + p_.N + 1) * 8;
+    return std::min<size_t>(0x7fffffffull, fr / 2 / per);
 }
 
 void Engine::eval_gate_multi_device(int gate, size_t count, uint32_t k, const uint64_t* const* a,

@@ -72,6 +72,19 @@ public:
     const uint32_t* ext_a() const { return d_ext_a_; }
     const uint32_t* ext_b() const { return d_ext_b_; }
 
+    // ---- the Backend seam (backend.h:131-192) ----
+    // BlindRotate[Batch] = EvalAcc (rgsw-acc-cggi.cpp:59-68 / rgsw-acc-lmkcdey.cpp:70-158 /
+    // rgsw-acc-dm.cpp:62-77): acc [count][2][N] (EVALUATION, canonical mod Q) in/out, a [count][n]
+    // mod ctmod (a power of two <= 2N; EvalAcc reads a_i with the ciphertext's modulus)
+    void blind_rotate_acc_device(size_t count, const uint64_t* a, uint32_t ctmod, uint64_t* acc, hipStream_t s);
+    // ExternalProduct[Batch] = AddToAccLMKCDEY / AddToAccDM (rgsw-acc-lmkcdey.cpp:228-254,
+    // rgsw-acc-dm.cpp:119-145): result[g] = rgsw[g] (x) rlwe[g]; rgsw [count][digitsG2][2][N] and
+    // rlwe / result [count][2][N], EVALUATION, canonical mod Q; result may alias rlwe
+    void external_product_device(size_t count, const uint64_t* rgsw, const uint64_t* rlwe, uint64_t* result,
+                                 hipStream_t s);
+    // upper bound on the batch one call can take on this device (Backend::MaxBatchSize)
+    size_t max_batch() const;
+
     // EvalBinGate(gate, ctvector) for AND3 / OR3 / AND4 / OR4 / MAJORITY (binfhe-base-scheme.cpp:129-171):
     // k inputs a[j] [count][n], b[j] [count] (mod q), plaintext modulus p of the inputs
     void eval_gate_multi_device(int gate, size_t count, uint32_t k, const uint64_t* const* a,
@@ -168,6 +181,11 @@ private:
     uint32_t* d_tv_ = nullptr;
     size_t fbcap_ = 0;
     uint64_t* d_fb_ = nullptr;
+    // ExternalProduct: packed per-item keys and one-op lists (grown on demand)
+    size_t epcap_ = 0;
+    uint32_t* d_epk_ = nullptr;
+    uint16_t* d_epops_ = nullptr;
+    uint32_t* d_epn_ = nullptr;
     // staging for host entry points: up to 4 inputs + one ctExt-sized output
     size_t hcap_ = 0;
     uint64_t* d_io_ = nullptr;

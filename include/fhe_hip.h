@@ -216,6 +216,31 @@ int fhe_hip_eval_decomp_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a,
 int fhe_hip_bootstrap_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b,
                                  uint32_t ctmod, const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out);
 
+/* ---- the reference GPU seam lux::fhe::backend::Backend (src/binfhe/include/backend/backend.h) ----
+ * Backend::BlindRotate / BlindRotateBatch (backend.h:131-136, 177-182) = the accumulator's EvalAcc
+ * (rgsw-acc-cggi.cpp:59-68, rgsw-acc-lmkcdey.cpp:70-158, rgsw-acc-dm.cpp:62-77) on `count` pairs:
+ * a[count][n] mod ctmod (the LWE ciphertext's modulus: a power of two <= 2N; 2N for LMKCDEY, q for
+ * AP), acc[count][2][N] in/out (RLWECiphertext elements 0 and 1, EVALUATION, bit-reversed as the
+ * reference stores them, canonical mod Q).  32-bit parameter sets (STD128, STD128_LMKCDEY, ...). */
+int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, uint64_t ctmod, uint64_t* acc);
+int fhe_hip_blind_rotate_acc_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, uint64_t ctmod,
+                                          uint64_t* d_acc, void* stream);
+/* Backend::ExternalProduct / ExternalProductBatch (backend.h:141-146, 187-192): RGSW x RLWE -> RLWE,
+ * result[g] = sum_d D_d(rlwe[g]) * rgsw[g][d] with D = SignedDigitDecompose (rgsw-acc.cpp:54-91) --
+ * AddToAccLMKCDEY / AddToAccDM (rgsw-acc-lmkcdey.cpp:228-254, rgsw-acc-dm.cpp:119-145) under the
+ * context's baseG.  rgsw[count][digitsG2][2][N] (RingGSWEvalKeyImpl rows, EVALUATION), rlwe and
+ * result [count][2][N] (EVALUATION), canonical mod Q; result may equal rlwe. */
+int fhe_hip_external_product_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* rgsw, const uint64_t* rlwe,
+                                   uint64_t* result);
+int fhe_hip_external_product_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_rgsw,
+                                          const uint64_t* d_rlwe, uint64_t* d_result, void* stream);
+/* Backend::MaxBatchSize (backend.h:86): gates one call can take given the device's free memory */
+int fhe_hip_max_batch_size(fhe_hip_ctx* ctx, size_t* max_count);
+/* Backend::UnpackBootstrappingKey (backend.h:229-233): packed keys (fhe_hip_pack_keys) back to the
+ * raw layouts; either key may be skipped (NULL) */
+int fhe_hip_unpack_keys(int paramset, int method, const uint8_t* bsk_packed, size_t bsk_size, uint64_t* bsk,
+                        const uint8_t* ksk_packed, size_t ksk_size, uint64_t* kskA, uint64_t* kskB);
+
 /* LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372): (N, qKS) -> (n, qKS) */
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
                             uint64_t* b_out);
@@ -268,6 +293,8 @@ int fhe_hip_copy_to_device(void* d_dst, const void* h_src, size_t bytes);
 int fhe_hip_copy_to_host(void* h_dst, const void* d_src, size_t bytes);
 int fhe_hip_synchronize(int device);
 int fhe_hip_device_count(int* count);
+/* Backend::DeviceMemory (backend.h:87): free / total bytes of the device (either may be NULL) */
+int fhe_hip_device_memory(int device, size_t* free_bytes, size_t* total_bytes);
 /* message of the last error on this host thread */
 const char* fhe_hip_last_error(void);
 

@@ -1,0 +1,338 @@
+// bh_driver.cpp -- TEST INFRASTRUCTURE ONLY: extern "C" hooks that register our BackendHIP
+// (integration/backend_hip.cpp) in the REFERENCE's own BackendRegistry (backend.cpp:241-305) and
+// run each seam operation both through the registered backend (on the GPU) and through the
+// reference's CPU path on the same objects, for tests/test_backend.py.  Linked with the reference
+// sources into oracle/_ref/libbackend_hip.so by oracle/Makefile; never part of fhe_amd.
+//
+// Reference side of each comparison:
+//   BlindRotateBatch     RingGSWAccumulator{CGGI,LMKCDEY,DM}::EvalAcc (rgsw-acc-cggi.cpp:59-68,
+//                        rgsw-acc-lmkcdey.cpp:70-158, rgsw-acc-dm.cpp:62-77)
+//   ExternalProductBatch AddToAccLMKCDEY (rgsw-acc-lmkcdey.cpp:228-254, private) restated with the
+//                        public SignedDigitDecompose (rgsw-acc.cpp:54-91) and NativePoly products
+//   KeySwitchBatch       LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372)
+//   ModSwitchBatch       LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:254-261)
+//   EvalBinGateBatch     lux::fhe::EvalBinGateBatch (batch/batch.cpp:176-210)
+#include <omp.h>
+
+#include <cstdint>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <vector>
+
+#include "backend_hip.h"
+#include "batch/binfhe-batch.h"
+#include "rgsw-acc-cggi.h"
+#include "rgsw-acc-dm.h"
+#include "rgsw-acc-lmkcdey.h"
+
+using namespace lux::fhe;
+using namespace lux::fhe::backend;
+
+extern "C" void* ref_ctx_context(void* h);  // ref_driver.cpp
+
+namespace {
+
+thread_local std::string g_err;
+BackendHIP* g_be = nullptr;  // owned by the registry
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return 0;
+    }
+    catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+    catch (...) {
+        g_err = "unknown exception";
+        return -1;
+    }
+}
+
+BinFHEContext& CC(void* h) {
+    return *static_cast<BinFHEContext*>(ref_ctx_context(h));
+}
+
+NativeVector vec_from(const uint64_t* p, uint32_t len, const NativeInteger& mod) {
+    NativeVector v(len, mod);
+    for (uint32_t i = 0; i < len; ++i)
+        v[i] = NativeInteger(p[i]);
+    return v;
+}
+
+NativePoly poly_from(const std::shared_ptr<ILNativeParams>& pp, const uint64_t* src, uint32_t N,
+                     const NativeInteger& Q) {
+    NativePoly poly(pp, Format::EVALUATION, true);
+    poly.SetValues(vec_from(src, N, Q), Format::EVALUATION);
+    return poly;
+}
+
+void poly_out(const NativePoly& p, uint64_t* dst) {
+    const auto& v = p.GetValues();
+    for (uint32_t i = 0; i < v.GetLength(); ++i)
+        dst[i] = v[i].ConvertToInt();
+}
+
+RLWECiphertext rlwe_from(const std::shared_ptr<ILNativeParams>& pp, const uint64_t* src, uint32_t N,
+                         const NativeInteger& Q) {
+    std::vector<NativePoly> el{poly_from(pp, src, N, Q), poly_from(pp, src + N, N, Q)};
+    return std::make_shared<RLWECiphertextImpl>(std::move(el));
+}
+
+void rlwe_out(const RLWECiphertext& c, uint64_t* dst, uint32_t N) {
+    poly_out(c->GetElements()[0], dst);
+    poly_out(c->GetElements()[1], dst + N);
+}
+
+std::vector<LWECiphertext> lwe_vec(const uint64_t* a, const uint64_t* b, size_t count, uint32_t len, uint64_t mod) {
+    std::vector<LWECiphertext> v(count);
+    for (size_t g = 0; g < count; ++g)
+        v[g] = std::make_shared<LWECiphertextImpl>(vec_from(a + g * len, len, NativeInteger(mod)),
+                                                   NativeInteger(b ? b[g] : 0));
+    return v;
+}
+
+void lwe_out(const std::vector<LWECiphertext>& v, uint64_t* a, uint64_t* b) {
+    for (size_t g = 0; g < v.size(); ++g) {
+        const uint32_t len = v[g]->GetLength();
+        for (uint32_t i = 0; i < len; ++i)
+            a[g * len + i] = v[g]->GetA()[i].ConvertToInt();
+        b[g] = v[g]->GetB().ConvertToInt();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bh_last_error() {
+    return g_err.c_str();
+}
+
+// BackendRegistry::Instance().Register(BackendHIP) + SetDefault, for the context's parameter set
+int bh_register(int paramset, int method, int device) {
+    return guarded([&] {
+        auto be = std::make_unique<BackendHIP>(static_cast<BINFHE_PARAMSET>(paramset),
+                                               static_cast<BINFHE_METHOD>(method), device);
+        g_be = be.get();
+        BackendRegistry::Instance().Register(std::move(be));
+        BackendRegistry::Instance().SetDefault(kBackendHIP);
+        if (CurrentBackend() != g_be)
+            throw std::runtime_error("registry does not return the registered backend");
+    });
+}
+
+// releases the device context before static destruction; the default goes back to CPU
+int bh_unregister() {
+    return guarded([&] {
+        if (g_be)
+            g_be->Release();
+        BackendRegistry::Instance().SetDefault(BackendType::CPU);
+    });
+}
+
+// out: Type, IsAvailable, MaxBatchSize, DeviceMemory, registry IsAvailable(kBackendHIP); name
+int bh_info(uint64_t* out, char* name, size_t cap) {
+    return guarded([&] {
+        Backend* be = BackendRegistry::Instance().Get(kBackendHIP);
+        if (!be)
+            throw std::runtime_error("not registered");
+        out[0] = static_cast<uint64_t>(be->Type());
+        out[1] = be->IsAvailable();
+        out[2] = be->MaxBatchSize();
+        out[3] = be->DeviceMemory();
+        out[4] = BackendRegistry::Instance().IsAvailable(kBackendHIP);
+        std::strncpy(name, be->Name().c_str(), cap - 1);
+        name[cap - 1] = 0;
+    });
+}
+
+// Allocate / CopyToDevice / CopyToHost / Synchronize / Free through CurrentBackend()
+int bh_memory_roundtrip(const uint8_t* src, size_t bytes, uint8_t* back) {
+    return guarded([&] {
+        Backend* be   = CurrentBackend();
+        DeviceBuffer d = be->Allocate(bytes);
+        if (!d.IsValid() || !d.IsDevice())
+            throw std::runtime_error("Allocate returned no device buffer");
+        be->CopyToDevice(src, d, bytes);
+        be->Synchronize();
+        be->CopyToHost(d, back, bytes);
+        be->Free(d);
+        if (d.ptr)
+            throw std::runtime_error("Free left the pointer set");
+    });
+}
+
+// BlindRotateBatch through CurrentBackend() vs EvalAcc on the CPU; keys = the ones BTKeyLoad put in
+// the reference context (ref_load_keys / ref_keygen)
+int bh_blind_rotate(void* h, size_t count, const uint64_t* a, uint64_t ctmod, const uint64_t* acc_in,
+                    uint64_t* acc_gpu, uint64_t* acc_ref, int nthreads) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto rg           = cc.GetParams()->GetRingGSWParams();
+        const uint32_t n = cc.GetParams()->GetLWEParams()->Getn(), N = rg->GetN();
+        const NativeInteger Q = rg->GetQ();
+        const auto pp         = rg->GetPolyParams();
+        const auto& ek        = cc.GetRefreshKey();
+        auto cts              = lwe_vec(a, nullptr, count, n, ctmod);
+        std::vector<RLWECiphertext> accs(count);
+        for (size_t g = 0; g < count; ++g)
+            accs[g] = rlwe_from(pp, acc_in + g * 2 * N, N, Q);
+        CurrentBackend()->BlindRotateBatch(rg, cts, ek, accs);
+        for (size_t g = 0; g < count; ++g)
+            rlwe_out(accs[g], acc_gpu + g * 2 * N, N);
+        std::string err;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : omp_get_max_threads()) schedule(dynamic)
+        for (size_t g = 0; g < count; ++g) {
+            try {
+                auto acc = rlwe_from(pp, acc_in + g * 2 * N, N, Q);
+                const NativeVector& av = cts[g]->GetA();
+                switch (rg->GetMethod()) {
+                    case GINX: RingGSWAccumulatorCGGI().EvalAcc(rg, ek, acc, av); break;
+                    case LMKCDEY: RingGSWAccumulatorLMKCDEY().EvalAcc(rg, ek, acc, av); break;
+                    default: RingGSWAccumulatorDM().EvalAcc(rg, ek, acc, av); break;
+                }
+                rlwe_out(acc, acc_ref + g * 2 * N, N);
+            }
+            catch (const std::exception& e) {
+#pragma omp critical
+                err = e.what();
+            }
+        }
+        if (!err.empty())
+            throw std::runtime_error(err);
+    });
+}
+
+// ExternalProductBatch through CurrentBackend() vs AddToAccLMKCDEY restated with public pieces
+int bh_external_product(void* h, size_t count, const uint64_t* rgsw, const uint64_t* rlwe, uint64_t* out_gpu,
+                        uint64_t* out_ref) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto rg           = cc.GetParams()->GetRingGSWParams();
+        const uint32_t N = rg->GetN(), dG2 = 2 * (rg->GetDigitsG() - 1);
+        const NativeInteger Q = rg->GetQ();
+        const auto pp         = rg->GetPolyParams();
+        const size_t kw       = (size_t)dG2 * 2 * N;
+        std::vector<RingGSWEvalKey> keys(count);
+        std::vector<RLWECiphertext> cts(count), res;
+        for (size_t g = 0; g < count; ++g) {
+            std::vector<std::vector<NativePoly>> el(dG2, std::vector<NativePoly>(2));
+            for (uint32_t d = 0; d < dG2; ++d)
+                for (uint32_t c = 0; c < 2; ++c)
+                    el[d][c] = poly_from(pp, rgsw + g * kw + ((size_t)d * 2 + c) * N, N, Q);
+            keys[g] = std::make_shared<RingGSWEvalKeyImpl>(el);
+            cts[g]  = rlwe_from(pp, rlwe + g * 2 * N, N, Q);
+        }
+        CurrentBackend()->ExternalProductBatch(rg, keys, cts, res);
+        for (size_t g = 0; g < count; ++g)
+            rlwe_out(res[g], out_gpu + g * 2 * N, N);
+        const RingGSWAccumulatorLMKCDEY scheme;
+        for (size_t g = 0; g < count; ++g) {  // rgsw-acc-lmkcdey.cpp:228-254
+            std::vector<NativePoly> ct(cts[g]->GetElements());
+            ct[0].SetFormat(Format::COEFFICIENT);
+            ct[1].SetFormat(Format::COEFFICIENT);
+            std::vector<NativePoly> dct(dG2, NativePoly(pp, Format::COEFFICIENT, true));
+            scheme.SignedDigitDecompose(rg, ct, dct);
+            for (uint32_t d = 0; d < dG2; ++d)
+                dct[d].SetFormat(Format::EVALUATION);
+            const auto& ev = keys[g]->GetElements();
+            NativePoly r0  = dct[0] * ev[0][0];
+            for (uint32_t d = 1; d < dG2; ++d)
+                r0 += dct[d] * ev[d][0];
+            NativePoly r1 = dct[0] * ev[0][1];
+            for (uint32_t d = 1; d < dG2; ++d)
+                r1 += dct[d] * ev[d][1];
+            poly_out(r0, out_ref + g * 2 * N);
+            poly_out(r1, out_ref + g * 2 * N + N);
+        }
+    });
+}
+
+// KeySwitchBatch (inputs mod qKS, dimension N) vs LWEEncryptionScheme::KeySwitch
+int bh_keyswitch(void* h, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* ga, uint64_t* gb,
+                 uint64_t* ra, uint64_t* rb) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        auto cts          = lwe_vec(a, b, count, lp->GetN(), lp->GetqKS().ConvertToInt());
+        std::vector<LWECiphertext> out;
+        CurrentBackend()->KeySwitchBatch(lp, cts, cc.GetSwitchKey(), out);
+        lwe_out(out, ga, gb);
+        std::vector<LWECiphertext> ref(count);
+        const LWEEncryptionScheme lwe;
+#pragma omp parallel for
+        for (size_t g = 0; g < count; ++g)
+            ref[g] = lwe.KeySwitch(lp, cc.GetSwitchKey(), cts[g]);
+        lwe_out(ref, ra, rb);
+    });
+}
+
+// ModSwitchBatch (inputs mod `mod` = Q or qKS) vs LWEEncryptionScheme::ModSwitch to the next modulus
+int bh_modswitch(void* h, size_t count, uint32_t len, uint64_t mod, const uint64_t* a, const uint64_t* b,
+                 uint64_t* ga, uint64_t* gb, uint64_t* ra, uint64_t* rb, uint64_t* mod_out) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        auto cts          = lwe_vec(a, b, count, len, mod);
+        std::vector<LWECiphertext> out;
+        CurrentBackend()->ModSwitchBatch(lp, cts, out);
+        lwe_out(out, ga, gb);
+        *mod_out = count ? out[0]->GetModulus().ConvertToInt() : 0;
+        const NativeInteger to = mod == lp->GetQ().ConvertToInt() ? lp->GetqKS() : lp->Getq();
+        const LWEEncryptionScheme lwe;
+        std::vector<LWECiphertext> ref(count);
+        for (size_t g = 0; g < count; ++g)
+            ref[g] = lwe.ModSwitch(to, cts[g]);
+        lwe_out(ref, ra, rb);
+    });
+}
+
+// the backend's fused gate path vs the reference's EvalBinGateBatch (OpenMP over EvalBinGate)
+int bh_eval_gates(void* h, int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
+                  const uint64_t* b2, uint64_t* ga, uint64_t* gb, uint64_t* ra, uint64_t* rb) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        const uint64_t q  = lp->Getq().ConvertToInt();
+        auto c1 = lwe_vec(a1, b1, count, lp->Getn(), q), c2 = lwe_vec(a2, b2, count, lp->Getn(), q);
+        RingGSWBTKey keys;
+        keys.BSkey = cc.GetRefreshKey();
+        keys.KSkey = cc.GetSwitchKey();
+        std::vector<LWECiphertext> out, ref;
+        g_be->EvalBinGateBatch(static_cast<BINGATE>(gate), keys, c1, c2, out);
+        lwe_out(out, ga, gb);
+        BatchResult r = EvalBinGateBatch(cc, static_cast<BINGATE>(gate), c1, c2, ref, 0);
+        if (!r.success)
+            throw std::runtime_error("reference EvalBinGateBatch: " + r.error);
+        lwe_out(ref, ra, rb);
+    });
+}
+
+// PackCiphertexts -> UnpackCiphertexts and PackBootstrappingKey -> UnpackBootstrappingKey round trips
+// through device memory; *ok bit 0: ciphertexts equal, bit 1: key equal to the context's refresh key
+int bh_pack_roundtrip(void* h, size_t count, const uint64_t* a, const uint64_t* b, int* ok) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        Backend* be       = CurrentBackend();
+        auto cts          = lwe_vec(a, b, count, lp->Getn(), lp->Getq().ConvertToInt());
+        DeviceBuffer pc = be->PackCiphertexts(cts);
+        std::vector<LWECiphertext> back;
+        be->UnpackCiphertexts(pc, back);
+        be->Free(pc);
+        bool same = back.size() == cts.size();
+        for (size_t g = 0; same && g < count; ++g)
+            same = *back[g] == *cts[g];
+        DeviceBuffer pk = be->PackBootstrappingKey(cc.GetRefreshKey());
+        RingGSWACCKey ek;
+        be->UnpackBootstrappingKey(pk, ek);
+        be->Free(pk);
+        *ok = (same ? 1 : 0) | (*ek == *cc.GetRefreshKey() ? 2 : 0);
+    });
+}
+
+}  // extern "C"

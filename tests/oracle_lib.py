@@ -14,6 +14,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libfhe_ref.so")
 RESTATE_SO = os.path.join(ROOT, "oracle", "_ref", "libtfhe_oracle.so")
+# the reference + our BackendHIP (integration/backend_hip.cpp) registered in its BackendRegistry
+BACKEND_SO = os.path.join(ROOT, "oracle", "_ref", "libbackend_hip.so")
 
 u64p = ctypes.POINTER(ctypes.c_uint64)
 vp = ctypes.c_void_p
@@ -117,9 +119,13 @@ def restatement_available():
     return os.path.exists(RESTATE_SO)
 
 
+def backend_available():
+    return os.path.exists(BACKEND_SO)
+
+
 class Ref:
-    def __init__(self, paramset, method):
-        self.L = ctypes.CDLL(REF_SO)
+    def __init__(self, paramset, method, so=REF_SO):
+        self.L = ctypes.CDLL(so)
         L = self.L
         L.ref_ctx_create.restype = vp
         L.ref_ctx_create.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -138,6 +144,7 @@ class Ref:
             self._chk(L.ref_ctx_info(self.h, _p(info)))
             (self.n, self.N, self.q, self.Q, self.qKS, self.baseKS, self.digitsKS, self.baseG,
              self.digitsG, self.psi, self.numAutoKeys, self.keyDist) = [int(x) for x in info]
+            self.method_is_ginx = method == GINX
 
     def err(self):
         return self.L.ref_last_error().decode()

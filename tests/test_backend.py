@@ -1,0 +1,239 @@
+"""The drop-in boundary as the reference sees it: our BackendHIP (integration/backend_hip.cpp), built
+against the reference's own backend.h (oracle/Makefile -> oracle/_ref/libbackend_hip.so), is
+registered in the reference's BackendRegistry and every seam operation is run through
+CurrentBackend() on the GPU and through the reference's CPU path on the same objects
+(oracle/bh_driver.cpp):
+
+  BlindRotateBatch      vs RingGSWAccumulator{CGGI,LMKCDEY}::EvalAcc on arbitrary accumulators
+  ExternalProductBatch  vs AddToAccLMKCDEY (SignedDigitDecompose + NativePoly products)
+  KeySwitchBatch        vs LWEEncryptionScheme::KeySwitch
+  ModSwitchBatch        vs LWEEncryptionScheme::ModSwitch (Q -> qKS, qKS -> q)
+  EvalBinGateBatch      vs lux::fhe::EvalBinGateBatch (batch.cpp)
+  Pack/Unpack{BootstrappingKey,Ciphertexts}, memory calls, info calls.
+Keys: our seeded keys (as the goldens use) and, for GINX, keys the reference generated itself."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle_lib import BACKEND_SO, Ref, backend_available
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "fhe_amd", "libfhe_amd.so")
+vp = ctypes.c_void_p
+sz = ctypes.c_size_t
+u64 = ctypes.c_uint64
+STD128, STD128_LMKCDEY, GINX, LMKCDEY = 3, 21, 2, 3
+BH = ["bh_register", "bh_unregister", "bh_info", "bh_memory_roundtrip", "bh_blind_rotate", "bh_external_product",
+      "bh_keyswitch", "bh_modswitch", "bh_eval_gates", "bh_pack_roundtrip", "bh_last_error"]
+
+needs_backend = pytest.mark.skipif(not backend_available(), reason="oracle/_ref/libbackend_hip.so not built")
+
+
+def P(a):
+    assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return a.ctypes.data_as(vp)
+
+
+def dyn_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def undefined_symbols(path):
+    out = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+# ----------------------------------------------------------------- CPU ----
+def test_product_library_links_nothing_from_the_reference():
+    """libfhe_amd.so neither needs nor defines any reference (lux::fhe) symbol"""
+    needed = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True, check=True).stdout
+    assert "fhe_ref" not in needed and "backend_hip" not in needed
+    assert not [s for s in dyn_symbols(LIB) | undefined_symbols(LIB) if "3lux3fhe" in s]
+
+
+@needs_backend
+def test_backend_library_exports_and_binds_through_the_c_abi():
+    syms = dyn_symbols(BACKEND_SO)
+    assert all(s in syms for s in BH)
+    # BackendHIP reaches libfhe_amd only through the C-ABI of include/fhe_hip.h
+    used = {s for s in undefined_symbols(BACKEND_SO) if s.startswith("fhe_hip_")}
+    hdr = open(os.path.join(ROOT, "include", "fhe_hip.h")).read()
+    assert used and all(s + "(" in hdr for s in used), used
+    # every pure virtual of backend.h is overridden (the class compiled as concrete: it is instantiated)
+    src = open(os.path.join(ROOT, "integration", "backend_hip.h")).read()
+    for m in ("Type", "Name", "IsAvailable", "MaxBatchSize", "DeviceMemory", "Allocate", "Free", "CopyToDevice",
+              "CopyToHost", "Synchronize", "BlindRotate", "ExternalProduct", "KeySwitch", "ModSwitch",
+              "BlindRotateBatch", "ExternalProductBatch", "KeySwitchBatch", "ModSwitchBatch", "PackBootstrappingKey",
+              "UnpackBootstrappingKey", "PackCiphertexts", "UnpackCiphertexts"):
+        assert f" {m}(" in src and "override" in src.split(f" {m}(")[1].split(";")[0], m
+
+
+# ----------------------------------------------------------------- GPU ----
+class Backend:
+    """ctypes view of oracle/_ref/libbackend_hip.so for one parameter set"""
+
+    def __init__(self, paramset, method, keys=None):
+        self.ref = Ref(paramset, method, so=BACKEND_SO)
+        self.L = self.ref.L
+        self.L.bh_last_error.restype = ctypes.c_char_p
+        self.ps, self.m = paramset, method
+        if keys is None:     # the reference's own key generation
+            self.sk, bsk, A, B = self.ref.keygen()
+            self.ref.load_keys(bsk, A, B)
+        else:
+            self.sk = keys.sk
+            self.ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        self.chk(self.L.bh_register(paramset, method, 0))
+
+    def chk(self, rc):
+        if rc != 0:
+            raise RuntimeError("bh: " + self.L.bh_last_error().decode())
+
+    def close(self):
+        self.chk(self.L.bh_unregister())
+
+    @property
+    def h(self):
+        return self.ref.h
+
+
+_backends = {}
+
+
+def backend(name):
+    from fhe_amd import binfhe as bf
+    if name not in _backends:
+        for b in _backends.values():
+            b.close()
+        _backends.clear()
+        ps, m = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "std128_refkeys": (STD128, GINX)}[name]
+        keys = None if name.endswith("refkeys") else bf.keygen(ps, m, 0xB0070000 + ps)
+        _backends[name] = Backend(ps, m, keys)
+    return _backends[name]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _release():
+    yield
+    for b in _backends.values():
+        b.close()
+    _backends.clear()
+
+
+SETS = ["std128", "lmkcdey", "std128_refkeys"]
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("name", SETS[:2])
+def test_gpu_backend_registered_info_and_memory(name):
+    b = backend(name)
+    out = np.zeros(5, np.uint64)
+    buf = ctypes.create_string_buffer(256)
+    b.chk(b.L.bh_info(P(out), buf, sz(256)))
+    assert out[0] == 4 and out[1] == 1 and out[4] == 1       # kBackendHIP, available, in the registry
+    assert out[2] >= 65536 and out[3] > 100e9                 # MaxBatchSize, DeviceMemory (bytes)
+    assert b"HIP" in buf.value
+    src = np.random.default_rng(3).integers(0, 256, 1 << 20, dtype=np.uint8)
+    back = np.zeros_like(src)
+    b.chk(b.L.bh_memory_roundtrip(src.ctypes.data_as(vp), sz(src.size), back.ctypes.data_as(vp)))
+    assert np.array_equal(src, back)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_backend_blind_rotate_equals_evalacc(name):
+    """BlindRotateBatch on arbitrary accumulators (uniform mod Q, EVALUATION) and ragged counts"""
+    b = backend(name)
+    r = b.ref
+    rng = np.random.default_rng(11)
+    mods = [r.q, 2 * r.N] if r.method_is_ginx else [2 * r.N]
+    for ctmod in mods:
+        for count in (1, 6):
+            a = rng.integers(0, ctmod, (count, r.n), dtype=np.uint64)
+            acc = rng.integers(0, r.Q, (count, 2, r.N), dtype=np.uint64)
+            g, ref = np.zeros_like(acc), np.zeros_like(acc)
+            b.chk(b.L.bh_blind_rotate(b.h, sz(count), P(a), u64(ctmod), P(acc), P(g), P(ref), 0))
+            assert np.array_equal(g, ref), (name, ctmod, count)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("name", SETS[:2])
+def test_gpu_backend_external_product_equals_reference(name):
+    b = backend(name)
+    r = b.ref
+    rng = np.random.default_rng(12)
+    dG2 = 2 * (r.digitsG - 1)
+    for count in (1, 7):
+        rgsw = rng.integers(0, r.Q, (count, dG2, 2, r.N), dtype=np.uint64)
+        rlwe = rng.integers(0, r.Q, (count, 2, r.N), dtype=np.uint64)
+        g, ref = np.zeros_like(rlwe), np.zeros_like(rlwe)
+        b.chk(b.L.bh_external_product(b.h, sz(count), P(rgsw), P(rlwe), P(g), P(ref)))
+        assert np.array_equal(g, ref), (name, count)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_backend_keyswitch_and_modswitch_equal_reference(name):
+    b = backend(name)
+    r = b.ref
+    rng = np.random.default_rng(13)
+    count = 9
+    a = rng.integers(0, r.qKS, (count, r.N), dtype=np.uint64)
+    bb = rng.integers(0, r.qKS, count, dtype=np.uint64)
+    ga, gb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+    ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+    b.chk(b.L.bh_keyswitch(b.h, sz(count), P(a), P(bb), P(ga), P(gb), P(ra), P(rb)))
+    assert np.array_equal(ga, ra) and np.array_equal(gb, rb)
+    for mod, ln, to in ((r.Q, r.N, r.qKS), (r.qKS, r.n, r.q)):
+        a = rng.integers(0, mod, (count, ln), dtype=np.uint64)
+        bb = rng.integers(0, mod, count, dtype=np.uint64)
+        ga, gb = np.zeros_like(a), np.zeros_like(bb)
+        ra, rb = np.zeros_like(a), np.zeros_like(bb)
+        mo = ctypes.c_uint64()
+        b.chk(b.L.bh_modswitch(b.h, sz(count), ctypes.c_uint32(ln), u64(mod), P(a), P(bb), P(ga), P(gb), P(ra),
+                               P(rb), ctypes.byref(mo)))
+        assert mo.value == to
+        assert np.array_equal(ga, ra) and np.array_equal(gb, rb), (mod, to)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_backend_gate_batch_equals_reference_evalbingatebatch(name):
+    from fhe_amd import binfhe as bf
+    b = backend(name)
+    r = b.ref
+    count = 12
+    rng = np.random.default_rng(14)
+    x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+    a1, b1 = bf.encrypt(b.ps, b.m, b.sk, x1, 501)
+    a2, b2 = bf.encrypt(b.ps, b.m, b.sk, x2, 502)
+    for gate, truth in ((1, x1 & x2), (4, x1 ^ x2), (3, 1 - (x1 & x2))):
+        ga, gb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+        ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+        b.chk(b.L.bh_eval_gates(b.h, gate, sz(count), P(a1), P(b1), P(a2), P(b2), P(ga), P(gb), P(ra), P(rb)))
+        assert np.array_equal(ga, ra) and np.array_equal(gb, rb), gate
+        assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), truth), gate
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("name", SETS[:2])
+def test_gpu_backend_pack_roundtrips(name):
+    b = backend(name)
+    r = b.ref
+    rng = np.random.default_rng(15)
+    count = 33
+    a = rng.integers(0, r.q, (count, r.n), dtype=np.uint64)
+    bb = rng.integers(0, r.q, count, dtype=np.uint64)
+    ok = ctypes.c_int()
+    b.chk(b.L.bh_pack_roundtrip(b.h, sz(count), P(a), P(bb), ctypes.byref(ok)))
+    assert ok.value == 3, ok.value
