@@ -421,8 +421,8 @@ void BackendHIP::UnpackBootstrappingKey(const DeviceBuffer& packed, RingGSWACCKe
         ek = std::make_shared<RingGSWACCKeyImpl>(1, 2, n);
         for (uint32_t i = 0; i < n; ++i)
             (*ek)[0][0][i] = rgsw_from(pp, raw.data() + (size_t)i * rgsw, dG2, N, Q);
+        // (*ek)[0][1] keeps n slots with the first numAutoKeys + 1 used (rgsw-acc-lmkcdey.cpp:51-67)
         const size_t arow = (size_t)(p_.digitsG - 1) * 2 * N;
-        (*ek)[0][1].resize(p_.numAutoKeys + 1);
         for (uint32_t k = 0; k <= p_.numAutoKeys; ++k)
             (*ek)[0][1][k] = rgsw_from(pp, raw.data() + (size_t)n * rgsw + k * arow, p_.digitsG - 1, N, Q);
     }
