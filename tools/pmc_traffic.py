@@ -27,8 +27,19 @@ def per_kernel(pas, counter):
 
 
 def short(name):
-    m = re.search(r"(k_[a-z0-9_]+)(<[^>(]*>)?", name)
-    return (m.group(1) + (m.group(2) or "")) if m else name[:40]
+    """the names bench.py reports: k_blind_rotate_ginx, k_ntt1024w<fwd, SignedA>, k_ntt1024<uint64_t, inv>, ..."""
+    m = re.search(r"(k_[a-z0-9_]+)", name)
+    if not m:
+        return name[:40]
+    base = m.group(1)
+    if base.startswith("k_ntt1024"):
+        args = name[name.index(base) + len(base):].split("(")[0] + name.split(">(")[0]
+        inv = "inv" if re.search(r"<\s*(unsigned long, )?true", name) else "fwd"
+        if base == "k_ntt1024w":
+            arith = "SignedA" if "SignedA" in name else "ShoupA"
+            return f"k_ntt1024w<{inv}, {arith}>"
+        return f"k_ntt1024<{'uint64_t' if 'unsigned long,' in name else 'uint32_t'}, {inv}>"
+    return base
 
 
 fetch, write = per_kernel("p3", "FETCH_SIZE"), per_kernel("p4", "WRITE_SIZE")
@@ -46,8 +57,7 @@ for k in fetch:
     f = sum(fetch[k]) / len(fetch[k])
     w = sum(write.get(k, [0])) / max(1, len(write.get(k, [0])))
     key = short(k)
-    base = re.sub(r"<.*", "", key)
-    out["kernels"][base if base not in out["kernels"] else key] = {
+    out["kernels"][key] = {
         "kernel": key, "batch": NTT_POLYS if "ntt" in key else batch, "launches": len(fetch[k]),
         "fetch_kib": round(f, 1), "write_kib": round(w, 1),
         "hbm_bytes_per_launch": round(2 * f * 1024 + w * 1024)}

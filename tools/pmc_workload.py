@@ -1,5 +1,6 @@
-"""GPU workload for rocprofv3 --pmc passes: one STD128 GINX gate batch, one LMKCDEY
-batch and a 4096-polynomial NTT pass (device-resident)."""
+"""GPU workload for rocprofv3 --pmc passes (tools/pmc_run.sh): one STD128 GINX and one
+STD128_LMKCDEY AND batch of B gates (device-resident, as bench.py runs them), and 4096-polynomial
+forward + inverse NTT passes for the STD128 modulus (k_ntt1024w) and the 60-bit prime (k_ntt1024<u64>)."""
 import ctypes
 import sys
 
@@ -10,7 +11,7 @@ from fhe_amd import NttPlan  # noqa: E402
 from fhe_amd import binfhe as bf  # noqa: E402
 from fhe_amd._lib import check, lib, ptr, vp  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 
 
 def dalloc(x):
@@ -34,11 +35,13 @@ for ps, m in ((bf.STD128, bf.GINX), (bf.STD128_LMKCDEY, bf.LMKCDEY)):
     check(lib().fhe_hip_synchronize(0))
     e.close()
 
-Q = 134215681
-plan = NttPlan(Q)
-xs = np.random.default_rng(2).integers(0, Q, size=(4096, 1024), dtype=np.uint64)
-dx = dalloc(xs)
-for _ in range(3):
-    plan.run_device(dx, dx, 4096, False)
-check(lib().fhe_hip_synchronize(0))
+for Q in (134215681, 1152921504606830593):
+    plan = NttPlan(Q)
+    xs = np.random.default_rng(2).integers(0, Q, size=(4096, 1024), dtype=np.uint64)
+    dx = dalloc(xs)
+    for inv in (False, True):
+        for _ in range(3):
+            plan.run_device(dx, dx, 4096, inv)
+    check(lib().fhe_hip_synchronize(0))
+    plan.close()
 print("pmc workload done")
