@@ -63,6 +63,10 @@ __host__ __device__ constexpr size_t ginx_u4_off(uint32_t ks, uint32_t d, uint32
     return (((size_t)d * 16 + k) * 64 + lane) * 4 + ks * 2 + e;
 }
 
+// u16 key-switching-key rows: A[n] then B at column n, zero-padded to 512 columns (n < 512, both
+// STD128 sets) or 1024 (n < 1024: STD128_3, LPF_STD128, ...)
+__host__ __device__ constexpr uint32_t ksk_width(uint32_t n) { return n < 512 ? 512u : 1024u; }
+
 struct GateArgs {
     uint32_t count, n, N, q, qKS;
     uint32_t ctmod;                   // modulus of the bootstrapped ct's a (q; 2q for BootstrapFunc), power of 2

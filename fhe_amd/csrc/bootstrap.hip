@@ -506,6 +506,14 @@ FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
 // the same register of the other half-wave (lane ^ 32), through the LDS crossbar (no VALU)
 FHE_DEV uint32_t other_half(uint32_t x, int xaddr) { return (uint32_t)__builtin_amdgcn_ds_bpermute(xaddr, (int)x); }
 
+// key vector load; FHE_ABL & 64 (timing ablation, wrong results): every key index folded to key 0,
+// the same instructions always hitting in cache, to measure what key cache misses cost
+#if defined(FHE_ABL) && (FHE_ABL & 64)
+#define FHE_KEY_INDEX(x) ((x) * 0)
+#else
+#define FHE_KEY_INDEX(x) (x)
+#endif
+FHE_DEV uint4 kload(const uint4* p, size_t i) { return p[i]; }
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 
 // SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = 3: centre x in [0, Q) to
@@ -739,12 +747,12 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         const uint32_t Pn = gl + (gl >> 5);                    // index eper - el - 64k -> Pn - 66k
 #if FHE_GINX_U4
         // one 16-byte vector per digit row and slot pair: (K+[2k], K+[2k+1], K-[2k], K-[2k+1])
-        const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)i * (4 * 16 * 64);
+        const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)FHE_KEY_INDEX(i) * (4 * 16 * 64);
         uint4 kq[FHE_KEY_PF + 1][4];
 #pragma unroll
         for (int k = 0; k < FHE_KEY_PF; ++k)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) kq[k][d] = kb4[(d * 16 + k) * 64 + lofs];
+            for (int d = 0; d < 4; ++d) kq[k][d] = kload(kb4, (d * 16 + k) * 64 + lofs);
 #if FHE_MAC_PIPE
         // the other half's digits (ds_bpermute) and the monomial pairs of slot pair k + 1 are
         // requested before slot pair k is consumed (LDS latency off the critical path)
@@ -772,7 +780,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         for (int k = 0; k < 16; ++k) {
             if (k + FHE_KEY_PF < 16) {
 #pragma unroll
-                for (int d = 0; d < 4; ++d) kq[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d] = kb4[(d * 16 + k + FHE_KEY_PF) * 64 + lofs];
+                for (int d = 0; d < 4; ++d) kq[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d] = kload(kb4, (d * 16 + k + FHE_KEY_PF) * 64 + lofs);
             }
 #if FHE_MAC_PIPE
             if (k + 1 < 16) issue(k + 1, (k + 1) & 1);
@@ -1205,10 +1213,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             fwd_pass2<FM, !DM && FHE_LMK_TWPRE>(dA, dB, tile, l, twAf, s_twBf, m);
 #if FHE_ROW_U4
             // one 16-byte vector per digit row and 4 slots (boot.h row_off)
-            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)op * (4 * 8 * 64);
+            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)FHE_KEY_INDEX(op) * (4 * 8 * 64);
             uint4 kq[2][4];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) kq[0][d] = kb4[(d * 8 + 0) * 64 + lane];
+            for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
             // LMKCDEY: the other half's digits of slots 4(kk+1).. requested before 4kk.. are consumed
             constexpr bool PIPE = !DM && FHE_LMK_PIPE;
             uint32_t xq[2][8];
@@ -1224,7 +1232,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             for (int kk = 0; kk < 8; ++kk) {
                 if (kk + 1 < 8) {  // request slots 4(kk+1).. while 4kk.. are consumed
 #pragma unroll
-                    for (int d = 0; d < 4; ++d) kq[(kk + 1) & 1][d] = kb4[(d * 8 + kk + 1) * 64 + lane];
+                    for (int d = 0; d < 4; ++d) kq[(kk + 1) & 1][d] = kload(kb4, (d * 8 + kk + 1) * 64 + lane);
                     if (PIPE) issue(kk + 1, (kk + 1) & 1);
                 }
                 asm volatile("" ::: "memory");
@@ -1324,10 +1332,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #endif
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
 #if FHE_ROW_U4
-            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
+            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)FHE_KEY_INDEX(t) * (2 * 8 * 64);
             uint4 ka[2][2];
-            ka[0][0] = kb4[(0 * 8 + 0) * 64 + lane];
-            ka[0][1] = kb4[(1 * 8 + 0) * 64 + lane];
+            ka[0][0] = kload(kb4, (0 * 8 + 0) * 64 + lane);
+            ka[0][1] = kload(kb4, (1 * 8 + 0) * 64 + lane);
             uint32_t xa[2][4];
             auto issue = [&](int kk, int b) {
 #pragma unroll
@@ -1337,8 +1345,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #pragma clang loop unroll(full)
             for (int kk = 0; kk < 8; ++kk) {
                 if (kk + 1 < 8) {
-                    ka[(kk + 1) & 1][0] = kb4[(0 * 8 + kk + 1) * 64 + lane];
-                    ka[(kk + 1) & 1][1] = kb4[(1 * 8 + kk + 1) * 64 + lane];
+                    ka[(kk + 1) & 1][0] = kload(kb4, (0 * 8 + kk + 1) * 64 + lane);
+                    ka[(kk + 1) & 1][1] = kload(kb4, (1 * 8 + kk + 1) * 64 + lane);
                     if (FHE_LMK_PIPE) issue(kk + 1, (kk + 1) & 1);
                 }
                 asm volatile("" ::: "memory");
@@ -1441,8 +1449,8 @@ __global__ void __launch_bounds__(64 * kPrepWaves)
                  uint32_t* __restrict__ nops, uint32_t* __restrict__ tvb, uint32_t maxops, uint32_t numAutoKeys) {
     __shared__ uint32_t s_start[kPrepWaves][1025];
     __shared__ uint16_t s_fill[kPrepWaves][1024];
-    __shared__ uint16_t s_bkt[kPrepWaves][512];
-    __shared__ uint16_t s_sorted[kPrepWaves][512];
+    __shared__ uint16_t s_bkt[kPrepWaves][1024];     // n < 1024 (Engine::fast_path)
+    __shared__ uint16_t s_sorted[kPrepWaves][1024];
     __shared__ uint32_t s_part[kPrepWaves][64];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t gate = blockIdx.x * kPrepWaves + wv;
@@ -1593,7 +1601,7 @@ hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_
                            hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
-    if (g.n > 512 || g.N != 1024) return hipErrorInvalidValue;  // k_prep_lmk_w LDS sizes
+    if (g.n > 1024 || g.N != 1024) return hipErrorInvalidValue;  // k_prep_lmk_w LDS sizes
     hipLaunchKernelGGL(k_prep_lmk_w, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, in, g,
                        logGen, ops, nops, tvb, maxops, numAutoKeys);
     return hipGetLastError();

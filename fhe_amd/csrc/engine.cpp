@@ -17,25 +17,33 @@ inline uint32_t neg_inv32(uint32_t Q) {  // -Q^-1 mod 2^32 (Newton)
 }
 }  // namespace
 
+bool Engine::fast_path(const Params& p) {
+    const bool pow2q = !(p.q & (p.q - 1)), pow2ks = !(p.qKS & (p.qKS - 1));
+    return !is_large(p.paramset) && p.N == 1024 && p.Q < (1ull << 28) && p.digitsG == 3 && pow2q && pow2ks &&
+           p.qKS <= 65536 && p.n < 1024;
+}
+
 Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, method)), device_(device) {
-    if (is_large(paramset)) {  // 64-bit accumulator (bootstrap_wide.hip)
+    // Two accumulator kernels: the 32-bit one (bootstrap.hip) for N = 1024, Q < 2^28, digitsG = 3 (the
+    // STD128 / MEDIUM / STD128*_LMKCDEY sets); the 64-bit one (bootstrap_wide.hip) for every other
+    // GINX set with N = 1024 / 2048 (any digitsG, Q up to 2^62) and the large-precision family.
+    if (is_large(paramset) || (!fast_path(p_) && method == M_GINX)) {
         wide_ = true;
         if (p_.N != 1024 && p_.N != 2048)
-            throw std::invalid_argument("device path supports N = 1024 / 2048 for the large-precision family");
+            throw std::invalid_argument("device path supports ring dimension N = 1024 / 2048");
         if ((double)p_.digitsG2 * (double)p_.Q >= 18446744073709551616.0)
             throw std::invalid_argument("device path: digitsG2 * Q must stay below 2^64");
         if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
+        if (p_.q & (p_.q - 1)) throw std::invalid_argument("device path needs a power-of-two q");
         if (p_.n > 2048) throw std::invalid_argument("device path supports n <= 2048");
         FHE_HIP_CHECK(hipSetDevice(device_));
         FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         build_tables_wide();
         return;
     }
-    if (p_.N != 1024) throw std::invalid_argument("device path supports ring dimension N = 1024 (STD128 sets)");
-    if (p_.Q >= (1ull << 28)) throw std::invalid_argument("device path needs Q < 2^28");
-    if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
-    if (p_.q & (p_.q - 1)) throw std::invalid_argument("device path needs a power-of-two q");
-    if (p_.digitsG != 3) throw std::invalid_argument("device path expects digitsG = 3");
+    if (!fast_path(p_))
+        throw std::invalid_argument(
+            "device path for AP / LMKCDEY: N = 1024, Q < 2^28, digitsG = 3, power-of-two q and qKS <= 2^16, n < 1024");
     FHE_HIP_CHECK(hipSetDevice(device_));
     FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     build_tables();
@@ -296,17 +304,18 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
         FHE_HIP_CHECK(hipMemcpy(d_wksk_ + nA, B, nB * 8, hipMemcpyHostToDevice));
         return;
     }
-    std::vector<uint16_t> dev(rows * 512, 0);
+    const size_t W = ksk_width(p_.n);
+    std::vector<uint16_t> dev(rows * W, 0);
     bool bad = false;
 #pragma omp parallel for schedule(static) reduction(|| : bad)
     for (int64_t r = 0; r < (int64_t)rows; ++r) {
         for (uint32_t k = 0; k < p_.n; ++k) {
             const uint64_t v = A[(size_t)r * p_.n + k];
             bad = bad || v >= p_.qKS;
-            dev[(size_t)r * 512 + k] = (uint16_t)v;
+            dev[(size_t)r * W + k] = (uint16_t)v;
         }
         bad = bad || B[r] >= p_.qKS;
-        dev[(size_t)r * 512 + p_.n] = (uint16_t)B[r];
+        dev[(size_t)r * W + p_.n] = (uint16_t)B[r];
     }
     if (bad) throw std::invalid_argument("ksk value not reduced mod qKS");
     FHE_HIP_CHECK(hipSetDevice(device_));
@@ -341,7 +350,7 @@ void Engine::keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t
     uint64_t *rb = nullptr, *ra = nullptr, *rk = nullptr;
     try {
         FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * 4));
-        FHE_HIP_CHECK(hipMalloc(&d_ksk_, rows * 512 * 2));
+        FHE_HIP_CHECK(hipMalloc(&d_ksk_, rows * ksk_width(p_.n) * 2));
         const size_t raw_words = (bsk_out ? words : 0) + (kskA_out ? rows * p_.n : 0) + (kskB_out ? rows : 0);
         if (raw_words) FHE_HIP_CHECK(hipMalloc(&raw, raw_words * 8));
         uint64_t* cur = static_cast<uint64_t*>(raw);

@@ -50,8 +50,11 @@ public:
     void end_call(hipStream_t s);
     void sync_streams();  // waits for the context's stream and the last asynchronous call
     bool ready() const { return d_bsk_ && (d_ksk_ || d_wksk_); }
-    // the large-precision family (64-bit accumulator, boot_wide.h)
+    // the 64-bit accumulator (boot_wide.h): the large-precision family and the GINX sets outside
+    // the 32-bit kernel's range
     bool wide() const { return wide_; }
+    // the 32-bit kernels' range: N = 1024, Q < 2^28, digitsG = 3, power-of-two q, qKS <= 2^16, n < 1024
+    static bool fast_path(const Params& p);
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);

@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
     }
 }
 
-// one wave per KSK row [N][baseKS][digitsKS]; rows of the u16 layout are 512 wide (A, B, zeros)
+// one wave per KSK row [N][baseKS][digitsKS]; rows of the u16 layout are ksk_width(n) wide (A, B, zeros)
 __global__ void __launch_bounds__(256) k_kg_ksk(uint64_t seed, uint32_t rows, uint32_t n, uint32_t bKS, uint32_t dKS,
                                                 uint64_t qk, const uint64_t* __restrict__ sv,
                                                 const uint64_t* __restrict__ svN, const uint64_t* __restrict__ dig,
@@ -127,10 +127,11 @@ __global__ void __launch_bounds__(256) k_kg_ksk(uint64_t seed, uint32_t rows, ui
     if (row >= rows) return;
     const uint64_t s0 = seed * kRngGamma ^ ((uint64_t)T_KSK << 56) ^ ((uint64_t)row * 0xD1B54A32D192ED03ull);
     uint64_t acc = 0;
-    for (uint32_t t = lane; t < 512; t += 64) {
+    const uint32_t W = ksk_width(n);
+    for (uint32_t t = lane; t < W; t += 64) {
         const uint64_t v = t < n ? draw_uniform(s0, t, qk) : 0;
         acc += v * sv[t];
-        if (t != n) ksk[(size_t)row * 512 + t] = (uint16_t)v;
+        if (t != n) ksk[(size_t)row * W + t] = (uint16_t)v;
         if (rawA && t < n) rawA[(size_t)row * n + t] = v;
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(256) k_kg_ksk(uint64_t seed, uint32_t rows, ui
         uint64_t b = draw_cbd(s0, n, qk);
         b = (b + svN[i] * ((j * dig[kk]) % qk)) % qk;
         b = (b + acc % qk) % qk;
-        ksk[(size_t)row * 512 + n] = (uint16_t)b;
+        ksk[(size_t)row * W + n] = (uint16_t)b;
         if (rawB) rawB[row] = b;
     }
 }
@@ -274,12 +275,13 @@ void keygen_bootstrap_device(const Params& p, const std::vector<uint64_t>& sk, u
     // key-switching key
     const uint64_t qk = p.qKS;
     const uint32_t rows = (uint32_t)p.ksk_rows();
-    std::vector<uint64_t> sv(512, 0), svN(N), dig(p.digitsKS);
+    const uint32_t W = ksk_width(n);
+    std::vector<uint64_t> sv(W, 0), svN(N), dig(p.digitsKS);
     for (uint32_t i = 0; i < n; ++i) sv[i] = sk[i] % qk;
     for (uint32_t i = 0; i < N; ++i) svN[i] = lift(signed_of(skN[i], Q), qk);
     for (uint32_t k = 0, v = 1; k < p.digitsKS; ++k, v *= p.baseKS) dig[k] = v;
-    DevBuf<uint64_t> dsv(512), dsvN(N), ddig(dig.size());
-    FHE_HIP_CHECK(hipMemcpyAsync(dsv.p, sv.data(), 512 * 8, hipMemcpyHostToDevice, s));
+    DevBuf<uint64_t> dsv(W), dsvN(N), ddig(dig.size());
+    FHE_HIP_CHECK(hipMemcpyAsync(dsv.p, sv.data(), W * 8, hipMemcpyHostToDevice, s));
     FHE_HIP_CHECK(hipMemcpyAsync(dsvN.p, svN.data(), N * 8, hipMemcpyHostToDevice, s));
     FHE_HIP_CHECK(hipMemcpyAsync(ddig.p, dig.data(), dig.size() * 8, hipMemcpyHostToDevice, s));
     k_kg_ksk<<<(rows + 3) / 4, 256, 0, s>>>(seed, rows, n, p.baseKS, p.digitsKS, qk, dsv.p, dsvN.p, ddig.p, d_ksk,

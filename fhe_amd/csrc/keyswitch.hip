@@ -34,15 +34,16 @@ FHE_DEV uint64_t mod_switch_up(uint64_t v, uint32_t qKS, uint64_t q_out) {
 }
 }  // namespace
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
     k_keyswitch(GateArgs g, uint32_t logBase, uint32_t digitsKS, const uint32_t* __restrict__ ksk,
                 const uint32_t* __restrict__ ms_a, const uint32_t* __restrict__ ms_b, uint64_t q_out,
                 uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
     __shared__ uint32_t s_a[1024];
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
-    for (uint32_t i = t; i < g.N; i += 256) s_a[i] = ms_a[(size_t)gate * g.N + i];
+    for (uint32_t i = t; i < g.N; i += blockDim.x) s_a[i] = ms_a[(size_t)gate * g.N + i];
     __syncthreads();
     const uint32_t base = 1u << logBase, mask = base - 1;
+    const uint32_t rw = blockDim.x;   // u32 words per row = ksk_width(n) / 2
     uint32_t lo = 0, hi = 0;
 #pragma unroll 4
     for (uint32_t i = 0; i < g.N; ++i) {
@@ -50,7 +51,7 @@ __global__ void __launch_bounds__(256)
         for (uint32_t j = 0; j < digitsKS; ++j) {
             const uint32_t dig = (ai >> (logBase * j)) & mask;
             const uint32_t row = (i * base + dig) * digitsKS + j;
-            const uint32_t w   = ksk[(size_t)row * 256 + t];
+            const uint32_t w   = ksk[(size_t)row * rw + t];
             lo += w & 0xffffu;
             hi += w >> 16;
         }
@@ -135,7 +136,7 @@ __global__ void __launch_bounds__(G)
         const uint32_t x = t + G * r, sd = x / kKsPartsPerSlice, sp = x % kKsPartsPerSlice;
         const uint32_t i = round * kKsIPR + q / kKsDigits, j = q % kKsDigits;
         const size_t row = ((size_t)i * (1u << kKsLogBase) + sd) * kKsDigits + j;
-        return reinterpret_cast<const uint4*>(ksk + row * 512 + col0) + sp;
+        return reinterpret_cast<const uint4*>(ksk + row * ksk_width(g.n) + col0) + sp;
     };
     auto slice_dst = [&](unsigned char* sb, int r) -> unsigned char* {
         const uint32_t x = t + G * r;
@@ -240,7 +241,8 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
                             uint64_t* b_out, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (baseKS & (baseKS - 1)) return hipErrorInvalidValue;
-    if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 512 || g.N > 1024) return hipErrorInvalidValue;
+    if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 1024 || g.N > 1024) return hipErrorInvalidValue;
+    const uint32_t W = ksk_width(g.n);
     const uint32_t logBase = (uint32_t)__builtin_ctz(baseKS);
 #ifndef FHE_KS_TILE
 #define FHE_KS_TILE 0   // 0: choose by batch size; 1: per-gate kernel; 256: gate tile
@@ -249,10 +251,10 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     if (tile == 0) tile = g.count >= 4096 ? 256 : 1;  // tiles need >= 16 x 8 workgroups to pay
     if (tile > 1 && (logBase != (uint32_t)kKsLogBase || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
     if (tile > 1) {
-        hipLaunchKernelGGL(k_keyswitch_tiled<FHE_KS_G>, dim3((g.count + FHE_KS_G - 1) / FHE_KS_G, 512 / kKsCols),
+        hipLaunchKernelGGL(k_keyswitch_tiled<FHE_KS_G>, dim3((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols),
                            dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, a_out, b_out);
     } else {
-        hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(256), 0, s, g, logBase, digitsKS,
+        hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(W / 2), 0, s, g, logBase, digitsKS,
                            reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
     }
     return hipGetLastError();

@@ -83,18 +83,70 @@ Params make_params_large(int code, int method) {
 }
 }  // namespace
 
+namespace {
+// BinFHEContext::GenerateBinFHEContext(set, method) rows (binfhecontext.cpp:113-159), indexed by
+// BINFHE_PARAMSET (binfhe-constants.h:49-95).  qks = 0: modKS = PRIME (the ring modulus Q).
+struct Row {
+    uint32_t bits, cyc, n, q, qks, bks, bg, brk, nauto;
+    int kd;
+};
+constexpr int G_ = KD_GAUSSIAN, T_ = KD_UNIFORM_TERNARY;
+constexpr Row kRows[] = {
+    {27, 1024, 64, 512, 0, 25, 512, 23, 9, T_},                  // TOY
+    {28, 2048, 422, 1024, 16384, 128, 1024, 32, 10, T_},         // MEDIUM
+    {27, 2048, 503, 1024, 16384, 32, 512, 32, 10, T_},           // STD128_AP
+    {27, 2048, 503, 1024, 16384, 32, 512, 32, 10, T_},           // STD128
+    {27, 2048, 595, 1024, 65536, 64, 128, 32, 10, T_},           // STD128_3
+    {27, 2048, 595, 2048, 65536, 64, 128, 64, 10, T_},           // STD128_4
+    {25, 2048, 534, 1024, 16384, 32, 128, 32, 10, T_},           // STD128Q
+    {50, 4096, 600, 2048, 32768, 32, 33554432, 64, 10, T_},      // STD128Q_3
+    {50, 4096, 641, 2048, 65536, 64, 33554432, 64, 10, T_},      // STD128Q_4
+    {37, 4096, 790, 2048, 16384, 32, 524288, 64, 10, T_},        // STD192
+    {37, 4096, 875, 4096, 65536, 64, 524288, 64, 10, T_},        // STD192_3
+    {37, 4096, 875, 4096, 65536, 64, 8192, 64, 10, T_},          // STD192_4
+    {35, 4096, 875, 1024, 32768, 32, 4096, 32, 10, T_},          // STD192Q
+    {34, 4096, 922, 2048, 65536, 16, 4096, 64, 10, T_},          // STD192Q_3
+    {34, 4096, 980, 2048, 131072, 16, 4096, 64, 10, T_},         // STD192Q_4
+    {29, 4096, 1076, 2048, 32768, 32, 1024, 64, 10, T_},         // STD256
+    {29, 4096, 1145, 2048, 65536, 64, 256, 64, 10, T_},          // STD256_3
+    {29, 4096, 1145, 4096, 65536, 64, 256, 64, 10, T_},          // STD256_4
+    {27, 4096, 1225, 1024, 65536, 16, 128, 32, 10, T_},          // STD256Q
+    {27, 4096, 1400, 4096, 65536, 21, 64, 64, 10, T_},           // STD256Q_3
+    {27, 4096, 1625, 4096, 2097152, 16, 64, 64, 10, T_},         // STD256Q_4
+    {28, 2048, 447, 2048, 16384, 32, 1024, 64, 10, G_},          // STD128_LMKCDEY
+    {27, 2048, 556, 2048, 32768, 32, 512, 64, 10, T_},           // STD128_3_LMKCDEY
+    {27, 2048, 595, 2048, 65536, 64, 128, 64, 10, T_},           // STD128_4_LMKCDEY
+    {27, 2048, 483, 2048, 16384, 32, 512, 64, 10, G_},           // STD128Q_LMKCDEY
+    {25, 2048, 643, 2048, 65536, 64, 128, 64, 10, T_},           // STD128Q_3_LMKCDEY
+    {50, 4096, 641, 4096, 65536, 64, 33554432, 64, 10, T_},      // STD128Q_4_LMKCDEY
+    {39, 4096, 716, 2048, 32768, 32, 1048576, 64, 10, G_},       // STD192_LMKCDEY
+    {39, 4096, 771, 4096, 65536, 64, 1048576, 64, 10, G_},       // STD192_3_LMKCDEY
+    {37, 4096, 875, 4096, 65536, 64, 8192, 64, 10, T_},          // STD192_4_LMKCDEY
+    {36, 4096, 776, 4096, 32768, 32, 262144, 64, 10, G_},        // STD192Q_LMKCDEY
+    {36, 4096, 834, 4096, 65536, 64, 4096, 64, 10, G_},          // STD192Q_3_LMKCDEY
+    {34, 4096, 949, 4096, 65536, 64, 4096, 64, 10, T_},          // STD192Q_4_LMKCDEY
+    {30, 4096, 939, 2048, 32768, 32, 1024, 64, 10, G_},          // STD256_LMKCDEY
+    {29, 4096, 1076, 4096, 32768, 32, 256, 64, 10, T_},          // STD256_3_LMKCDEY
+    {29, 4096, 1145, 4096, 65536, 64, 256, 64, 10, T_},          // STD256_4_LMKCDEY
+    {28, 4096, 1019, 4096, 32768, 32, 1024, 64, 10, G_},         // STD256Q_LMKCDEY
+    {26, 4096, 1242, 4096, 65536, 64, 128, 64, 10, T_},          // STD256Q_3_LMKCDEY
+    {26, 4096, 1320, 4096, 131072, 64, 64, 64, 10, T_},          // STD256Q_4_LMKCDEY
+    {27, 2048, 556, 2048, 32768, 32, 128, 64, 10, T_},           // LPF_STD128
+    {25, 2048, 645, 2048, 65536, 64, 128, 64, 10, T_},           // LPF_STD128Q
+    {27, 2048, 556, 2048, 32768, 32, 512, 64, 10, T_},           // LPF_STD128_LMKCDEY
+    {25, 2048, 600, 2048, 32768, 32, 128, 64, 10, T_},           // LPF_STD128Q_LMKCDEY
+    {28, 2048, 512, 1024, 0, 25, 128, 23, 10, T_},               // SIGNED_MOD_TEST
+};
+constexpr int kNumRows = (int)(sizeof(kRows) / sizeof(kRows[0]));
+}  // namespace
+
 Params make_params(int paramset, int method) {
     if (is_large(paramset)) return make_params_large(paramset, method);
-    //            bits cyc   n    q     qKS    Bks  Bg    nAuto keyDist   (binfhecontext.cpp:113-159)
-    uint32_t bits, cyc, n, q, qks, bks, bg, nauto;
-    int kd;
-    switch (paramset) {
-        case PS_TOY:            bits = 27; cyc = 1024; n = 64;  q = 512;  qks = 0;     bks = 25; bg = 512;  nauto = 9;  kd = KD_UNIFORM_TERNARY; break;
-        case PS_STD128_AP:
-        case PS_STD128:         bits = 27; cyc = 2048; n = 503; q = 1024; qks = 16384; bks = 32; bg = 512;  nauto = 10; kd = KD_UNIFORM_TERNARY; break;
-        case PS_STD128_LMKCDEY: bits = 28; cyc = 2048; n = 447; q = 2048; qks = 16384; bks = 32; bg = 1024; nauto = 10; kd = KD_GAUSSIAN; break;
-        default: throw std::invalid_argument("unsupported parameter set (TOY, STD128_AP, STD128, STD128_LMKCDEY)");
-    }
+    if (paramset < 0 || paramset >= kNumRows) throw std::invalid_argument("unknown parameter set");
+    const Row& R = kRows[paramset];
+    const uint32_t bits = R.bits, cyc = R.cyc, n = R.n, q = R.q, qks = R.qks, bks = R.bks, bg = R.bg;
+    const uint32_t nauto = R.nauto;
+    const int kd = R.kd;
     if (method != M_GINX && method != M_LMKCDEY && method != M_AP)
         throw std::invalid_argument("unsupported method (AP, GINX, LMKCDEY)");
     Params p;
@@ -113,7 +165,7 @@ Params make_params(int paramset, int method) {
     p.digitsG2 = (p.digitsG - 1) * 2;
     p.numAutoKeys = nauto;
     p.keyDist = kd;
-    p.baseR = 32;  // baseRK column of every row (binfhecontext.cpp:113-159)
+    p.baseR = R.brk;  // the baseRK column (binfhecontext.cpp:113-159)
     p.digitsR = (uint32_t)std::ceil(std::log((double)q) / std::log((double)p.baseR));
     p.psi = root_of_unity(cyc, p.Q);
     uint64_t v = 1;

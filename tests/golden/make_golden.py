@@ -44,38 +44,55 @@ def make_ntt():
 
 
 GATE_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "ap": (STD128_AP, AP)}
+# the other BINFHE_PARAMSET rows (binfhecontext.cpp:113-159) the device path covers: GINX on every
+# non-LMKCDEY set with N = 1024 / 2048 and a power-of-two baseKS / qKS, LMKCDEY on the N = 1024,
+# digitsG = 3 sets; reference enum values (binfhe-constants.h:49-95)
+WIDER_SETS = {"medium": (1, GINX), "medium_ap": (1, AP), "medium_lmkcdey": (1, LMKCDEY),
+              "std128_3": (4, GINX), "std128_4": (5, GINX), "std128q": (6, GINX),
+              "std128q_3": (7, GINX), "std128q_4": (8, GINX), "std192": (9, GINX), "std192_3": (10, GINX),
+              "std192_4": (11, GINX), "std192q": (12, GINX), "std192q_3": (13, GINX), "std192q_4": (14, GINX),
+              "std256": (15, GINX), "std256_3": (16, GINX), "std256_4": (17, GINX), "std256q": (18, GINX),
+              "std256q_4": (20, GINX), "std128_3_lmkcdey": (22, LMKCDEY), "std128q_lmkcdey": (24, LMKCDEY),
+              "lpf_std128": (39, GINX), "lpf_std128q": (40, GINX), "lpf_std128_lmkcdey": (41, LMKCDEY)}
+GATE_SETS.update(WIDER_SETS)
+WIDER_PER_GATE = 2
 GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}
 PER_GATE = 8
 
 
-def gate_inputs(ps, m, key_seed):
+def gate_inputs(ps, m, key_seed, per_gate=PER_GATE):
     """Deterministic keys (fhe_amd host keygen, seeded) + encrypted inputs."""
     from fhe_amd import binfhe as bf
     keys = bf.keygen(ps, m, key_seed)
-    return (keys,) + gate_inputs_for(ps, m, key_seed, keys.sk)
+    return (keys,) + gate_inputs_for(ps, m, key_seed, keys.sk, per_gate)
 
 
-def gate_inputs_for(ps, m, key_seed, sk):
+def gate_inputs_for(ps, m, key_seed, sk, per_gate=PER_GATE):
     """the encrypted inputs of gate_inputs() under the secret key sk (= keygen(key_seed).sk)"""
     from fhe_amd import binfhe as bf
     rng = np.random.default_rng(key_seed)
-    bits1 = rng.integers(0, 2, size=(len(GATES), PER_GATE))
-    bits2 = rng.integers(0, 2, size=(len(GATES), PER_GATE))
+    bits1 = rng.integers(0, 2, size=(len(GATES), per_gate))
+    bits2 = rng.integers(0, 2, size=(len(GATES), per_gate))
     a1, b1 = bf.encrypt(ps, m, sk, bits1.ravel(), key_seed + 1)
     a2, b2 = bf.encrypt(ps, m, sk, bits2.ravel(), key_seed + 2)
     return bits1, bits2, a1, b1, a2, b2
 
 
+def gate_key_seed(ps, m):
+    return 0xB0070000 + ps + (0 if m in (GINX,) or ps in (STD128_LMKCDEY, STD128_AP) else m << 8)
+
+
 def make_gates(names=("std128", "lmkcdey")):
     for name in names:
         ps, m = GATE_SETS[name]
-        key_seed = 0xB0070000 + ps
-        keys, bits1, bits2, a1, b1, a2, b2 = gate_inputs(ps, m, key_seed)
+        key_seed = gate_key_seed(ps, m)
+        pg = WIDER_PER_GATE if name in WIDER_SETS else PER_GATE
+        keys, bits1, bits2, a1, b1, a2, b2 = gate_inputs(ps, m, key_seed, pg)
         ref = Ref(ps, m)
         ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
         outs, exts, extb, outb = [], [], [], []
         for gi, (gname, g) in enumerate(GATES.items()):
-            sl = slice(gi * PER_GATE, (gi + 1) * PER_GATE)
+            sl = slice(gi * pg, (gi + 1) * pg)
             ao, bo = ref.eval_gate(g, a1[sl], b1[sl], a2[sl], b2[sl])
             ea, eb = ref.eval_gate(g, a1[sl], b1[sl], a2[sl], b2[sl], extended=True)
             outs.append(ao); outb.append(bo); exts.append(ea); extb.append(eb)
@@ -83,15 +100,17 @@ def make_gates(names=("std128", "lmkcdey")):
         # intermediates of SwitchCTtoqn on ctExt: ModSwitch(Q -> qKS), KeySwitch, ModSwitch(qKS -> q)
         ms_a, ms_b = ref.modswitch(ref.Q, ref.qKS, exts, extb)
         ks_a, ks_b = ref.keyswitch(ms_a, ms_b)
+        dec = np.array([ref.decrypt(keys.sk, outs[i], outb[i], ref.q) for i in range(len(outb))])
         np.savez_compressed(os.path.join(HERE, f"gates_{name}.npz"), paramset=ps, method=m, key_seed=np.uint64(key_seed),
                             gates=np.array(list(GATES.values())), bits1=bits1, bits2=bits2,
                             out_a=outs.astype(np.uint16), out_b=outb.astype(np.uint16),
-                            ext_a=exts[::PER_GATE // 2].astype(np.uint32), ext_b=extb.astype(np.uint32),
+                            ext_a=exts[::pg // 2].astype(np.uint64 if ref.Q >= 1 << 32 else np.uint32),
+                            ext_b=extb.astype(np.uint64),
                             ext_sha=np.array(sha(exts)), ks_sha=np.array(sha(ks_a) + sha(ks_b)),
-                            ms_sha=np.array(sha(ms_a) + sha(ms_b)),
+                            ms_sha=np.array(sha(ms_a) + sha(ms_b)), ref_dec=dec,
                             keys_sha=np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB)),
                             in_sha=np.array(sha(a1) + sha(b1) + sha(a2) + sha(b2)))
-        print(name, "ok", outs.shape)
+        print(name, "ok", outs.shape, flush=True)
 
 
 # multi-input gates (binfhe-base-scheme.cpp:129-187): (gate, k, plaintext modulus) as the
@@ -307,6 +326,8 @@ if __name__ == "__main__":
         make_ntt()
     if what in ("gates", "all"):
         make_gates(sys.argv[2:] or ("std128",))
+    if what == "wider":   # one process per call keeps the reference's memory bounded
+        make_gates(sys.argv[2:] or tuple(WIDER_SETS))
     if what in ("multi", "all"):
         make_multi(sys.argv[2:] or ("std128", "lmkcdey"))
     if what == "fb":   # one parameter set per process (see tests/test_fb.py)

@@ -1,0 +1,73 @@
+"""The other BINFHE_PARAMSET rows (binfhecontext.cpp:113-159) on the device path, bit-exact against
+the reference's own outputs for the same keys and ciphertexts (tests/golden/gates_<set>.npz, made by
+tests/golden/make_golden.py wider from oracle/_ref):
+
+  * the 32-bit kernels (N = 1024, Q < 2^28, digitsG = 3): MEDIUM (GINX, AP, LMKCDEY),
+    STD128_3_LMKCDEY, STD128Q_LMKCDEY, LPF_STD128_LMKCDEY (n = 556: 1024-column key-switching rows,
+    qKS = 2^15);
+  * the 64-bit kernel (bootstrap_wide.hip) for every other GINX set: digitsG = 4 / 5 (STD128_3/4,
+    STD128Q, LPF_STD128/Q, STD256*), N = 2048 with 29- to 50-bit Q (STD128Q_3/4, STD192*, STD256*),
+    qKS up to 2^21.
+Six gate types per set, final outputs and the extended ctExt."""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, GOLD)
+from make_golden import GATES, WIDER_PER_GATE, WIDER_SETS  # noqa: E402
+
+TRUTH = {0: lambda a, b: a | b, 1: lambda a, b: a & b, 2: lambda a, b: 1 - (a | b), 3: lambda a, b: 1 - (a & b),
+         4: lambda a, b: a ^ b, 5: lambda a, b: 1 - (a ^ b)}
+SETS = [s for s in WIDER_SETS if os.path.exists(os.path.join(GOLD, f"gates_{s}.npz"))]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.uint64).tobytes()).hexdigest()
+
+
+def golden(name):
+    return np.load(os.path.join(GOLD, f"gates_{name}.npz"))
+
+
+def test_wider_goldens_present():
+    assert len(SETS) >= 20, SETS
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_reference_wider_outputs_decrypt_to_truth_table(name):
+    """the reference, run on our keys, computes every gate correctly (its own decryptions)"""
+    g = golden(name)
+    pg = WIDER_PER_GATE
+    for i, gate in enumerate(g["gates"]):
+        exp = TRUTH[int(gate)](g["bits1"][i], g["bits2"][i])
+        assert np.array_equal(g["ref_dec"][i * pg:(i + 1) * pg], exp), (name, int(gate))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
+def test_gpu_wider_paramset_gates_bit_exact_vs_reference(name):
+    from fhe_amd import binfhe as bf
+    from make_golden import gate_inputs
+    g = golden(name)
+    ps, m = int(g["paramset"]), int(g["method"])
+    pg = WIDER_PER_GATE
+    keys, bits1, bits2, a1, b1, a2, b2 = gate_inputs(ps, m, int(g["key_seed"]), pg)
+    assert sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB) == str(g["keys_sha"])
+    assert sha(a1) + sha(b1) + sha(a2) + sha(b2) == str(g["in_sha"])
+    e = bf.GateEngine(ps, m, device=0)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    del keys
+    outs, outb, exts = [], [], []
+    for i, gate in enumerate(GATES.values()):
+        sl = slice(i * pg, (i + 1) * pg)
+        ao, bo = e.eval_gate(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        ea, eb = e.eval_gate_extended(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        outs.append(ao); outb.append(bo); exts.append(ea)
+    e.close()
+    assert np.array_equal(np.concatenate(outs), g["out_a"].astype(np.uint64))
+    assert np.array_equal(np.concatenate(outb), g["out_b"].astype(np.uint64))
+    assert sha(np.concatenate(exts)) == str(g["ext_sha"])

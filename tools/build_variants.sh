@@ -14,6 +14,6 @@ while [ $# -ge 2 ]; do
     g++ -std=c++17 -O3 -fPIC -fopenmp -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ $flags -c $f -o $out/$(basename $f .cpp).o &
   done
   wait
-  /opt/rocm/bin/hipcc -shared -fopenmp --offload-arch=gfx950 -o build/variants/$name.so $out/*.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o build/variants/$name.so $out/*.o -lgomp
   echo "built build/variants/$name.so ($flags)"
 done
