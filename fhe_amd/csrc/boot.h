@@ -24,6 +24,7 @@ struct BootTables {
     const uint32_t* monoP;       // plain (non-Montgomery) copies of mono / mono_full: the signed
     const uint32_t* monoP_full;  // accumulator multiplies the unreduced 64-bit digit-key sums by both
     const uint32_t* tabI;        // TableI[0..1023] (the LMKCDEY automorphism's wave-wide inverse NTT)
+    const uint32_t* tabF;        // Table[0..1023] (the split GINX kernel's wave-wide forward NTT)
     uint32_t Q, Q2, qinv;     // qinv = -Q^-1 mod 2^32
     // The resident keys carry a factor N^-1 (folded in at packing), so the EVALUATION accumulator
     // is N^-1 * acc and the last inverse stage needs no N^-1 multiply: it scales by TableI[1] only.
@@ -102,6 +103,12 @@ struct GateInputs {
 
 // GINX/CGGI: inputs -> monomial exponents + test-vector b
 hipError_t launch_prep_ginx(const GateArgs& g, const GateInputs& in, uint16_t* idx, uint32_t* tvb, hipStream_t s);
+// GINX with two waves per gate (one RLWE component each): keys repacked from the resident GINX
+// layout (launch_repack_ginx2); launched for gate batches with Q < 2^27 and ciphertext modulus q < 2N
+hipError_t launch_repack_ginx2(const void* bsk, uint32_t n, void* bsk2, hipStream_t s);
+hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, const void* bsk2, const uint16_t* idx,
+                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
+bool ginx2_supported(const GateArgs& g, const BootTables& t);
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);

@@ -2,6 +2,8 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 #include "keygen.h"
 #include "nt.h"
@@ -48,6 +50,8 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     build_tables();
     maxops_ = p_.N + p_.n + 128;
+    // FHE_HIP_GINX_KERNEL = wave | split: pin the GINX blind-rotation kernel (tests, A/B); default by batch size
+    if (const char* k = std::getenv("FHE_HIP_GINX_KERNEL")) ginx_kernel_ = std::string(k) == "split" ? 2 : std::string(k) == "wave" ? 1 : 0;
 }
 
 Engine::~Engine() {
@@ -56,7 +60,7 @@ Engine::~Engine() {
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
                       (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
-                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_})
+                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_})
         if (ptr) (void)hipFree(ptr);
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -89,7 +93,7 @@ void Engine::build_tables() {
     const uint64_t Q = p_.Q;
     HostNtt h;
     h.init(p_.N, Q, p_.psi);
-    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2 * (kMonoHalfWords + kMonoTableWords) + 1024, 0);
+    std::vector<uint32_t> t(32 + 32 + 992 + 992 + 2 * (kMonoHalfWords + kMonoTableWords) + 2048, 0);
     uint32_t* twAf = t.data();
     uint32_t* twAi = twAf + 32;
     uint32_t* twBf = twAi + 32;
@@ -99,7 +103,11 @@ void Engine::build_tables() {
     uint32_t* monoP = monoF + kMonoTableWords;
     uint32_t* monoPF = monoP + kMonoHalfWords;
     uint32_t* tabI = monoPF + kMonoTableWords;
-    for (uint32_t i = 0; i < 1024 && i < p_.N; ++i) tabI[i] = to_mont(h.tabI[i], Q);
+    uint32_t* tabF = tabI + 1024;
+    for (uint32_t i = 0; i < 1024 && i < p_.N; ++i) {
+        tabI[i] = to_mont(h.tabI[i], Q);
+        tabF[i] = to_mont(h.tab[i], Q);
+    }
     for (int i = 0; i < 32; ++i) {
         twAf[i] = to_mont(h.tab[i], Q);
         twAi[i] = to_mont(h.tabI[i], Q);
@@ -158,6 +166,7 @@ void Engine::build_tables() {
     tabs_.monoP = tabs_.mono_full + kMonoTableWords;
     tabs_.monoP_full = tabs_.monoP + kMonoHalfWords;
     tabs_.tabI = tabs_.monoP_full + kMonoTableWords;
+    tabs_.tabF = tabs_.tabI + 1024;
     tabs_.Q = (uint32_t)Q;
     tabs_.Q2 = (uint32_t)(2 * Q);
     tabs_.qinv = neg_inv32((uint32_t)Q);
@@ -284,6 +293,16 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     FHE_HIP_CHECK(hipMalloc(&d_bsk_, dev.size() * 4));
     FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
     d_autok_ = static_cast<uint32_t*>(d_bsk_) + nrgsw * dG2 * 2 * N;
+    repack_ginx2();
+}
+
+// the split GINX kernel's key layout (k_blind_rotate_ginx2), repacked on the device from the resident one
+void Engine::repack_ginx2() {
+    if (p_.method != M_GINX || wide_ || !d_bsk_) return;
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    if (!d_bsk2_) FHE_HIP_CHECK(hipMalloc(&d_bsk2_, (size_t)p_.n * 16384 * 4));
+    FHE_HIP_CHECK(launch_repack_ginx2(d_bsk_, p_.n, d_bsk2_, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB) {
@@ -374,6 +393,7 @@ void Engine::keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t
                          : p_.method == M_AP ? (size_t)p_.n * p_.baseR * p_.digitsR
                                              : (size_t)p_.n;
     d_autok_ = static_cast<uint32_t*>(d_bsk_) + nrgsw * p_.digitsG2 * 2 * p_.N;
+    repack_ginx2();
 }
 
 GateArgs Engine::gate_args(int gate, size_t count, uint32_t p, bool multi) const {
@@ -498,7 +518,13 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
     if (g.gbits < 2 || h * (1 + (1ull << g.gbits) + (1ull << (2 * g.gbits))) + p_.Q >= (1ull << 32))
         throw std::invalid_argument("device path expects log2(baseG) <= 10");
     if (p_.method == M_GINX) {
-        FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+        // two waves per gate below kSplitBatch gates (fills the chip at small batches), else one
+        const bool split = d_bsk2_ && ginx2_supported(g, tabs_) &&
+                           (ginx_kernel_ == 2 || (ginx_kernel_ == 0 && g.count < kSplitBatch));
+        if (split)
+            FHE_HIP_CHECK(launch_blind_rotate_ginx2(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+        else
+            FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
     } else {
         FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_bsk_, d_autok_, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
                                               d_ext_b_, p_.method == M_AP, s));

@@ -166,6 +166,15 @@ private:
     uint16_t* d_ops_ = nullptr;
     uint32_t* d_nops_ = nullptr;
     uint16_t* d_ksk_ = nullptr;
+    // GINX kernel choice: 0 by batch size, 1 one wave per gate, 2 two waves per gate.  Measured
+    // (tools/gate_time.py, STD128 AND): the split kernel is slower at every batch size -- 1024 gates
+    // 5.55 vs 5.17 ms, 65,536 gates 260 vs 211 ms (twice the LDS traffic: two transposes per
+    // 16-coefficient transform plus the digit exchange, two workgroup barriers per index) -- so the
+    // default never selects it (kSplitBatch = 0); FHE_HIP_GINX_KERNEL=split pins it.
+    int ginx_kernel_ = 0;
+    static constexpr uint32_t kSplitBatch = 0;
+    void* d_bsk2_ = nullptr;   // k_blind_rotate_ginx2 key layout
+    void repack_ginx2();
     // cross-stream ordering (use_stream)
     hipStream_t last_stream_ = nullptr;
     hipEvent_t order_ev_ = nullptr;

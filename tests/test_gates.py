@@ -268,3 +268,34 @@ def test_gpu_multi_engine_shards_match_single():
     sa, sb = engine("std128").eval_gate(5, a1, b1, a2, b2)
     assert np.array_equal(ao, sa) and np.array_equal(bo, sb)
     assert np.array_equal(bf.decrypt(ps, m, keys.sk, ao, bo), TRUTH[5](x1, x2).astype(np.int64))
+
+
+@pytest.mark.gpu
+def test_gpu_split_ginx_kernel_bit_exact():
+    """k_blind_rotate_ginx2 (two waves per gate, FHE_HIP_GINX_KERNEL=split) == the reference goldens and
+    == the one-wave kernel on ragged batches"""
+    import os
+    from fhe_amd import binfhe as bf
+    g, keys, (a1, b1, a2, b2) = fixture("std128")
+    engines = {}
+    for kind in ("split", "wave"):
+        os.environ["FHE_HIP_GINX_KERNEL"] = kind
+        try:
+            e = bf.GateEngine(bf.STD128, bf.GINX, device=0)
+        finally:
+            del os.environ["FHE_HIP_GINX_KERNEL"]
+        e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        engines[kind] = e
+    for i, gate, sl in per_gate(g):
+        ao, bo = engines["split"].eval_gate(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        assert np.array_equal(ao, g["out_a"][sl].astype(np.uint64)) and np.array_equal(bo, g["out_b"][sl].astype(np.uint64))
+    rng = np.random.default_rng(77)
+    for count in (1, 5, 1027):
+        x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+        c1, d1 = bf.encrypt(bf.STD128, bf.GINX, keys.sk, x1, 90 + count)
+        c2, d2 = bf.encrypt(bf.STD128, bf.GINX, keys.sk, x2, 91 + count)
+        s = engines["split"].eval_gate(bf.XOR, c1, d1, c2, d2)
+        w = engines["wave"].eval_gate(bf.XOR, c1, d1, c2, d2)
+        assert np.array_equal(s[0], w[0]) and np.array_equal(s[1], w[1]), count
+    for e in engines.values():
+        e.close()
