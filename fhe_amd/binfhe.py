@@ -145,6 +145,13 @@ def params(paramset, method):
     return Params(**{f: int(getattr(p, f)) for f, _ in _Params._fields_})
 
 
+def uses_fast_kernels(paramset, method):
+    """True when (paramset, method) runs on the 32-bit kernels (N = 1024, Q < 2^28, digitsG = 3, ...)"""
+    P = params(paramset, method)
+    return (not paramset & LARGE and P.N == 1024 and P.Q < (1 << 28) and P.digitsG == 3 and P.qKS <= 65536
+            and P.n < 1024)
+
+
 def _u64(a):
     return np.ascontiguousarray(a, dtype=np.uint64)
 
