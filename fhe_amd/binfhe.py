@@ -24,15 +24,19 @@ from ._lib import FheHipError, check, lib, ptr, sz, u64, vp
 # reference enum values (src/binfhe/include/binfhe-constants.h:49-126)
 TOY, STD128_AP, STD128, STD128_LMKCDEY = 0, 2, 3, 21
 LARGE = 1 << 30
+TIMEOPT = 1 << 14
 
 
-def large_paramset(paramset, arbFunc, logQ, N=0):
-    """paramset code of GenerateBinFHEContext(paramset, arbFunc, logQ, N, GINX, False)
-    (binfhecontext.cpp:55-104), the large-precision family (54-bit Q, N = 2048, qKS = 2^35)"""
+def large_paramset(paramset, arbFunc, logQ, N=0, timeOptimization=False):
+    """paramset code of GenerateBinFHEContext(paramset, arbFunc, logQ, N, GINX, timeOptimization)
+    (binfhecontext.cpp:55-104), the large-precision family (54-bit Q, N = 2048, qKS = 2^35).  With
+    timeOptimization (logQ != 11) the bootstrapping key is the map of BTKeyGen (:285-307): one key per
+    baseG 2^14, 2^18, 2^27, concatenated in that order (Params.bsk_words covers all three)"""
     logN = 0 if not N else N.bit_length() - 1
     if N and N != 1 << logN:
         raise ValueError("N must be a power of two")
-    return LARGE | (paramset << 16) | (int(bool(arbFunc)) << 15) | (logN << 8) | int(logQ)
+    return (LARGE | (paramset << 16) | (int(bool(arbFunc)) << 15) | (TIMEOPT if timeOptimization else 0) |
+            (logN << 8) | int(logQ))
 AP, GINX, LMKCDEY = 1, 2, 3
 OR, AND, NOR, NAND, XOR, XNOR, MAJORITY, AND3, OR3, AND4, OR4, XOR_FAST, XNOR_FAST, CMUX = range(14)
 GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR, "MAJORITY": MAJORITY,
@@ -608,9 +612,7 @@ class BinFHEContext:
             N = rest.pop(0) if rest else N
             method = rest.pop(0) if rest else GINX
             timeOptimization = rest.pop(0) if rest else timeOptimization
-            if timeOptimization:
-                raise FheHipError(-2, "timeOptimization (dynamic baseG) is not supported")
-            paramset = large_paramset(paramset, arb, logQ, N)
+            paramset = large_paramset(paramset, arb, logQ, N, timeOptimization)
         self.paramset, self.method = paramset, method
         self.params = params(paramset, method)
         self.engine = GateEngine(paramset, method, self.device)

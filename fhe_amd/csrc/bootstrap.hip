@@ -130,6 +130,12 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
+#ifndef FHE_LMK_L2PF
+#define FHE_LMK_L2PF 0   // LMKCDEY: dwords per lane of the next op's key lines touched ahead (8 KB of lines per wave each)
+#endif
+#ifndef FHE_LMK_K0EARLY
+#define FHE_LMK_K0EARLY 0  // LMKCDEY: the op's first key vectors requested before its inverse pass
+#endif
 FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
 #if FHE_ASM_MAD == 1
     int64_t d;
@@ -1202,9 +1208,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         const uint32_t* twAi = T.twA_inv;
         asm volatile("" : "+s"(twAf), "+s"(twAi));
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+#if FHE_LMK_L2PF
+        // the next op's key rows, one dword per 128-byte line in consumption order, pulled into L2
+        // while this op's transforms run; the values are retired (not used) at the end of the op
+        uint32_t pf[FHE_LMK_L2PF];
+        {
+            const uint32_t nx = __builtin_amdgcn_readfirstlane((uint32_t)gops[it + 1 < cnt ? it + 1 : it]);
+            const bool ext    = DM || !(nx & 0x8000u);
+            const uint32_t* base = ext ? reinterpret_cast<const uint32_t*>(bsk) + (size_t)nx * (4 * 8 * 64 * 4)
+                                       : reinterpret_cast<const uint32_t*>(autok) + (size_t)(nx & 0x7fffu) * (2 * 8 * 64 * 4);
+#pragma unroll
+            for (int j = 0; j < FHE_LMK_L2PF; ++j) {
+                const uint32_t Ln  = (uint32_t)(j * 64 + lane);
+                const uint32_t off = ext ? ((((Ln >> 3) & 3) * 8 + (Ln >> 5)) << 8) + ((Ln & 7) << 5)
+                                         : (((((Ln >> 3) & 1) * 8 + ((Ln >> 4) & 7)) << 8) + ((Ln & 7) << 5));
+                pf[j] = base[off];
+            }
+        }
+#endif
         uint32_t dA[32], dB[32];
         if (DM || !(op & 0x8000u)) {
             // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
+#if FHE_ROW_U4
+            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)FHE_KEY_INDEX(op) * (4 * 8 * 64);
+            uint4 kq[2][4];
+            if (FHE_LMK_K0EARLY)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
+#endif
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
             inv_pass_s<20, LZ, !DM && FHE_LMK_TWPRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
@@ -1213,10 +1244,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             fwd_pass2<FM, !DM && FHE_LMK_TWPRE>(dA, dB, tile, l, twAf, s_twBf, m);
 #if FHE_ROW_U4
             // one 16-byte vector per digit row and 4 slots (boot.h row_off)
-            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)FHE_KEY_INDEX(op) * (4 * 8 * 64);
-            uint4 kq[2][4];
+            if (!FHE_LMK_K0EARLY)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
+                for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
             // LMKCDEY: the other half's digits of slots 4(kk+1).. requested before 4kk.. are consumed
             constexpr bool PIPE = !DM && FHE_LMK_PIPE;
             uint32_t xq[2][8];
@@ -1399,6 +1429,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             }
 #endif
         }
+#if FHE_LMK_L2PF
+#pragma unroll
+        for (int j = 0; j < FHE_LMK_L2PF; ++j) asm volatile("" ::"v"(pf[j]));
+#endif
     }
     if (ACCIO) {
         acc_store(acc, g, gate, h, l, T.nR, m);

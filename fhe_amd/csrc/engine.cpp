@@ -41,6 +41,7 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         FHE_HIP_CHECK(hipSetDevice(device_));
         FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         build_tables_wide();
+        set_base(p_.baseG);
         return;
     }
     if (!fast_path(p_))
@@ -174,6 +175,11 @@ void Engine::build_tables() {
     tabs_.w1R = to_mont(h.tabI[1], Q);
     tabs_.oneR = to_mont(1, Q);
     tabs_.nR = to_mont(p_.N, Q);
+}
+
+void Engine::set_base(uint32_t bg) {
+    cur_ = p_.timeopt ? p_.with_base(bg) : p_;
+    cur_off_ = p_.bsk_offset(bg);
 }
 
 void Engine::build_tables_wide() {
@@ -501,15 +507,15 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.factor = g.factor;
         w.lb = g.lb;
         w.ub = g.ub;
-        w.digitsG = p_.digitsG;
-        w.gbits = p_.gBits;
+        w.digitsG = cur_.digitsG;
+        w.gbits = cur_.gBits;
         w.msb_out = g.msb_out;
         w.lv = g.lv64;
         w.uv = g.uv64;
         w.b_const = g.b64;
         w.qKS = p_.qKS;
         w.tv = g.tv64;
-        FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_), d_idx_, d_tvb_,
+        FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_) + cur_off_, d_idx_, d_tvb_,
                                                d_wext_a_, d_wext_b_, s));
         return;
     }

@@ -208,6 +208,16 @@ private:
     uint64_t* d_wksk_ = nullptr;
     uint64_t* d_wext_a_ = nullptr;
     uint64_t* d_wext_b_ = nullptr;
+    // the key the wide kernel bootstraps with: the context's own baseG, or (timeOptimization) the
+    // one EvalSign / EvalDecomp switched to (set_base); word offset into d_bsk_ and its digits
+    Params cur_;
+    size_t cur_off_ = 0;
+    void set_base(uint32_t bg);
+    void dynamic_base(uint64_t mod);
+    struct BaseGuard {  // Change_BaseG(curBase) when EvalSign / EvalDecomp end (:453, :518)
+        Engine* e;
+        ~BaseGuard() { e->set_base(e->p_.baseG); }
+    };
     uint64_t* d_wtv_ = nullptr;
 };
 

@@ -188,8 +188,17 @@ void Engine::eval_floor_device(size_t count, const uint64_t* a, const uint64_t* 
     fb_floor(count, a, b, mod, roundbits, a_out, b_out, fb_work(count, 2), s);
 }
 
-// EvalSign (:381-449), one bootstrapping key (no dynamic base change: the STD128 sets have one
-// baseG), outputs mod q
+// timeOptimization (:409-431, :498-514): after each ModSwitch the running modulus picks the base,
+// 2^27 up to 2^17, 2^18 up to 2^26, else unchanged (binLog = log2(mod): mod is a power of two)
+void Engine::dynamic_base(uint64_t mod) {
+    if (!p_.timeopt) return;
+    const uint32_t binLog = 63 - __builtin_clzll(mod);
+    if (binLog <= 17) set_base(1u << 27);
+    else if (binLog <= 26) set_base(1u << 18);
+}
+
+// EvalSign (:381-449), outputs mod q; the bootstrapping key changes with the modulus under
+// timeOptimization
 void Engine::eval_sign_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, bool scheme_switch,
                               uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
     const uint64_t q = p_.q;
@@ -201,11 +210,13 @@ void Engine::eval_sign_device(size_t count, const uint64_t* a, const uint64_t* b
     uint64_t *ta = w, *tb = w + count * n, *fa = tb + count, *fb = fa + count * n, *tmp = fb + count;
     FHE_HIP_CHECK(hipMemcpyAsync(ta, a, count * n * 8, hipMemcpyDeviceToDevice, s));
     FHE_HIP_CHECK(hipMemcpyAsync(tb, b, count * 8, hipMemcpyDeviceToDevice, s));
+    BaseGuard restore{this};
     while (mod > q) {
         fb_floor(count, ta, tb, mod, 0, fa, fb, tmp, s);
         const uint64_t nmod = (mod << 1) * kBeta / q;
         FHE_HIP_CHECK(launch_modswitch(mod, nmod, (uint32_t)n, (uint32_t)count, fa, fb, ta, tb, s));
         mod = nmod;
+        dynamic_base(mod);
     }
     FHE_HIP_CHECK(launch_lwe_addb(tb, kBeta % mod, mod, count, s));
     auto f3 = tv_values(scheme_switch ? TV_SIGN_SS : TV_SIGN, nullptr, 0, mod, q);
@@ -236,6 +247,7 @@ void Engine::eval_decomp_device(size_t count, const uint64_t* a, const uint64_t*
     FHE_HIP_CHECK(hipMemcpyAsync(ta, a, count * n * 8, hipMemcpyDeviceToDevice, s));
     FHE_HIP_CHECK(hipMemcpyAsync(tb, b, count * 8, hipMemcpyDeviceToDevice, s));
     size_t part = 0;
+    BaseGuard restore{this};
     while (mod > q) {
         FHE_HIP_CHECK(launch_lwe_reduce(ta, tb, a_out + part * count * n, b_out + part * count, q, (uint32_t)n, count, s));
         ++part;
@@ -243,6 +255,7 @@ void Engine::eval_decomp_device(size_t count, const uint64_t* a, const uint64_t*
         const uint64_t nmod = mod / q * 2 * kBeta;
         FHE_HIP_CHECK(launch_modswitch(mod, nmod, (uint32_t)n, (uint32_t)count, fa, fb, ta, tb, s));
         mod = nmod;
+        dynamic_base(mod);
     }
     FHE_HIP_CHECK(hipMemcpyAsync(a_out + part * count * n, ta, count * n * 8, hipMemcpyDeviceToDevice, s));
     FHE_HIP_CHECK(hipMemcpyAsync(b_out + part * count, tb, count * 8, hipMemcpyDeviceToDevice, s));

@@ -62,7 +62,40 @@ void keygen_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& sk) {
         sk[i] = lift(p.keyDist == KD_GAUSSIAN ? r.cbd() : r.ternary(), p.qKS);
 }
 
+namespace {
+void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed, uint64_t bseed, bool with_ksk,
+                KeySet& out);
+}
+
+// timeOptimization (BTKeyGen, binfhecontext.cpp:285-307): one key per baseG of the map, all under
+// one RLWE secret skN and sharing one switching key; the key of the context's own baseG is the
+// one keygen without timeOptimization makes from the same seed
 void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed, KeySet& out) {
+    if (!p.timeopt) {
+        keygen_one(p, sk, seed, seed, true, out);
+        return;
+    }
+    out.bsk.assign(p.bsk_words(), 0);
+    for (uint32_t bg : kSignBases) {
+        Params pb = p.with_base(bg);
+        pb.timeopt = false;
+        KeySet t;
+        const bool own = bg == p.baseG;
+        keygen_one(pb, sk, seed, own ? seed : seed ^ ((uint64_t)bg * kRngGamma), own, t);
+        std::copy(t.bsk.begin(), t.bsk.end(), out.bsk.begin() + p.bsk_offset(bg));
+        if (own) {
+            out.sk = std::move(t.sk);
+            out.skN = std::move(t.skN);
+            out.kskA = std::move(t.kskA);
+            out.kskB = std::move(t.kskB);
+        }
+    }
+}
+
+namespace {
+// seed: skN and the switching key; bseed: the bootstrapping key's randomness
+void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed, uint64_t bseed, bool with_ksk,
+                KeySet& out) {
     if (sk.size() != p.n) throw std::invalid_argument("secret key has wrong length");
     const uint32_t n = p.n, N = p.N, dG2 = p.digitsG2;
     const uint64_t Q = p.Q;
@@ -97,7 +130,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
             std::vector<uint64_t> msg(N);
             for (int ks = 0; ks < 2; ++ks) {
                 const bool m = ks == 0 ? s == 1 : s == -1;  // 0 -> {0,0}, 1 -> {1,0}, -1 -> {0,1}
-                Rng r(seed, T_BSK, (uint64_t)i * 2 + ks);
+                Rng r(bseed, T_BSK, (uint64_t)i * 2 + ks);
                 uint64_t* key = out.bsk.data() + ((size_t)i * 2 + ks) * rg;
                 for (uint32_t row = 0; row < dG2; ++row) {
                     // message G^{(row>>1)+1} on coefficient 0: constant in EVALUATION domain
@@ -123,7 +156,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
                     bool neg = false;
                     if (mm >= (int64_t)N) { mm -= N; neg = true; }
                     const size_t slot = ((size_t)i * bR + j) * dR + k;
-                    Rng r(seed, T_BSK, slot);
+                    Rng r(bseed, T_BSK, slot);
                     uint64_t* key = out.bsk.data() + slot * rg;
                     for (uint32_t row = 0; row < dG2; ++row) {
                         std::fill(msg.begin(), msg.end(), 0);
@@ -143,7 +176,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
             int64_t mm = lift(s, p.q) * (2 * N / p.q);
             bool neg = false;
             if (mm >= (int64_t)N) { mm -= N; neg = true; }
-            Rng r(seed, T_BSK, (uint64_t)i);
+            Rng r(bseed, T_BSK, (uint64_t)i);
             uint64_t* key = out.bsk.data() + (size_t)i * rg;
             std::vector<uint64_t> msg(N);
             for (uint32_t row = 0; row < dG2; ++row) {
@@ -161,7 +194,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
             uint32_t kk = k == 0 ? 2 * N - 5 : (uint32_t)powmod(5, k, 2 * N);
             std::vector<uint64_t> skAuto(N), e(N);
             auto_eval(p, kk, S.data(), skAuto.data());
-            Rng r(seed, T_AUTO, k);
+            Rng r(bseed, T_AUTO, k);
             uint64_t* key = autok + k * ak;
             for (uint32_t row = 0; row + 1 < p.digitsG; ++row) {
                 uint64_t* r0 = key + (size_t)row * 2 * N;
@@ -176,6 +209,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
         }
     }
 
+    if (!with_ksk) return;
     // ---- key-switching key (KeySwitchGen): rows [N][baseKS][digitsKS], A row of n, B
     const uint64_t qk = p.qKS;
     out.kskA.assign(p.ksk_rows() * n, 0);
@@ -207,6 +241,7 @@ void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t
             }
     }
 }
+}  // namespace
 
 void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
              uint64_t* b, uint32_t ptmod, uint64_t mod) {

@@ -9,6 +9,41 @@
 namespace fhe_amd {
 
 size_t Params::bsk_words() const {
+    if (!timeopt) return bsk_words_one();
+    size_t w = 0;
+    for (uint32_t bg : kSignBases) w += with_base(bg).bsk_words_one();
+    return w;
+}
+
+size_t Params::bsk_offset(uint32_t bg) const {
+    if (!timeopt) {
+        if (bg != baseG) throw std::invalid_argument("no bootstrapping key for this baseG");
+        return 0;
+    }
+    size_t w = 0;
+    for (uint32_t b : kSignBases) {
+        if (b == bg) return w;
+        w += with_base(b).bsk_words_one();
+    }
+    throw std::invalid_argument("no bootstrapping key for this baseG");
+}
+
+Params Params::with_base(uint32_t bg) const {
+    Params p = *this;
+    p.baseG = bg;
+    p.gBits = ilog2(bg);
+    p.digitsG = (uint32_t)std::ceil(std::log((double)p.Q) / std::log((double)bg));  // rgsw-cryptoparameters.h:226-228
+    p.digitsG2 = (p.digitsG - 1) * 2;
+    p.gpow.clear();
+    uint64_t v = 1;
+    for (uint32_t i = 0; i < p.digitsG; ++i) {
+        p.gpow.push_back(v);
+        v = mulmod(v, bg, p.Q);
+    }
+    return p;
+}
+
+size_t Params::bsk_words_one() const {
     if (method == M_GINX) return (size_t)n * 2 * digitsG2 * 2 * N;
     // AP: [n][baseR][digitsR][digitsG2][2][N], the j = 0 slots unused (rgsw-acc-dm.cpp:39-58)
     if (method == M_AP) return (size_t)n * baseR * digitsR * digitsG2 * 2 * N;
@@ -71,6 +106,7 @@ Params make_params_large(int code, int method) {
     p.digitsG2 = (p.digitsG - 1) * 2;
     p.numAutoKeys = 10;
     p.keyDist = KD_UNIFORM_TERNARY;
+    p.timeopt = (code & kTimeOpt) != 0 && logQ != 11;  // RingGSWCryptoParams(..., signEval = logQ != 11 && timeOpt)
     p.baseR = 23;
     p.digitsR = (uint32_t)std::ceil(std::log((double)p.q) / std::log((double)p.baseR));
     p.psi = root_of_unity(2 * N, p.Q);

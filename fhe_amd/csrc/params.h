@@ -17,9 +17,15 @@ enum ParamSet : int { PS_TOY = 0, PS_STD128_AP = 2, PS_STD128 = 3, PS_STD128_LMK
 // (binfhecontext.cpp:55-104) as one paramset code:
 //   kLargeFamily | set << 16 | arbFunc << 15 | log2(N) << 8 (0: the minimum secure N) | logQ
 constexpr int kLargeFamily = 1 << 30;
-inline int large_paramset(int set, bool arbFunc, uint32_t logQ, uint32_t logN = 0) {
-    return kLargeFamily | (set << 16) | ((arbFunc ? 1 : 0) << 15) | (int)(logN << 8) | (int)logQ;
+// timeOptimization = true (binfhecontext.cpp:55-104, BTKeyGen :285-307): for logQ != 11 the
+// context holds one bootstrapping key per baseG in {2^14, 2^18, 2^27} (m_BTKey_map), and
+// EvalSign / EvalDecomp change the base as the modulus shrinks (binfhe-base-scheme.cpp:409-431)
+constexpr int kTimeOpt = 1 << 14;
+inline int large_paramset(int set, bool arbFunc, uint32_t logQ, uint32_t logN = 0, bool timeopt = false) {
+    return kLargeFamily | (set << 16) | ((arbFunc ? 1 : 0) << 15) | (timeopt ? kTimeOpt : 0) | (int)(logN << 8) |
+           (int)logQ;
 }
+constexpr uint32_t kSignBases[3] = {1u << 14, 1u << 18, 1u << 27};  // rgsw-cryptoparameters.cpp:50
 inline bool is_large(int paramset) { return (paramset & kLargeFamily) != 0; }
 enum Method : int { M_AP = 1, M_GINX = 2, M_LMKCDEY = 3 };
 enum Gate : int { G_OR = 0, G_AND, G_NOR, G_NAND, G_XOR, G_XNOR, G_MAJORITY, G_AND3, G_OR3, G_AND4, G_OR4,
@@ -35,9 +41,15 @@ struct Params {
     int keyDist = KD_UNIFORM_TERNARY;
     uint64_t Q = 0, psi = 0;
     std::vector<uint64_t> gpow;  // Gpow[i] = baseG^i mod Q (rgsw-cryptoparameters.cpp:69-74)
+    bool timeopt = false;        // the three-key map of timeOptimization (kSignBases)
 
-    // raw (reference-layout) key sizes in u64 words
+    // raw (reference-layout) key sizes in u64 words; with timeopt the map's keys, concatenated in
+    // the map's (ascending baseG) order
     size_t bsk_words() const;
+    size_t bsk_words_one() const;            // one key at this baseG
+    size_t bsk_offset(uint32_t bg) const;    // timeopt: first word of the key for baseG bg
+    // RingGSWCryptoParams::Change_BaseG (rgsw-cryptoparameters.h:222-229): baseG, digitsG, Gpow
+    Params with_base(uint32_t bg) const;
     size_t ksk_rows() const { return (size_t)N * baseKS * digitsKS; }
     uint64_t gate_const(int gate) const;  // rgsw-cryptoparameters.cpp:78-92
 };

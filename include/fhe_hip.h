@@ -92,9 +92,14 @@ typedef struct {
 /* The large-precision family GenerateBinFHEContext(set, arbFunc, logQ, N, GINX, false)
  * (binfhecontext.cpp:55-104: Q = LastPrime(54, 2N), N = 2048, qKS = 2^35, n = 1305 (TOY: 32),
  * baseG 2^14 / 2^18 / 2^27 by logQ) is addressed by the paramset code
- *   FHE_HIP_LARGE | set << 16 | arbFunc << 15 | log2(N) << 8 (0: minimum N) | logQ
- * in every entry point that takes a paramset. */
+ *   FHE_HIP_LARGE | set << 16 | arbFunc << 15 | FHE_HIP_TIMEOPT? | log2(N) << 8 (0: minimum N) | logQ
+ * in every entry point that takes a paramset.  FHE_HIP_TIMEOPT is timeOptimization = true: for
+ * logQ != 11 the bootstrapping key is BTKeyGen's map (binfhecontext.cpp:285-307), one key per baseG
+ * 2^14, 2^18, 2^27 concatenated in that order in the raw bsk (bsk_words covers the three), and
+ * EvalSign / EvalDecomp switch keys as the modulus shrinks (binfhe-base-scheme.cpp:409-431, 498-514);
+ * gates and the other operations use the key of the set's own baseG. */
 #define FHE_HIP_LARGE (1 << 30)
+#define FHE_HIP_TIMEOPT (1 << 14)
 
 /* parameters of a set (host only; GenerateBinFHEContext, binfhecontext.cpp:107-179) */
 int fhe_hip_params_get(int paramset, int method, fhe_hip_params* out);

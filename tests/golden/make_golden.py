@@ -217,16 +217,20 @@ def make_fb(names=("std128", "lmkcdey")):
 # name -> (set, arbFunc, logQ); covers every baseG regime (2^27 / 2^18 / 2^14 at N = 2048) and
 # logQ = 11 (27-bit Q, N = 1024, baseG = 2^5); one STD128 (n = 1305) case
 LARGE_SETS = {"toy12arb": (0, True, 12), "toy17": (0, False, 17), "toy29": (0, False, 29), "toy11": (0, False, 11),
-              "std29": (3, False, 29)}
+              "std29": (3, False, 29),
+              # timeOptimization (:292-303): the three-key map; EvalSign / EvalDecomp from 2^29 walk
+              # 2^14 -> 2^18 -> 2^27, from 2^17 they go 2^18 -> 2^27 (binfhe-base-scheme.cpp:409-431)
+              "toy29t": (0, False, 29, True), "toy17t": (0, False, 17, True)}
 
 
 def large_inputs(name):
     """keys (seeded host keygen) and the inputs of each large-family fixture: gate bits (mod q),
     and values mod 2^logQ with plaintext modulus P = 2^logQ / (q / (2 beta)) around P/2"""
     from fhe_amd import binfhe as bf
-    st, arb, logQ = LARGE_SETS[name]
-    ps = bf.large_paramset(st, arb, logQ)
-    key_seed = 0xB1600000 + logQ + (st << 8) + (int(arb) << 7)
+    st, arb, logQ, *topt = LARGE_SETS[name]
+    topt = bool(topt and topt[0])
+    ps = bf.large_paramset(st, arb, logQ, 0, topt)
+    key_seed = 0xB1600000 + logQ + (st << 8) + (int(arb) << 7) + (int(topt) << 6)
     keys = bf.keygen(ps, GINX, key_seed)
     P = bf.params(ps, GINX)
     cnt = 2 if st == 3 else 4

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-TOY = ["toy12arb", "toy17", "toy29", "toy11"]
+TOY = ["toy12arb", "toy17", "toy29", "toy11", "toy29t", "toy17t"]   # *t: timeOptimization (three-key map)
 TRUTH = {"AND": lambda a, b: a & b, "XOR": lambda a, b: a ^ b}
 
 
@@ -46,6 +46,30 @@ def test_large_params_match_reference_table():
         bf.params(bf.large_paramset(bf.TOY, False, 30), bf.GINX)
     with pytest.raises(Exception):
         bf.params(bf.large_paramset(bf.TOY, False, 17), bf.LMKCDEY)
+
+
+def test_time_optimization_key_map_layout():
+    """timeOptimization (binfhecontext.cpp:55-104, 285-307): for logQ != 11 the raw key is the map of
+    one key per baseG 2^14 / 2^18 / 2^27 (digitsG 4 / 3 / 2 for the 54-bit Q), concatenated in that
+    order, whose slice for the set's own baseG is the key keygen makes without timeOptimization;
+    logQ = 11 keeps its single key (signEval = logQ != 11 && timeOptimization)"""
+    from fhe_amd import binfhe as bf
+    words = {bg: bf.params(bf.large_paramset(bf.TOY, False, lq), bf.GINX).bsk_words
+             for bg, lq in ((1 << 14, 29), (1 << 18, 17), (1 << 27, 12))}
+    for logQ in (12, 17, 29):
+        P = bf.params(bf.large_paramset(bf.TOY, False, logQ, 0, True), bf.GINX)
+        assert P.bsk_words == sum(words.values())
+        plain = bf.large_paramset(bf.TOY, False, logQ)
+        own = bf.params(plain, bf.GINX)
+        off = sum(w for bg, w in words.items() if bg < own.baseG)
+        kt = bf.keygen(bf.large_paramset(bf.TOY, False, logQ, 0, True), bf.GINX, 77)
+        k1 = bf.keygen(plain, bf.GINX, 77)
+        assert np.array_equal(kt.bsk[off:off + own.bsk_words], k1.bsk)
+        assert np.array_equal(kt.kskA, k1.kskA) and np.array_equal(kt.sk, k1.sk)
+        rest = np.concatenate([kt.bsk[:off], kt.bsk[off + own.bsk_words:]])
+        assert not np.array_equal(rest[:own.N], k1.bsk[:own.N])   # the other bases: their own randomness
+    P11 = bf.params(bf.large_paramset(bf.TOY, False, 11, 0, True), bf.GINX)
+    assert P11.bsk_words == bf.params(bf.large_paramset(bf.TOY, False, 11), bf.GINX).bsk_words
 
 
 @pytest.mark.parametrize("name", TOY)
@@ -132,6 +156,22 @@ def test_gpu_large_std128_bit_exact():
     assert np.array_equal(ao, g["sign_a"]) and np.array_equal(bo, g["sign_b"])
     _engines.pop(name)
     _cache.pop(name)
+
+
+@pytest.mark.gpu
+def test_gpu_time_optimization_context_api():
+    """GenerateBinFHEContext(TOY, false, 29, 0, GINX, true): BTKeyGen makes the three-key map on the
+    device path and EvalSign / EvalDecomp switch bases as the modulus shrinks (eval-sign.cpp flow)"""
+    from fhe_amd import binfhe as bf
+    cc = bf.BinFHEContext()
+    cc.GenerateBinFHEContext(bf.TOY, False, 29, 0, bf.GINX, True)
+    sk = cc.KeyGen()
+    cc.BTKeyGen(sk)
+    Q = 1 << 29
+    P = Q // (cc.params.q // 256)
+    for x in (0, 5, P // 4, P // 2, 3 * P // 4):
+        ct = cc.Encrypt(sk, x, p=P, mod=Q)
+        assert cc.Decrypt(sk, cc.EvalSign(ct), p=2) == int(x >= P // 2), x
 
 
 @pytest.mark.gpu

@@ -3,7 +3,7 @@ batches and EvalSign on the STD128 large set GenerateBinFHEContext(STD128, false
 N = 2048, 54-bit Q, qKS = 2^35).  Synthetic seeded keys and inputs; host round trip included
 (inputs are 10 KB per ciphertext, negligible next to a 1305-step blind rotation).
 
-    python tools/bench_large.py [--logq 29] [--batch 2048] [--steps 3]
+    python tools/bench_large.py [--logq 29] [--batch 2048] [--steps 3] [--time-opt]
 """
 import argparse
 import json
@@ -23,9 +23,10 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--sign-batch", type=int, default=256)
     ap.add_argument("--toy", action="store_true")
+    ap.add_argument("--time-opt", action="store_true", help="timeOptimization: the three-key map")
     args = ap.parse_args()
     from fhe_amd import binfhe as bf
-    ps = bf.large_paramset(bf.TOY if args.toy else bf.STD128, False, args.logq)
+    ps = bf.large_paramset(bf.TOY if args.toy else bf.STD128, False, args.logq, 0, args.time_opt)
     t0 = time.time()
     keys = bf.keygen(ps, bf.GINX, 0x1A46E)
     e = bf.GateEngine(ps, bf.GINX)
@@ -55,7 +56,8 @@ def main():
     far &= (xs > PL // 16) & (xs < PL - PL // 16)
     sign_ok = bool(np.array_equal(bf.decrypt(ps, bf.GINX, keys.sk, sa, sb, mod=P.q, p=2)[far], (xs >= PL // 2)[far]))
     print(json.dumps({"workload": f"{'TOY' if args.toy else 'STD128'} large-precision logQ={args.logq}", "n": P.n, "N": P.N,
-                      "Q_bits": P.Q.bit_length(), "digitsG": P.digitsG, "batch": B, "gates_per_s": B / gate_s,
+                      "Q_bits": P.Q.bit_length(), "digitsG": P.digitsG,
+                      "time_optimization": args.time_opt, "batch": B, "gates_per_s": B / gate_s,
                       "ms_per_batch": gate_s * 1e3, "gates_decrypt_ok": ok, "evalsign_batch": S,
                       "evalsign_per_s": S / sign_s, "evalsign_ok": sign_ok, "setup_s": setup}))
 
