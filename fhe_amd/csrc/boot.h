@@ -133,9 +133,13 @@ hipError_t launch_pack_rgsw(const uint64_t* raw, size_t count, uint32_t N, uint3
 hipError_t launch_single_ops(uint16_t* ops, uint32_t* nops, uint32_t count, uint32_t maxops, hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out) (:254-261), KSK as u16 rows of 512;
 // q_out = 0: no final switch (output mod qKS)
+// part: optional scratch of part_words u32 for the row-split tiled kernel below 4096 gates (null:
+// the per-gate kernel there)
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
                             const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
-                            uint64_t* b_out, hipStream_t s);
+                            uint64_t* b_out, hipStream_t s, uint32_t* part = nullptr, size_t part_words = 0);
+// the row-split factor launch_keyswitch uses for count gates with that scratch
+uint32_t keyswitch_split(size_t count, uint32_t n, uint32_t N, size_t part_words);
 // LWE element-wise operations on [count][len] / [count] u64 arrays (lwe.hip):
 //   reduce: (a, b) mod m (LWECiphertextImpl::SetModulus, lwe-ciphertext.h:116-120)
 //   sub:    x - y mod m, inputs < m (EvalSubEq / EvalSubEq2, lwe-pke.cpp:234-242); outputs may alias

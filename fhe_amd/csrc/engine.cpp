@@ -61,7 +61,7 @@ Engine::~Engine() {
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
                       (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
-                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_})
+                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_})
         if (ptr) (void)hipFree(ptr);
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -705,7 +705,19 @@ void Engine::keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64
         return;
     }
     GateArgs g = gate_args(G_AND, count);
-    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, q_out, a_out, b_out, s));
+    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, q_out, a_out, b_out, s,
+                                   ks_part(count), kKsPartWords));
+}
+
+// scratch of the row-split key switch (launch_keyswitch, below 4096 gates): S count <= 2^16 for
+// every count, so 2^16 partial rows of ksk_width / 2 words
+uint32_t* Engine::ks_part(size_t count) {
+    if (count >= 4096) return nullptr;
+    if (!d_kspart_) {
+        sync_streams();
+        FHE_HIP_CHECK(hipMalloc(&d_kspart_, kKsPartWords * sizeof(uint32_t)));
+    }
+    return d_kspart_;
 }
 
 void Engine::copy_ext_host(size_t count, uint64_t* ext_a, uint64_t* ext_b) {
@@ -810,7 +822,8 @@ void Engine::keyswitch_host(size_t count, const uint64_t* a, const uint64_t* b, 
     FHE_HIP_CHECK(hipMemcpyAsync(d_ext_a_, ha.data(), count * N * 4, hipMemcpyHostToDevice, stream_));
     FHE_HIP_CHECK(hipMemcpyAsync(d_ext_b_, hb.data(), count * 4, hipMemcpyHostToDevice, stream_));
     GateArgs g = gate_args(G_AND, count);
-    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, 0, dao, dbo, stream_));
+    FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, 0, dao, dbo, stream_,
+                                   ks_part(count), kKsPartWords));
     FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * p_.n * 8, hipMemcpyDeviceToHost, stream_));
     FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
     FHE_HIP_CHECK(hipStreamSynchronize(stream_));

@@ -166,6 +166,9 @@ private:
     uint16_t* d_ops_ = nullptr;
     uint32_t* d_nops_ = nullptr;
     uint16_t* d_ksk_ = nullptr;
+    uint32_t* d_kspart_ = nullptr;   // row-split key-switch partials (ks_part)
+    static constexpr size_t kKsPartWords = (size_t)1 << 25;  // 2^16 rows x 512 u32
+    uint32_t* ks_part(size_t count);
     // GINX kernel choice: 0 by batch size, 1 one wave per gate, 2 two waves per gate.  Measured
     // (tools/gate_time.py, STD128 AND): the split kernel is slower at every batch size -- 1024 gates
     // 5.55 vs 5.17 ms, 65,536 gates 260 vs 211 ms (twice the LDS traffic: two transposes per

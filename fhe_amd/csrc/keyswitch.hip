@@ -114,11 +114,16 @@ constexpr int kKsDigits = 3, kKsLogBase = 5;    // digitsKS, log2(baseKS)
 constexpr int kKsIPR   = FHE_KS_IPR;            // values of i per round (4: one uint4 of a_i)
 constexpr int kKsStep  = kKsIPR * kKsDigits;    // (i, j) steps per round / LDS buffer / barrier
 
+// Row split (blockIdx.z, small batches): a workgroup sums the rounds [z R/S, (z+1) R/S) only and
+// writes its packed partial sums to part [S][count][W/2]; k_keyswitch_reduce adds the S partials
+// (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
+// 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
+// staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
 template <int G>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
-                      uint64_t* __restrict__ b_out) {
+                      uint64_t* __restrict__ b_out, uint32_t* __restrict__ part) {
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
     __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][32 * kKsRowB];
@@ -126,15 +131,16 @@ __global__ void __launch_bounds__(G)
     const uint32_t gate = blockIdx.x * G + t;
     const bool valid = gate < g.count;
     const uint32_t col0 = blockIdx.y * kKsCols;
-    const uint32_t rounds = g.N / kKsIPR;
+    const uint32_t rounds = g.N / kKsIPR / gridDim.z;    // this workgroup's share of the rounds
+    const uint32_t r0 = blockIdx.z * rounds;
     using AV = typename std::conditional<kKsIPR == 4, uint4, uint2>::type;
     static_assert(kKsIPR == 4 || kKsIPR == 2, "a_i vector width");
-    const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N);
+    const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N) + r0;
 
     // staging role: part x = t + G*r -> slice x / kKsPartsPerSlice, 16-byte part x % kKsPartsPerSlice
     auto slice_src = [&](uint32_t round, int q, int r) -> const uint4* {
         const uint32_t x = t + G * r, sd = x / kKsPartsPerSlice, sp = x % kKsPartsPerSlice;
-        const uint32_t i = round * kKsIPR + q / kKsDigits, j = q % kKsDigits;
+        const uint32_t i = (r0 + round) * kKsIPR + q / kKsDigits, j = q % kKsDigits;
         const size_t row = ((size_t)i * (1u << kKsLogBase) + sd) * kKsDigits + j;
         return reinterpret_cast<const uint4*>(ksk + row * ksk_width(g.n) + col0) + sp;
     };
@@ -219,6 +225,14 @@ __global__ void __launch_bounds__(G)
         }
     }
     if (!valid) return;
+    if (part) {
+        uint4* pp = reinterpret_cast<uint4*>(part + ((size_t)blockIdx.z * g.count + gate) * (ksk_width(g.n) / 2) +
+                                             col0 / 2);
+#pragma unroll
+        for (int k = 0; k < kKsCols / 8; ++k)
+            pp[k] = make_uint4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
+        return;
+    }
     const uint32_t qm = g.qKS - 1;
     const uint32_t b = ms_b[gate];
     uint64_t* oa = a_out + (size_t)gate * g.n;
@@ -236,9 +250,43 @@ __global__ void __launch_bounds__(G)
     }
 }
 
+// the S row-split partials of a gate, one thread per packed column pair, then the epilogue
+__global__ void __launch_bounds__(512)
+    k_keyswitch_reduce(GateArgs g, const uint32_t* __restrict__ part, uint32_t S, const uint32_t* __restrict__ ms_b,
+                       uint64_t q_out, uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
+    const uint32_t gate = blockIdx.x, t = threadIdx.x, hw = blockDim.x;
+    uint32_t acc = 0;
+    for (uint32_t z = 0; z < S; ++z) {
+        const uint32_t w = part[((size_t)z * g.count + gate) * hw + t];
+        asm("v_pk_add_u16 %0, %1, %2" : "=v"(acc) : "v"(acc), "v"(w));
+    }
+    const uint32_t qm = g.qKS - 1;
+    const uint32_t b = ms_b[gate];
+    uint64_t* oa = a_out + (size_t)gate * g.n;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t c = 2 * t + h;
+        const uint32_t neg = h ? (acc >> 16) : (acc & 0xffffu);  // -sum mod 2^16
+        uint64_t v = ((c == g.n ? b : 0u) + neg) & qm;
+        if (q_out) v = mod_switch_up(v, g.qKS, q_out);
+        if (c < g.n) oa[c] = v;
+        else if (c == g.n) b_out[gate] = v;
+    }
+}
+
+// row-split factor of the tiled kernel for `count` gates: enough workgroups for 4 per CU, at
+// least 8 rounds each, within the scratch the caller holds (part_words u32)
+uint32_t keyswitch_split(size_t count, uint32_t n, uint32_t N, size_t part_words) {
+    const size_t tiles = ((count + FHE_KS_G - 1) / FHE_KS_G) * (ksk_width(n) / kKsCols);
+    uint32_t S = 1;
+    while (tiles * S < 1024 && N / kKsIPR / (2 * S) >= 8 && (size_t)2 * S * count * (ksk_width(n) / 2) <= part_words)
+        S *= 2;
+    return S;
+}
+
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
                             const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
-                            uint64_t* b_out, hipStream_t s) {
+                            uint64_t* b_out, hipStream_t s, uint32_t* part, size_t part_words) {
     if (g.count == 0) return hipSuccess;
     if (baseKS & (baseKS - 1)) return hipErrorInvalidValue;
     if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 1024 || g.N > 1024) return hipErrorInvalidValue;
@@ -248,11 +296,19 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
 #define FHE_KS_TILE 0   // 0: choose by batch size; 1: per-gate kernel; 256: gate tile
 #endif
     int tile = FHE_KS_TILE;
-    if (tile == 0) tile = g.count >= 4096 ? 256 : 1;  // tiles need >= 16 x 8 workgroups to pay
+    // tiles need >= 16 x 8 workgroups to pay, or a row split (scratch) below 4096 gates
+    if (tile == 0) tile = g.count >= 4096 || part ? 256 : 1;
     if (tile > 1 && (logBase != (uint32_t)kKsLogBase || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
     if (tile > 1) {
-        hipLaunchKernelGGL(k_keyswitch_tiled<FHE_KS_G>, dim3((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols),
-                           dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, a_out, b_out);
+        const uint32_t S = part ? keyswitch_split(g.count, g.n, g.N, part_words) : 1;
+        hipLaunchKernelGGL(k_keyswitch_tiled<FHE_KS_G>, dim3((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols, S),
+                           dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, a_out, b_out, S > 1 ? part : nullptr);
+        if (S > 1) {
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_keyswitch_reduce, dim3(g.count), dim3(W / 2), 0, s, g, part, S, ms_b, q_out, a_out,
+                               b_out);
+        }
     } else {
         hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(W / 2), 0, s, g, logBase, digitsKS,
                            reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
