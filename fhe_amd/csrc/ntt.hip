@@ -621,6 +621,261 @@ __global__ void __launch_bounds__(512)
         step(bufB, poly + W);
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// One polynomial per wave64 for 64-bit moduli (2^30 <= Q < 2^62): the layouts A / B / C of
+// k_ntt1024w with 16 u64 coefficients per lane, Harvey-lazy butterflies in 64 bits (forward values
+// in [0, 4Q), inverse in [0, 2Q): 4Q < 2^64) around Shoup's lazy product x w - hi(x w') Q in
+// [0, 2Q).  The transposes move the low and the high words as two 32-bit planes through the same
+// conflict-free tile (word address x + 4 (x >> 6)).
+// ---------------------------------------------------------------------------------------------
+struct Lazy64 {
+    uint64_t Q, Q2;
+    ulonglong2 lo, hi;  // (N^-1, pre), (w1 N^-1, pre)
+    FHE_DEV static uint64_t csub(uint64_t x, uint64_t m) { return x >= m ? x - m : x; }
+    FHE_DEV uint64_t lazy_mul(uint64_t x, ulonglong2 w) const {
+        if (FHE_NTT_COPY) return x;
+        return x * w.x - __umul64hi(x, w.y) * Q;
+    }
+    FHE_DEV void ct(uint64_t& x, uint64_t& y, ulonglong2 w) const {
+        x = csub(x, Q2);
+        const uint64_t t = lazy_mul(y, w);
+        y = x + Q2 - t;
+        x = x + t;
+    }
+    FHE_DEV void gs(uint64_t& x, uint64_t& y, ulonglong2 w) const {
+        const uint64_t d = x + Q2 - y;
+        x = csub(x + y, Q2);
+        y = lazy_mul(d, w);
+    }
+    FHE_DEV void gs_last(uint64_t& x, uint64_t& y) const {
+        const uint64_t d = x + Q2 - y;
+        x = csub(lazy_mul(x + y, lo), Q);
+        y = csub(lazy_mul(d, hi), Q);
+    }
+    FHE_DEV uint64_t fwd_out(uint64_t x) const { return csub(csub(x, Q2), Q); }
+};
+
+FHE_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+FHE_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+FHE_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+
+#ifndef FHE_NTT64_PF
+#define FHE_NTT64_PF 1   // k_ntt1024w64: the next polynomial's rows loaded during this one
+#endif
+#ifndef FHE_NTT64_WPS
+#define FHE_NTT64_WPS 4  // k_ntt1024w64: waves per SIMD (register budget and grid size)
+#endif
+
+template <bool INV>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NTT64_WPS)))
+    k_ntt1024w64(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
+                 const ulonglong2* __restrict__ tab, Lazy64 m) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ulonglong2* s_tw = reinterpret_cast<ulonglong2*>(smem);                            // 1024 entries
+    uint32_t* tiles  = reinterpret_cast<uint32_t*>(smem + 1024 * sizeof(ulonglong2));  // 8 x kWTile
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) s_tw[i] = tab[i];
+
+    const int L    = threadIdx.x & 63;
+    const int wv   = threadIdx.x >> 6;
+    uint32_t* tile = tiles + wv * kWTile;
+    const int G = L >> 2, j = L & 3;  // layout B lane fields
+    const uint32_t W = gridDim.x * (blockDim.x >> 6);
+    uint32_t poly    = blockIdx.x * (blockDim.x >> 6) + wv;
+    auto rowp        = [&](uint32_t p) -> uint32_t { return p < count ? p : count - 1; };
+
+    // A (word address (r << 6) | L) <-> B ((G << 6) | (r << 2) | j), one 32-bit plane at a time
+    auto a_to_b = [&](uint64_t (&v)[16]) {
+        uint32_t h[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { tile[wt((r << 6) | L)] = lo32(v[r]); h[r] = hi32(v[r]); }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = tile[wt((G << 6) | (r << 2) | j)];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tile[wt((r << 6) | L)] = h[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] |= (uint64_t)tile[wt((G << 6) | (r << 2) | j)] << 32;
+        wave_sync();
+    };
+    auto b_to_a = [&](uint64_t (&v)[16]) {
+        uint32_t h[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { tile[wt((G << 6) | (r << 2) | j)] = lo32(v[r]); h[r] = hi32(v[r]); }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = tile[wt((r << 6) | L)];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tile[wt((G << 6) | (r << 2) | j)] = h[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] |= (uint64_t)tile[wt((r << 6) | L)] << 32;
+        wave_sync();
+    };
+    // B <-> C (C: 4 consecutive words (hh << 8) | (L << 2) .. + 3, 16-byte runs)
+    auto b_to_c = [&](uint64_t (&v)[16]) {
+        uint32_t h[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { tile[wt((G << 6) | (r << 2) | j)] = lo32(v[r]); h[r] = hi32(v[r]); }
+        wave_sync();
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh) {
+            const uint4 q = *reinterpret_cast<const uint4*>(tile + wt((hh << 8) | (L << 2)));
+            v[4 * hh] = q.x; v[4 * hh + 1] = q.y; v[4 * hh + 2] = q.z; v[4 * hh + 3] = q.w;
+        }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tile[wt((G << 6) | (r << 2) | j)] = h[r];
+        wave_sync();
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh) {
+            const uint4 q = *reinterpret_cast<const uint4*>(tile + wt((hh << 8) | (L << 2)));
+            v[4 * hh] |= (uint64_t)q.x << 32; v[4 * hh + 1] |= (uint64_t)q.y << 32;
+            v[4 * hh + 2] |= (uint64_t)q.z << 32; v[4 * hh + 3] |= (uint64_t)q.w << 32;
+        }
+        wave_sync();
+    };
+    auto c_to_b = [&](uint64_t (&v)[16]) {
+        uint32_t h[16];
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh) {
+            *reinterpret_cast<uint4*>(tile + wt((hh << 8) | (L << 2))) =
+                make_uint4(lo32(v[4 * hh]), lo32(v[4 * hh + 1]), lo32(v[4 * hh + 2]), lo32(v[4 * hh + 3]));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h[4 * hh + e] = hi32(v[4 * hh + e]);
+        }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = tile[wt((G << 6) | (r << 2) | j)];
+        wave_sync();
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh)
+            *reinterpret_cast<uint4*>(tile + wt((hh << 8) | (L << 2))) =
+                make_uint4(h[4 * hh], h[4 * hh + 1], h[4 * hh + 2], h[4 * hh + 3]);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] |= (uint64_t)tile[wt((G << 6) | (r << 2) | j)] << 32;
+        wave_sync();
+    };
+    // Global I/O needs no third transpose: the forward transform reads rows in layout A and writes
+    // layout C (4 consecutive u64 per lane and x9x8: 32-byte runs), the inverse reads C and writes A
+    using Raw = uint64_t[16];
+    auto load = [&](Raw& buf, uint32_t p) {
+        const uint64_t* src = in + (size_t)rowp(p) * 1024;
+        if (!INV) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) buf[r] = src[(r << 6) + L];
+        } else {
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(src + (hh << 8) + (L << 2));
+                const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(src + (hh << 8) + (L << 2) + 2);
+                buf[4 * hh] = a.x; buf[4 * hh + 1] = a.y; buf[4 * hh + 2] = b.x; buf[4 * hh + 3] = b.y;
+            }
+        }
+    };
+    auto step = [&](Raw& v, uint32_t p) {
+        uint64_t* dst = out + (size_t)rowp(p) * 1024;
+        if (!INV) {
+            // A: stages 9..6 (uniform twiddles)
+#pragma unroll
+            for (int b = 9; b >= 6; --b) {
+                const int rb = b - 6;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.ct(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            a_to_b(v);
+#pragma unroll
+            for (int b = 5; b >= 2; --b) {
+                const int rb = b - 2;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.ct(v[r], v[r | (1 << rb)], s_tw[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            b_to_c(v);
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const ulonglong2 w1 = s_tw[256 + (hh << 6) + L];
+                m.ct(v[4 * hh], v[4 * hh + 2], w1);
+                m.ct(v[4 * hh + 1], v[4 * hh + 3], w1);
+                m.ct(v[4 * hh], v[4 * hh + 1], s_tw[512 + (hh << 7) + (L << 1)]);
+                m.ct(v[4 * hh + 2], v[4 * hh + 3], s_tw[512 + (hh << 7) + (L << 1) + 1]);
+            }
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                *reinterpret_cast<ulonglong2*>(dst + (hh << 8) + (L << 2)) =
+                    ulonglong2{m.fwd_out(v[4 * hh]), m.fwd_out(v[4 * hh + 1])};
+                *reinterpret_cast<ulonglong2*>(dst + (hh << 8) + (L << 2) + 2) =
+                    ulonglong2{m.fwd_out(v[4 * hh + 2]), m.fwd_out(v[4 * hh + 3])};
+            }
+        } else {
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                m.gs(v[4 * hh], v[4 * hh + 1], s_tw[512 + (hh << 7) + (L << 1)]);
+                m.gs(v[4 * hh + 2], v[4 * hh + 3], s_tw[512 + (hh << 7) + (L << 1) + 1]);
+                const ulonglong2 w1 = s_tw[256 + (hh << 6) + L];
+                m.gs(v[4 * hh], v[4 * hh + 2], w1);
+                m.gs(v[4 * hh + 1], v[4 * hh + 3], w1);
+            }
+            c_to_b(v);
+#pragma unroll
+            for (int b = 2; b <= 5; ++b) {
+                const int rb = b - 2;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.gs(v[r], v[r | (1 << rb)], s_tw[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))]);
+                }
+            }
+            b_to_a(v);
+#pragma unroll
+            for (int b = 6; b <= 8; ++b) {
+                const int rb = b - 6;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (r & (1 << rb)) continue;
+                    m.gs(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) m.gs_last(v[r], v[r | 8]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dst[(r << 6) + L] = v[r];
+        }
+    };
+    __syncthreads();  // s_tw ready
+    if (!FHE_NTT64_PF) {
+        for (; poly < count; poly += W) {
+            Raw v;
+            load(v, poly);
+            step(v, poly);
+        }
+        return;
+    }
+    Raw bufA, bufB;
+    if (poly < count) load(bufA, poly);
+    for (; poly < count; poly += 2 * W) {
+        load(bufB, poly + W);
+        __builtin_amdgcn_sched_barrier(0);
+        step(bufA, poly);
+        if (poly + W >= count) break;
+        load(bufA, poly + 2 * W);
+        __builtin_amdgcn_sched_barrier(0);
+        step(bufB, poly + W);
+    }
+}
 }  // namespace
 
 #ifndef FHE_NTT_WAVE
@@ -690,9 +945,28 @@ static hipError_t launch_wave(const NttPlan& p, const uint64_t* in, uint64_t* ou
     return hipGetLastError();
 }
 
+#ifndef FHE_NTT64_WAVE
+#define FHE_NTT64_WAVE 1   // 64-bit path: one polynomial per wave (k_ntt1024w64)
+#endif
+static hipError_t launch_wave64(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
+                                hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    // 8 waves (polynomials) per workgroup; 16 KB of twiddles + 8 tiles of 4.25 KB
+    const size_t sm       = 1024 * sizeof(ulonglong2) + (size_t)8 * kWTile * 4;
+    const uint32_t groups = (count + 7) / 8;
+    const uint32_t cap    = (uint32_t)p.cus * 4 * FHE_NTT64_WPS / 8;
+    dim3 grid(groups < cap ? groups : cap), block(512);
+    Lazy64 m{p.Q, 2 * p.Q, ulonglong2{p.ninv, p.ninv_pre}, ulonglong2{p.w1ninv, p.w1ninv_pre}};
+    const ulonglong2* tab = reinterpret_cast<const ulonglong2*>(inverse ? p.d_tab_inv : p.d_tab_fwd);
+    if (inverse) hipLaunchKernelGGL((k_ntt1024w64<true>), grid, block, sm, s, in, out, count, tab, m);
+    else hipLaunchKernelGGL((k_ntt1024w64<false>), grid, block, sm, s, in, out, count, tab, m);
+    return hipGetLastError();
+}
+
 hipError_t ntt1024_launch(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                           hipStream_t s) {
-    if (p.wide) return launch<uint64_t>(p, in, out, count, inverse, s);
+    if (p.wide) return FHE_NTT64_WAVE ? launch_wave64(p, in, out, count, inverse, s)
+                                      : launch<uint64_t>(p, in, out, count, inverse, s);
     if (FHE_NTT_WAVE) return launch_wave(p, in, out, count, inverse, s);
     return launch<uint32_t>(p, in, out, count, inverse, s);
 }
