@@ -20,7 +20,7 @@ gate prep + blind rotation (k_blind_rotate_ginx), then key switch + ModSwitch
   * config3        -- BASELINE config 3: B = 1024 GINX gates on one GPU (N = 1 only);
   * ntt_roofline   -- BASELINE config 2: 4096-polynomial N = 1024 NTT and iNTT passes,
                       27-bit STD128 modulus (k_ntt1024w) and 60-bit poly-benchmark prime
-                      (k_ntt1024<u64>), GB/s vs HBM peak;
+                      (k_ntt1024w64), GB/s vs HBM peak;
   * cpu_baseline   -- the reference's own CPU path (oracle/_ref/libfhe_ref.so, built
                       from /root/reference) on this host, rank 0, N = 1 only: all cores
                       available to the job and 1 core, host model recorded; config-1
@@ -331,10 +331,10 @@ def pmc_traffic(kernel, batch):
 
 def ntt_rooflines(NttPlan, torch, dev, stream, count, reps=20):
     """BASELINE config 2: forward and inverse passes over `count` polynomials for the STD128 modulus
-    (27-bit, k_ntt1024w SignedA) and the poly-benchmark 60-bit prime (k_ntt1024<uint64_t>)."""
+    (27-bit, k_ntt1024w SignedA) and the poly-benchmark 60-bit prime (k_ntt1024w64)."""
     out = []
     sp = stream.cuda_stream
-    for Q, kname in ((134215681, "k_ntt1024w<{}, SignedA>"), (1152921504606830593, "k_ntt1024<uint64_t, {}>")):
+    for Q, kname in ((134215681, "k_ntt1024w<{}, SignedA>"), (1152921504606830593, "k_ntt1024w64<{}>")):
         plan = NttPlan(Q, device=dev.index)
         x = torch.randint(0, min(Q, 2**62), (count, 1024), dtype=torch.int64, device=dev)
         for inv in (False, True):   # in place, as SwitchFormat transforms a polynomial in place

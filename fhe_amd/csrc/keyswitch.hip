@@ -119,7 +119,7 @@ constexpr int kKsStep  = kKsIPR * kKsDigits;    // (i, j) steps per round / LDS 
 // (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
 // 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
-template <int G>
+template <int G, bool SPLIT>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
@@ -131,8 +131,8 @@ __global__ void __launch_bounds__(G)
     const uint32_t gate = blockIdx.x * G + t;
     const bool valid = gate < g.count;
     const uint32_t col0 = blockIdx.y * kKsCols;
-    const uint32_t rounds = g.N / kKsIPR / gridDim.z;    // this workgroup's share of the rounds
-    const uint32_t r0 = blockIdx.z * rounds;
+    const uint32_t rounds = SPLIT ? g.N / kKsIPR / gridDim.z : g.N / kKsIPR;  // this workgroup's share
+    const uint32_t r0 = SPLIT ? blockIdx.z * rounds : 0;
     using AV = typename std::conditional<kKsIPR == 4, uint4, uint2>::type;
     static_assert(kKsIPR == 4 || kKsIPR == 2, "a_i vector width");
     const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N) + r0;
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(G)
         }
     }
     if (!valid) return;
-    if (part) {
+    if (SPLIT) {
         uint4* pp = reinterpret_cast<uint4*>(part + ((size_t)blockIdx.z * g.count + gate) * (ksk_width(g.n) / 2) +
                                              col0 / 2);
 #pragma unroll
@@ -301,8 +301,13 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     if (tile > 1 && (logBase != (uint32_t)kKsLogBase || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
     if (tile > 1) {
         const uint32_t S = part ? keyswitch_split(g.count, g.n, g.N, part_words) : 1;
-        hipLaunchKernelGGL(k_keyswitch_tiled<FHE_KS_G>, dim3((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols, S),
-                           dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, a_out, b_out, S > 1 ? part : nullptr);
+        const dim3 grid((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols, S);
+        if (S > 1)
+            hipLaunchKernelGGL((k_keyswitch_tiled<FHE_KS_G, true>), grid, dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b,
+                               q_out, a_out, b_out, part);
+        else
+            hipLaunchKernelGGL((k_keyswitch_tiled<FHE_KS_G, false>), grid, dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b,
+                               q_out, a_out, b_out, nullptr);
         if (S > 1) {
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

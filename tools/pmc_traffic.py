@@ -27,7 +27,7 @@ def per_kernel(pas, counter):
 
 
 def short(name):
-    """the names bench.py reports: k_blind_rotate_ginx, k_ntt1024w<fwd, SignedA>, k_ntt1024<uint64_t, inv>, ..."""
+    """the names bench.py reports: k_blind_rotate_ginx, k_ntt1024w<fwd, SignedA>, k_ntt1024w64<inv>, ..."""
     m = re.search(r"(k_[a-z0-9_]+)", name)
     if not m:
         return name[:40]
@@ -35,6 +35,8 @@ def short(name):
     if base.startswith("k_ntt1024"):
         args = name[name.index(base) + len(base):].split("(")[0] + name.split(">(")[0]
         inv = "inv" if re.search(r"<\s*(unsigned long, )?true", name) else "fwd"
+        if base == "k_ntt1024w64":
+            return f"k_ntt1024w64<{inv}>"
         if base == "k_ntt1024w":
             arith = "SignedA" if "SignedA" in name else "ShoupA"
             return f"k_ntt1024w<{inv}, {arith}>"

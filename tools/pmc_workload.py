@@ -1,6 +1,6 @@
 """GPU workload for rocprofv3 --pmc passes (tools/pmc_run.sh): one STD128 GINX and one
 STD128_LMKCDEY AND batch of B gates (device-resident, as bench.py runs them), and 4096-polynomial
-forward + inverse NTT passes for the STD128 modulus (k_ntt1024w) and the 60-bit prime (k_ntt1024<u64>)."""
+forward + inverse NTT passes for the STD128 modulus (k_ntt1024w) and the 60-bit prime (k_ntt1024w64)."""
 import ctypes
 import sys
 
