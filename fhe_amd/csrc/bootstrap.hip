@@ -1105,10 +1105,42 @@ FHE_DEV void inv_wave_s(uint32_t (&v)[16], uint32_t* tile, int L, const uint32_t
         v[r | 8]         = min(d, d + m.Q);
     }
 }
+#ifndef FHE_AUTO_EXPORD
+#define FHE_AUTO_EXPORD 1  // automorphism_wide: regions in exponent order (3 VALU per gathered slot)
+#endif
 // automorphism X -> X^k of both components (as automorphism_eval: every half-wave gets its own
 // component back in layout B'), plus acc0' gathered into layout C for inv_wave_s
 FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* region, const uint32_t* region0,
                                int l, int L, uint32_t k) {
+    if (FHE_AUTO_EXPORD) {
+        // slot s = (l << 5) | r is stored at its exponent index brv10(s) = brv5(r) << 5 | brv5(l)
+        // (EVAL slot s holds the value at psi^(2 brv10(s) + 1)); the slot that reads exponent
+        // index t' gathers index ((2 t' + 1) k mod 2N) >> 1: one add, one bit-field extract, one
+        // address add per value
+        // FHE_AUTO_EXPORD 2: index t at t + 2 (t >> 6) (< kTile), which spreads the layout-C
+        // gather's lanes (t = 4 b k + c over 64 lanes b) over all banks
+        auto at = [](uint32_t t) -> uint32_t { return FHE_AUTO_EXPORD == 2 ? t + ((t >> 6) << 1) : t; };
+        static_assert(1023 + 2 * 15 < kTile, "padded region fits the tile");
+        const uint32_t bl = __builtin_bitreverse32((uint32_t)l) >> 27;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) region[at(((__builtin_bitreverse32((uint32_t)r) >> 27) << 5) | bl)] = v[r];
+        wave_lds_sync();
+        const uint32_t cl = (2 * bl + 1) * k;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
+            v[r]              = region[at(((cl + sr) >> 1) & 1023)];
+        }
+        const uint32_t cL = (((__builtin_bitreverse32((uint32_t)L) >> 26) << 3) + 1) * k;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t H = (uint32_t)r >> 2, j = (uint32_t)r & 3;
+            const uint32_t su = ((((j & 1) << 1 | j >> 1) << 9) + (((H & 1) << 1 | H >> 1) << 1)) * k;  // uniform
+            a0[r]             = region0[at(((cL + su) >> 1) & 1023)];
+        }
+        wave_lds_sync();
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 32; ++r) region[l * 33 + r] = v[r];
     wave_lds_sync();
