@@ -40,6 +40,13 @@ struct WideArgs {
 
 hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
+// LMKCDEY / DM on the 64-bit accumulator: the op lists of launch_prep_lmk / launch_prep_dm
+// (k_blind_rotate_wide_ops); bsk = the EXT keys [keys][digitsG2][2][N], autok = [numAutoKeys +
+// 1][digitsG - 1][2][N], Montgomery form
+hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, const uint64_t* bsk,
+                                        const uint64_t* autok, const uint16_t* ops, const uint32_t* nops,
+                                        uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
+                                        bool dm, hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) mod qKS = 2^k with u64 rows A [rows][n], B [rows], then
 // ModSwitch(qKS -> q_out) (q_out = 0: none); ms_a [count][N], ms_b [count] mod qKS
 hipError_t launch_keyswitch_wide(size_t count, uint32_t n, uint32_t N, uint32_t baseKS, uint32_t digitsKS, uint64_t qKS,

@@ -1510,13 +1510,16 @@ constexpr int kPrepWaves = 4;
 // count them (LDS atomics), a wave scan gives the group starts, a chunked stable placement
 // (rank among equal positions of lower lanes) fills the sorted order, and the nSkips state
 // machine runs on scalar registers over 64-position ballots of the non-empty groups.
+// NMAX: the largest ring dimension and LWE dimension the LDS arrays hold (1024: the 32-bit sets;
+// 2048: N = 2048 and n up to 2048 for the 64-bit accumulator)
+template <int NMAX>
 __global__ void __launch_bounds__(64 * kPrepWaves)
     k_prep_lmk_w(GateInputs in, GateArgs g, const int16_t* __restrict__ logGen, uint16_t* __restrict__ ops,
                  uint32_t* __restrict__ nops, uint32_t* __restrict__ tvb, uint32_t maxops, uint32_t numAutoKeys) {
-    __shared__ uint32_t s_start[kPrepWaves][1025];
-    __shared__ uint16_t s_fill[kPrepWaves][1024];
-    __shared__ uint16_t s_bkt[kPrepWaves][1024];     // n < 1024 (Engine::fast_path)
-    __shared__ uint16_t s_sorted[kPrepWaves][1024];
+    __shared__ uint32_t s_start[kPrepWaves][NMAX + 1];
+    __shared__ uint16_t s_fill[kPrepWaves][NMAX];
+    __shared__ uint16_t s_bkt[kPrepWaves][NMAX];
+    __shared__ uint16_t s_sorted[kPrepWaves][NMAX];
     __shared__ uint32_t s_part[kPrepWaves][64];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t gate = blockIdx.x * kPrepWaves + wv;
@@ -1667,9 +1670,13 @@ hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_
                            hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
-    if (g.n > 1024 || g.N != 1024) return hipErrorInvalidValue;  // k_prep_lmk_w LDS sizes
-    hipLaunchKernelGGL(k_prep_lmk_w, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, in, g,
-                       logGen, ops, nops, tvb, maxops, numAutoKeys);
+    if (g.n > 2048 || (g.N != 1024 && g.N != 2048)) return hipErrorInvalidValue;  // k_prep_lmk_w LDS sizes
+    if (g.n <= 1024 && g.N == 1024)
+        hipLaunchKernelGGL(k_prep_lmk_w<1024>, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0,
+                           s, in, g, logGen, ops, nops, tvb, maxops, numAutoKeys);
+    else
+        hipLaunchKernelGGL(k_prep_lmk_w<2048>, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0,
+                           s, in, g, logGen, ops, nops, tvb, maxops, numAutoKeys);
     return hipGetLastError();
 }
 

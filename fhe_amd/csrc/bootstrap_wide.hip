@@ -360,6 +360,221 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
     }
 }
 
+// ---------------------------------------------------------------------------
+// LMKCDEY (rgsw-acc-lmkcdey.cpp:70-287) and DM (rgsw-acc-dm.cpp:62-145) on the 64-bit accumulator:
+// the per-gate op list of k_prep_lmk_w / k_prep_dm_w, in the work split of k_blind_rotate_wide.
+//   EXT(i)  (AddToAccLMKCDEY / AddToAccDM): both accumulators to COEF, digitsG - 1 gadget levels of
+//           both (rows 2L / 2L + 1 of ek[i]), acc_c <- sum_rows D x ek[i][row][c]  (acc replaced);
+//   AUTO(t) (Automorphism, k = 5^t, or 2N - 5 for t = 0): acc <- sigma_k(acc) in EVAL (a slot
+//           permutation), acc0' alone to COEF and decomposed, acc0 <- sum_L D_L x ak[t][L][0],
+//           acc1 <- acc1' + sum_L D_L x ak[t][L][1].
+// LMKCDEY starts with acc1 <- sigma_(2N-5)(acc1) (:99).  Keys in Montgomery form, 128-bit sums, one
+// reduction per slot and component.
+// ---------------------------------------------------------------------------
+namespace {
+// EVAL slot j holds the value at psi^(2 brv(j) + 1); sigma_k's slot j reads slot brv((e_j k mod 2N - 1) / 2)
+template <int LOGN>
+WD uint32_t auto_src(uint32_t j, uint32_t k) {
+    constexpr uint32_t N = 1u << LOGN;
+    const uint32_t e = 2 * (__brev(j) >> (32 - LOGN)) + 1;
+    return __brev(((e * k) & (2 * N - 1)) >> 1) >> (32 - LOGN);
+}
+}  // namespace
+
+template <int LOGN, bool DM>
+__global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
+    k_blind_rotate_wide_ops(WideArgs g, WideTables tb, const uint64_t* __restrict__ bsk,
+                            const uint64_t* __restrict__ autok, const uint16_t* __restrict__ ops,
+                            const uint32_t* __restrict__ nops, uint32_t maxops, const uint32_t* __restrict__ tvb,
+                            uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b) {
+    constexpr int N = 1 << LOGN, T = N / 4, S = 4;
+    __shared__ uint64_t buf[2 * N];
+    const uint32_t gate = blockIdx.x, t = threadIdx.x;
+    const uint64_t Q = tb.Q, QHalf = Q >> 1;
+    const uint32_t dA = g.digitsG - 1, dG2 = 2 * dA, gb = g.gbits, sh = 64 - gb;
+
+    uint64_t acc0[S], acc1[S];
+    {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const uint32_t x = t + T * r;
+            uint64_t v = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            buf[x] = v;
+        }
+        __syncthreads();
+        fwd<LOGN, 1>(buf, tb);
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            acc0[r] = 0;
+            acc1[r] = buf[DM ? t + T * r : auto_src<LOGN>(t + T * r, 2 * N - 5)];
+        }
+    }
+    // the decomposition of rgsw-acc.cpp:54-91 from the canonical COEF value at buf[p N + j]:
+    // centred, the lowest digit dropped, one level per call of digit()
+    auto start = [&](int p, uint32_t j) -> int64_t {
+        const uint64_t v = mul_shoup(buf[p * N + j], tb.ninv, tb.ninvS, Q);
+        const int64_t x = v < QHalf ? (int64_t)v : (int64_t)v - (int64_t)Q;
+        const int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
+        return (x - r0) >> gb;
+    };
+    auto digit = [&](int64_t& d) -> uint64_t {
+        int64_t r0 = (int64_t)((uint64_t)d << sh) >> sh;
+        d = (d - r0) >> gb;
+        if (r0 < 0) r0 += (int64_t)Q;
+        return (uint64_t)r0;
+    };
+    const uint16_t* gops = ops + (size_t)gate * maxops;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(nops[gate]);
+#pragma unroll 1
+    for (uint32_t it = 0; it < cnt; ++it) {
+        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+        U128 U[2][S];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < S; ++r) U[c][r] = U128{0, 0};
+        __syncthreads();
+        if (DM || !(op & 0x8000u)) {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                buf[t + T * r]     = acc0[r];
+                buf[N + t + T * r] = acc1[r];
+            }
+            __syncthreads();
+            inv<LOGN, 2>(buf, tb);
+            int64_t d[2][S];
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int r = 0; r < S; ++r) d[p][r] = start(p, t + T * r);
+            const uint64_t* key = bsk + (size_t)op * dG2 * 2 * N;
+#pragma unroll 1
+            for (uint32_t L = 0; L < dA; ++L) {
+                __syncthreads();
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int r = 0; r < S; ++r) buf[p * N + t + T * r] = digit(d[p][r]);
+                __syncthreads();
+                fwd<LOGN, 2>(buf, tb);
+#pragma unroll
+                for (int r = 0; r < S; ++r) {
+                    const uint32_t j = t + T * r;
+                    const uint64_t x0 = buf[j], x1 = buf[N + j];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        mac(U[c][r], x0, key[((size_t)(2 * L) * 2 + c) * N + j]);
+                        mac(U[c][r], x1, key[((size_t)(2 * L + 1) * 2 + c) * N + j]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                acc0[r] = redc(U[0][r], Q, tb.qinv);
+                acc1[r] = redc(U[1][r], Q, tb.qinv);
+            }
+        } else {
+            const uint32_t ta = op & 0x7fffu;
+            uint32_t k = 2 * N - 5;
+            if (ta) {
+                k = 1;
+                for (uint32_t z = 0; z < ta; ++z) k = (k * 5) & (2 * N - 1);
+            }
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                buf[t + T * r]     = acc0[r];
+                buf[N + t + T * r] = acc1[r];
+            }
+            __syncthreads();
+            uint64_t a0[S];
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                const uint32_t src = auto_src<LOGN>(t + T * r, k);
+                a0[r]   = buf[src];
+                acc1[r] = buf[N + src];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < S; ++r) buf[t + T * r] = a0[r];
+            __syncthreads();
+            inv<LOGN, 1>(buf, tb);
+            int64_t d[S];
+#pragma unroll
+            for (int r = 0; r < S; ++r) d[r] = start(0, t + T * r);
+            const uint64_t* key = autok + (size_t)ta * dA * 2 * N;
+#pragma unroll 1
+            for (uint32_t L = 0; L < dA; ++L) {
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < S; ++r) buf[t + T * r] = digit(d[r]);
+                __syncthreads();
+                fwd<LOGN, 1>(buf, tb);
+#pragma unroll
+                for (int r = 0; r < S; ++r) {
+                    const uint32_t j = t + T * r;
+                    const uint64_t x = buf[j];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) mac(U[c][r], x, key[((size_t)L * 2 + c) * N + j]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                acc0[r] = redc(U[0][r], Q, tb.qinv);
+                acc1[r] = add_q(acc1[r], redc(U[1][r], Q, tb.qinv), Q);
+            }
+        }
+    }
+
+    // extraction as k_blind_rotate_wide
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        buf[t + T * r]     = acc0[r];
+        buf[N + t + T * r] = acc1[r];
+    }
+    __syncthreads();
+    inv<LOGN, 2>(buf, tb);
+    uint64_t* oa = ext_a + (size_t)gate * N;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const uint32_t x = t + T * r;
+        const uint64_t c = mul_shoup(buf[x == 0 ? 0 : N - x], tb.ninv, tb.ninvS, Q);
+        const uint64_t v = (x == 0 || c == 0) ? c : Q - c;
+        oa[x] = g.msb_out ? round_qQ(v, g.qKS, Q) : v;
+    }
+    if (t == 0) {
+        const uint64_t bb = add_q(g.b_const % Q, mul_shoup(buf[N], tb.ninv, tb.ninvS, Q), Q);
+        ext_b[gate] = g.msb_out ? round_qQ(bb, g.qKS, Q) : bb;
+    }
+}
+
+hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, const uint64_t* bsk,
+                                        const uint64_t* autok, const uint16_t* ops, const uint32_t* nops,
+                                        uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
+                                        bool dm, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if ((g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 || g.factor == 0 ||
+        g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
+        return hipErrorInvalidValue;
+#define FHE_WIDE_OPS(LG, DM_)                                                                                  \
+    hipLaunchKernelGGL((k_blind_rotate_wide_ops<LG, DM_>), dim3(g.count), dim3((1 << LG) / 4), 0, s, g, t, bsk, \
+                       autok, ops, nops, maxops, tvb, ext_a, ext_b)
+    if (g.N == 2048) {
+        if (dm) FHE_WIDE_OPS(11, true);
+        else FHE_WIDE_OPS(11, false);
+    } else {
+        if (dm) FHE_WIDE_OPS(10, true);
+        else FHE_WIDE_OPS(10, false);
+    }
+#undef FHE_WIDE_OPS
+    return hipGetLastError();
+}
+
 hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;

@@ -29,7 +29,7 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     // Two accumulator kernels: the 32-bit one (bootstrap.hip) for N = 1024, Q < 2^28, digitsG = 3 (the
     // STD128 / MEDIUM / STD128*_LMKCDEY sets); the 64-bit one (bootstrap_wide.hip) for every other
     // GINX set with N = 1024 / 2048 (any digitsG, Q up to 2^62) and the large-precision family.
-    if (is_large(paramset) || (!fast_path(p_) && method == M_GINX)) {
+    if (is_large(paramset) || (!fast_path(p_) && (method == M_GINX || method == M_LMKCDEY))) {
         wide_ = true;
         if (p_.N != 1024 && p_.N != 2048)
             throw std::invalid_argument("device path supports ring dimension N = 1024 / 2048");
@@ -42,6 +42,11 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         build_tables_wide();
         set_base(p_.baseG);
+        if (method == M_LMKCDEY) {  // op lists (k_prep_lmk_w) for k_blind_rotate_wide_ops
+            if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");
+            build_loggen();
+            maxops_ = p_.N + p_.n + 128;
+        }
         return;
     }
     if (!fast_path(p_))
@@ -142,19 +147,7 @@ void Engine::build_tables() {
             x = mulmod(x, p_.psi, Q);
         }
     }
-    if (p_.method == M_LMKCDEY) {  // rgsw-cryptoparameters.cpp:115-127
-        const uint32_t M = 2 * p_.N;
-        std::vector<int16_t> lg(M, 0);
-        uint32_t gp = 1;
-        lg[M - gp] = (int16_t)M;
-        for (uint32_t i = 1; i < p_.N / 2; ++i) {
-            gp = (gp * 5) % M;
-            lg[gp] = (int16_t)i;
-            lg[M - gp] = (int16_t)-(int32_t)i;
-        }
-        FHE_HIP_CHECK(hipMalloc(&d_logGen_, M * sizeof(int16_t)));
-        FHE_HIP_CHECK(hipMemcpy(d_logGen_, lg.data(), M * sizeof(int16_t), hipMemcpyHostToDevice));
-    }
+    if (p_.method == M_LMKCDEY) build_loggen();
     FHE_HIP_CHECK(hipMalloc(&d_tables_, t.size() * 4));
     FHE_HIP_CHECK(hipMemcpy(d_tables_, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     const uint32_t* d = static_cast<const uint32_t*>(d_tables_);
@@ -175,6 +168,21 @@ void Engine::build_tables() {
     tabs_.w1R = to_mont(h.tabI[1], Q);
     tabs_.oneR = to_mont(1, Q);
     tabs_.nR = to_mont(p_.N, Q);
+}
+
+// logGen of rgsw-cryptoparameters.cpp:115-127 (k_prep_lmk_w's group positions)
+void Engine::build_loggen() {
+    const uint32_t M = 2 * p_.N;
+    std::vector<int16_t> lg(M, 0);
+    uint32_t gp = 1;
+    lg[M - gp] = (int16_t)M;
+    for (uint32_t i = 1; i < p_.N / 2; ++i) {
+        gp = (gp * 5) % M;
+        lg[gp] = (int16_t)i;
+        lg[M - gp] = (int16_t)-(int32_t)i;
+    }
+    FHE_HIP_CHECK(hipMalloc(&d_logGen_, M * sizeof(int16_t)));
+    FHE_HIP_CHECK(hipMemcpy(d_logGen_, lg.data(), M * sizeof(int16_t), hipMemcpyHostToDevice));
 }
 
 void Engine::set_base(uint32_t bg) {
@@ -515,6 +523,12 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.b_const = g.b64;
         w.qKS = p_.qKS;
         w.tv = g.tv64;
+        if (p_.method == M_LMKCDEY) {
+            const uint64_t* bsk = static_cast<const uint64_t*>(d_bsk_);
+            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, bsk, bsk + (size_t)p_.n * p_.digitsG2 * 2 * p_.N,
+                                                       d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, false, s));
+            return;
+        }
         FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_) + cur_off_, d_idx_, d_tvb_,
                                                d_wext_a_, d_wext_b_, s));
         return;

@@ -149,6 +149,7 @@ private:
     void ensure_host_stage(size_t count);
     void build_tables();
     void build_tables_wide();
+    void build_loggen();
     // KeySwitch + ModSwitch(qKS -> q_out) of workspace slots [0, count) (q_out = 0: none)
     void keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
     // ctExt of workspace slots [0, count) to host u64 arrays

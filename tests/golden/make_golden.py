@@ -53,7 +53,15 @@ WIDER_SETS = {"medium": (1, GINX), "medium_ap": (1, AP), "medium_lmkcdey": (1, L
               "std192_4": (11, GINX), "std192q": (12, GINX), "std192q_3": (13, GINX), "std192q_4": (14, GINX),
               "std256": (15, GINX), "std256_3": (16, GINX), "std256_4": (17, GINX), "std256q": (18, GINX),
               "std256q_4": (20, GINX), "std128_3_lmkcdey": (22, LMKCDEY), "std128q_lmkcdey": (24, LMKCDEY),
-              "lpf_std128": (39, GINX), "lpf_std128q": (40, GINX), "lpf_std128_lmkcdey": (41, LMKCDEY)}
+              "lpf_std128": (39, GINX), "lpf_std128q": (40, GINX), "lpf_std128_lmkcdey": (41, LMKCDEY),
+              # LMKCDEY on the 64-bit accumulator (k_blind_rotate_wide_ops): digitsG 2-5, N = 2048
+              "std128_4_lmkcdey": (23, LMKCDEY), "std128q_3_lmkcdey": (25, LMKCDEY),
+              "std128q_4_lmkcdey": (26, LMKCDEY), "std192_lmkcdey": (27, LMKCDEY), "std192_3_lmkcdey": (28, LMKCDEY),
+              "std192_4_lmkcdey": (29, LMKCDEY), "std192q_lmkcdey": (30, LMKCDEY),
+              "std192q_3_lmkcdey": (31, LMKCDEY), "std192q_4_lmkcdey": (32, LMKCDEY),
+              "std256_lmkcdey": (33, LMKCDEY), "std256_3_lmkcdey": (34, LMKCDEY), "std256_4_lmkcdey": (35, LMKCDEY),
+              "std256q_lmkcdey": (36, LMKCDEY), "std256q_3_lmkcdey": (37, LMKCDEY),
+              "std256q_4_lmkcdey": (38, LMKCDEY), "lpf_std128q_lmkcdey": (42, LMKCDEY)}
 GATE_SETS.update(WIDER_SETS)
 WIDER_PER_GATE = 2
 GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}

@@ -7,7 +7,9 @@ tests/golden/make_golden.py wider from oracle/_ref):
     qKS = 2^15);
   * the 64-bit kernel (bootstrap_wide.hip) for every other GINX set: digitsG = 4 / 5 (STD128_3/4,
     STD128Q, LPF_STD128/Q, STD256*), N = 2048 with 29- to 50-bit Q (STD128Q_3/4, STD192*, STD256*),
-    qKS up to 2^21.
+    qKS up to 2^21;
+  * its op-list form (k_blind_rotate_wide_ops) for every other LMKCDEY set: STD128_4, STD128Q_3/4,
+    STD192*, STD256*, LPF_STD128Q _LMKCDEY (digitsG 2-5, N = 1024 / 2048, n up to 1320).
 Six gate types per set, final outputs and the extended ctExt."""
 import hashlib
 import os
@@ -34,7 +36,7 @@ def golden(name):
 
 
 def test_wider_goldens_present():
-    assert len(SETS) >= 20, SETS
+    assert len(SETS) >= 40, SETS
 
 
 @pytest.mark.parametrize("name", SETS)
