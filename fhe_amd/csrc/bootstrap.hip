@@ -1670,8 +1670,8 @@ hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_
                            hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
-    if (g.n > 2048 || (g.N != 1024 && g.N != 2048)) return hipErrorInvalidValue;  // k_prep_lmk_w LDS sizes
-    if (g.n <= 1024 && g.N == 1024)
+    if (g.n > 2048 || (g.N != 512 && g.N != 1024 && g.N != 2048)) return hipErrorInvalidValue;  // LDS sizes
+    if (g.n <= 1024 && g.N <= 1024)
         hipLaunchKernelGGL(k_prep_lmk_w<1024>, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0,
                            s, in, g, logGen, ops, nops, tvb, maxops, numAutoKeys);
     else

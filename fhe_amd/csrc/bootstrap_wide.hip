@@ -558,8 +558,8 @@ hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, 
                                         uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
                                         bool dm, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if ((g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 || g.factor == 0 ||
-        g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
+    if ((g.N != 512 && g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 ||
+        g.factor == 0 || g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
         return hipErrorInvalidValue;
 #define FHE_WIDE_OPS(LG, DM_)                                                                                  \
     hipLaunchKernelGGL((k_blind_rotate_wide_ops<LG, DM_>), dim3(g.count), dim3((1 << LG) / 4), 0, s, g, t, bsk, \
@@ -567,9 +567,12 @@ hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, 
     if (g.N == 2048) {
         if (dm) FHE_WIDE_OPS(11, true);
         else FHE_WIDE_OPS(11, false);
-    } else {
+    } else if (g.N == 1024) {
         if (dm) FHE_WIDE_OPS(10, true);
         else FHE_WIDE_OPS(10, false);
+    } else {  // TOY
+        if (dm) FHE_WIDE_OPS(9, true);
+        else FHE_WIDE_OPS(9, false);
     }
 #undef FHE_WIDE_OPS
     return hipGetLastError();
@@ -578,25 +581,29 @@ hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, 
 hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if ((g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 || g.factor == 0 ||
-        g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
+    if ((g.N != 512 && g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 ||
+        g.factor == 0 || g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
         return hipErrorInvalidValue;
     if (g.N == 2048)
         hipLaunchKernelGGL(k_blind_rotate_wide<11>, dim3(g.count), dim3(512), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
-    else
+    else if (g.N == 1024)
         hipLaunchKernelGGL(k_blind_rotate_wide<10>, dim3(g.count), dim3(256), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
+    else  // TOY
+        hipLaunchKernelGGL(k_blind_rotate_wide<9>, dim3(g.count), dim3(128), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// KeySwitch mod qKS = 2^k (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out): one workgroup per
-// ciphertext, thread t owns columns t + blockDim c of the n-wide A rows (u64, read coalesced)
-// and thread 0 also the B column; the 2^35 values of N digitsKS rows sum below 2^64 unreduced.
+// KeySwitch (lwe-pke.cpp:348-372) + ModSwitch(qKS -> q_out): one workgroup per ciphertext, thread t
+// owns columns t + blockDim c of the n-wide A rows (u64, read coalesced) and thread 0 also the B
+// column; the N digitsKS row values (each < qKS) sum below 2^64 unreduced, then mod qKS: a mask for
+// qKS = 2^k, a remainder for the prime qKS of TOY / SIGNED_MOD_TEST (modKS = PRIME).  Digits of a_i
+// in base baseKS: shifts for a power of two, remainders otherwise (STD256Q_3: 21, TOY: 25).
 // ---------------------------------------------------------------------------
 constexpr int kKsWideCols = 8;
 
 __global__ void __launch_bounds__(256)
-    k_keyswitch_wide(uint32_t n, uint32_t N, uint32_t logBase, uint32_t digitsKS, uint64_t qKS,
+    k_keyswitch_wide(uint32_t n, uint32_t N, uint32_t baseKS, uint32_t logBase, uint32_t digitsKS, uint64_t qKS,
                      const uint64_t* __restrict__ A, const uint64_t* __restrict__ B, const uint64_t* __restrict__ ms_a,
                      const uint64_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                      uint64_t* __restrict__ b_out) {
@@ -609,10 +616,17 @@ __global__ void __launch_bounds__(256)
     uint64_t accb = 0;
 #pragma unroll 1
     for (uint32_t i = 0; i < N; ++i) {
-        const uint64_t ai = s_a[i];
+        uint64_t ai = s_a[i];
 #pragma unroll 1
         for (uint32_t j = 0; j < digitsKS; ++j) {
-            const uint64_t row = ((uint64_t)i << logBase | ((ai >> (logBase * j)) & mask)) * digitsKS + j;
+            uint64_t a0;
+            if (logBase) {
+                a0 = (ai >> (logBase * j)) & mask;
+            } else {
+                a0 = ai % baseKS;
+                ai /= baseKS;
+            }
+            const uint64_t row = ((uint64_t)i * baseKS + a0) * digitsKS + j;
             const uint64_t* Ar = A + row * n;
 #pragma unroll
             for (int c = 0; c < kKsWideCols; ++c) {
@@ -622,18 +636,24 @@ __global__ void __launch_bounds__(256)
             if (t == 0) accb += B[row];
         }
     }
+    const bool pow2 = (qKS & (qKS - 1)) == 0;
     const uint64_t qm = qKS - 1;
+    auto sub_from = [&](uint64_t b, uint64_t sum) -> uint64_t {  // (b - sum) mod qKS, b < qKS
+        if (pow2) return (b - sum) & qm;
+        const uint64_t r = sum % qKS;
+        return b >= r ? b - r : b + qKS - r;
+    };
     uint64_t* oa = a_out + (size_t)gate * n;
 #pragma unroll
     for (int c = 0; c < kKsWideCols; ++c) {
         const uint32_t k = t + nt * c;
         if (k < n) {
-            const uint64_t v = (0 - acc[c]) & qm;
+            const uint64_t v = sub_from(0, acc[c]);
             oa[k] = q_out ? round_qQ(v, q_out, qKS) : v;
         }
     }
     if (t == 0) {
-        const uint64_t v = (ms_b[gate] - accb) & qm;
+        const uint64_t v = sub_from(ms_b[gate], accb);
         b_out[gate] = q_out ? round_qQ(v, q_out, qKS) : v;
     }
 }
@@ -642,18 +662,20 @@ hipError_t launch_keyswitch_wide(size_t count, uint32_t n, uint32_t N, uint32_t 
                                  const uint64_t* A, const uint64_t* B, const uint64_t* ms_a, const uint64_t* ms_b,
                                  uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
     if (count == 0) return hipSuccess;
-    if (N > 2048 || (qKS & (qKS - 1)) || (baseKS & (baseKS - 1)) || baseKS < 2 || count > 0x7fffffffull)
-        return hipErrorInvalidValue;
-    uint32_t logBase = 0;
-    while ((1u << logBase) < baseKS) ++logBase;
+    if (N > 2048 || qKS < 2 || baseKS < 2 || count > 0x7fffffffull) return hipErrorInvalidValue;
+    uint32_t logBase = 0;  // 0: baseKS is not a power of two
+    if (!(baseKS & (baseKS - 1)))
+        while ((1u << logBase) < baseKS) ++logBase;
     uint32_t nt = (n + 63) / 64 * 64;
     if (nt > 256) nt = 256;
     if ((size_t)nt * kKsWideCols < n) return hipErrorInvalidValue;
-    // the digits must cover log2(qKS) bits and the unreduced column sums must fit 64 bits
-    if ((uint64_t)logBase * digitsKS < 64 && (qKS >> (logBase * digitsKS)) > 1) return hipErrorInvalidValue;
+    // the digits must cover qKS and the unreduced column sums must fit 64 bits
+    double cover = 1;
+    for (uint32_t j = 0; j < digitsKS && cover < 1e30; ++j) cover *= baseKS;
+    if (cover < (double)qKS) return hipErrorInvalidValue;
     if ((double)N * digitsKS * (double)qKS >= 18446744073709551616.0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_keyswitch_wide, dim3((uint32_t)count), dim3(nt), 0, s, n, N, logBase, digitsKS, qKS, A, B,
-                       ms_a, ms_b, q_out, a_out, b_out);
+    hipLaunchKernelGGL(k_keyswitch_wide, dim3((uint32_t)count), dim3(nt), 0, s, n, N, baseKS, logBase, digitsKS, qKS,
+                       A, B, ms_a, ms_b, q_out, a_out, b_out);
     return hipGetLastError();
 }
 

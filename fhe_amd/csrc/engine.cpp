@@ -29,13 +29,12 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     // Two accumulator kernels: the 32-bit one (bootstrap.hip) for N = 1024, Q < 2^28, digitsG = 3 (the
     // STD128 / MEDIUM / STD128*_LMKCDEY sets); the 64-bit one (bootstrap_wide.hip) for every other
     // GINX set with N = 1024 / 2048 (any digitsG, Q up to 2^62) and the large-precision family.
-    if (is_large(paramset) || (!fast_path(p_) && (method == M_GINX || method == M_LMKCDEY))) {
+    if (is_large(paramset) || !fast_path(p_)) {
         wide_ = true;
-        if (p_.N != 1024 && p_.N != 2048)
-            throw std::invalid_argument("device path supports ring dimension N = 1024 / 2048");
+        if (p_.N != 512 && p_.N != 1024 && p_.N != 2048)
+            throw std::invalid_argument("device path supports ring dimension N = 512 / 1024 / 2048");
         if ((double)p_.digitsG2 * (double)p_.Q >= 18446744073709551616.0)
             throw std::invalid_argument("device path: digitsG2 * Q must stay below 2^64");
-        if (p_.qKS & (p_.qKS - 1)) throw std::invalid_argument("device path needs a power-of-two qKS");
         if (p_.q & (p_.q - 1)) throw std::invalid_argument("device path needs a power-of-two q");
         if (p_.n > 2048) throw std::invalid_argument("device path supports n <= 2048");
         FHE_HIP_CHECK(hipSetDevice(device_));
@@ -46,6 +45,9 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
             if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");
             build_loggen();
             maxops_ = p_.N + p_.n + 128;
+        } else if (method == M_AP) {  // op lists (k_prep_dm_w): at most digitsR ops per index
+            if ((size_t)p_.n * p_.baseR * p_.digitsR > 0x8000u) throw std::invalid_argument("device path: AP keys");
+            maxops_ = std::max<uint32_t>(p_.N + p_.n + 128, p_.n * p_.digitsR);
         }
         return;
     }
@@ -523,10 +525,11 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.b_const = g.b64;
         w.qKS = p_.qKS;
         w.tv = g.tv64;
-        if (p_.method == M_LMKCDEY) {
+        if (p_.method == M_LMKCDEY || p_.method == M_AP) {
             const uint64_t* bsk = static_cast<const uint64_t*>(d_bsk_);
-            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, bsk, bsk + (size_t)p_.n * p_.digitsG2 * 2 * p_.N,
-                                                       d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, false, s));
+            const bool dm = p_.method == M_AP;
+            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, bsk, dm ? bsk : bsk + (size_t)p_.n * p_.digitsG2 * 2 * p_.N,
+                                                       d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, dm, s));
             return;
         }
         FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_) + cur_off_, d_idx_, d_tvb_,

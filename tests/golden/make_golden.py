@@ -61,7 +61,10 @@ WIDER_SETS = {"medium": (1, GINX), "medium_ap": (1, AP), "medium_lmkcdey": (1, L
               "std192q_3_lmkcdey": (31, LMKCDEY), "std192q_4_lmkcdey": (32, LMKCDEY),
               "std256_lmkcdey": (33, LMKCDEY), "std256_3_lmkcdey": (34, LMKCDEY), "std256_4_lmkcdey": (35, LMKCDEY),
               "std256q_lmkcdey": (36, LMKCDEY), "std256q_3_lmkcdey": (37, LMKCDEY),
-              "std256q_4_lmkcdey": (38, LMKCDEY), "lpf_std128q_lmkcdey": (42, LMKCDEY)}
+              "std256q_4_lmkcdey": (38, LMKCDEY), "lpf_std128q_lmkcdey": (42, LMKCDEY),
+              # N = 512 (TOY: all three methods), prime qKS (TOY, SIGNED_MOD_TEST), baseKS = 21 (STD256Q_3)
+              "toy": (0, GINX), "toy_ap": (0, AP), "toy_lmkcdey": (0, LMKCDEY), "signed_mod_test": (43, GINX),
+              "std256q_3": (19, GINX)}
 GATE_SETS.update(WIDER_SETS)
 WIDER_PER_GATE = 2
 GATES = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR": 4, "XNOR": 5}

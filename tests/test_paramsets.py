@@ -9,7 +9,9 @@ tests/golden/make_golden.py wider from oracle/_ref):
     STD128Q, LPF_STD128/Q, STD256*), N = 2048 with 29- to 50-bit Q (STD128Q_3/4, STD192*, STD256*),
     qKS up to 2^21;
   * its op-list form (k_blind_rotate_wide_ops) for every other LMKCDEY set: STD128_4, STD128Q_3/4,
-    STD192*, STD256*, LPF_STD128Q _LMKCDEY (digitsG 2-5, N = 1024 / 2048, n up to 1320).
+    STD192*, STD256*, LPF_STD128Q _LMKCDEY (digitsG 2-5, N = 1024 / 2048, n up to 1320);
+  * TOY (N = 512) with GINX, AP (the DM op list) and LMKCDEY, SIGNED_MOD_TEST: the prime qKS of
+    modKS = PRIME, STD256Q_3: baseKS = 21 (key-switching digits by remainders).
 Six gate types per set, final outputs and the extended ctExt."""
 import hashlib
 import os
