@@ -314,7 +314,8 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
 
 // the split GINX kernel's key layout (k_blind_rotate_ginx2), repacked on the device from the resident one
 void Engine::repack_ginx2() {
-    if (p_.method != M_GINX || wide_ || !d_bsk_) return;
+    // only when the split kernel can run (pinned, or chosen below kSplitBatch gates)
+    if (p_.method != M_GINX || wide_ || !d_bsk_ || (ginx_kernel_ != 2 && kSplitBatch == 0)) return;
     FHE_HIP_CHECK(hipSetDevice(device_));
     if (!d_bsk2_) FHE_HIP_CHECK(hipMalloc(&d_bsk2_, (size_t)p_.n * 16384 * 4));
     FHE_HIP_CHECK(launch_repack_ginx2(d_bsk_, p_.n, d_bsk2_, stream_));
