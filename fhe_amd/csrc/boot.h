@@ -109,6 +109,23 @@ hipError_t launch_repack_ginx2(const void* bsk, uint32_t n, void* bsk2, hipStrea
 hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, const void* bsk2, const uint16_t* idx,
                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 bool ginx2_supported(const GateArgs& g, const BootTables& t);
+// The same split kernel with three retained digits per component (digitsG = 4 at N = 1024, Q < 2^27:
+// STD128_3, STD128Q) for the sets whose keys otherwise live on the 64-bit accumulator: keys in the
+// g2_key_word layout (nd = 3), u64 ctExt into that path's workspace (launch_keyswitch_wide reads it)
+hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, const void* bsk3, const uint16_t* idx,
+                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
+bool ginx3_supported(const GateArgs& g, const BootTables& t);
+// split-kernel key layout, per index i (8192 nd words): [c][p < 2 nd][k2 < 8][64 lanes][4 words]
+// = (K+[r], K+[r+1], K-[r], K-[r+1]) of component c, digit row g2_row(c, p, nd), r = 2 k2, EVAL slot
+// x(L, r) = ((r >> 2) << 8) | (L << 2) | (r & 3): wave c multiplies (own digits D_c, D_{2+c}, ..,
+// partner digits D_{1-c}, D_{3-c}, ..) in that order
+__host__ __device__ constexpr uint32_t g2_row(uint32_t c, uint32_t p, uint32_t nd) {
+    return p < nd ? 2 * p + c : 2 * (p - nd) + 1 - c;
+}
+__host__ __device__ constexpr uint32_t g2_key_word(uint32_t nd, uint32_t c, uint32_t p, uint32_t k2, uint32_t L,
+                                                   uint32_t e4) {
+    return (((c * 2 * nd + p) * 8 + k2) * 64 + L) * 4 + e4;
+}
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);

@@ -1720,34 +1720,41 @@ hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops
 }
 
 // ===========================================================================
-// GINX with two waves per gate: k_blind_rotate_ginx2
+// GINX with two waves per gate: k_blind_rotate_ginx2<ND, OutT>
 // ===========================================================================
 // Wave c of a gate owns RLWE component c: 1024 values as 16 registers x 64 lanes, in the layouts of
 // ntt.hip k_ntt1024w (x = coefficient or EVAL slot):
 //   A (COEF): lane = x5..x0, register = x9..x6;   C (EVAL): lane = x7..x2, register = (x9x8) << 2 | x1x0.
 // Per index (AddToAccCGGI, rgsw-acc-cggi.cpp:102-151), wave c: inverse NTT of acc_c (C -> B -> A,
-// inv_wave_s), SignedDigitDecompose into D_c (digit A) and D_{2+c} (digit B), both forward-transformed
-// at once (A -> B -> C), written to this wave's LDS region; one workgroup barrier; then per slot the
-// MAC with its own two digits and the partner wave's two (read from the partner's region), the keys of
-// component c, and the monomials: acc_c <- acc_c + S+ (w^a - 1) + S- (w^-a - 1), one signed Montgomery
-// reduction per slot, as in k_blind_rotate_ginx.  Half the registers of the one-wave kernel per wave,
-// twice the waves: a 1024-gate batch fills 2048 waves.
+// inv_wave_s), SignedDigitDecompose into its ND retained digits D_c, D_{2+c}, .. (rgsw-acc.cpp:54-91:
+// digitsG - 1 of them, the lowest one dropped), all forward-transformed at once (A -> B -> C) and
+// written to this wave's LDS region; one workgroup barrier; then per slot the MAC with its own ND
+// digits and the partner wave's ND (read from the partner's region), the keys of component c, and the
+// monomials: acc_c <- acc_c + S+ (w^a - 1) + S- (w^-a - 1), one signed Montgomery reduction per slot,
+// as in k_blind_rotate_ginx.  Half the registers of the one-wave kernel per wave, twice the waves.
+//   ND = 2 (digitsG = 3: STD128, MEDIUM ...): pinned by FHE_HIP_GINX_KERNEL=split (the one-wave kernel
+//          is faster at every batch size, DESIGN K1), u32 ctExt for the 32-bit key switch;
+//   ND = 3 (digitsG = 4 at N = 1024, Q < 2^27: STD128_3, STD128Q): the one-wave layout would need 96
+//          digit registers per lane, so these sets ran on the 64-bit accumulator (bootstrap_wide.hip);
+//          this instantiation runs them in 32-bit residues and writes the u64 ctExt of that path's
+//          workspace, which its key switch (keyswitch_wide) reads unchanged.
+// Bounds (Q < 2^27): signed digits |d| <= 2^(g-1) grow to < 10 Q + 2^(g-1) through the forward NTT;
+// |S+-| < 2 ND (10 Q + 2^(g-1)) Q < 2^60; S < 2 (2^32 Q + 2 ND 0.32 Q^2) + 2.8 Q^2, so the reduced
+// acc stays below 2.8 Q (kAccBoundLZ) for ND <= 3.
 namespace {
-constexpr int kG2Gates  = 2;                  // gates per workgroup (2 waves each)
-constexpr int kG2Region = 2176;               // words per wave: two transpose tiles / the digit exchange
-constexpr int kG2Tile   = 1088;               // one tile (1024 + 64 pad, wt64 addressing)
-constexpr size_t g2_lds() { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 2 * kG2Gates * kG2Region) * 4; }
+constexpr int kG2Gates = 2;     // gates per workgroup (2 waves each)
+constexpr int kG2Tile  = 1088;  // one tile (1024 + 64 pad, wt64 addressing)
+// words per wave: ND transpose tiles, which also hold the ND digit polynomials of the exchange
+constexpr int g2_region(int nd) { return nd * kG2Tile; }
+constexpr size_t g2_lds(int nd) { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 2 * kG2Gates * g2_region(nd)) * 4; }
 
-// key layout of index i (words): [c][p][k2][64 lanes][4]: (K+[r], K+[r+1], K-[r], K-[r+1]) with
-// r = 2 k2, slot x(L, r) = ((r >> 2) << 8) | (L << 2) | (r & 3), row = g2_row(c, p): the digit order
-// (own A, own B, partner A, partner B) of wave c is (D_c, D_{2+c}, D_{1-c}, D_{3-c})
-__host__ __device__ constexpr uint32_t g2_row(uint32_t c, uint32_t p) {
-    return p == 0 ? c : p == 1 ? 2 + c : p == 2 ? 1 - c : 3 - c;
-}
+// key layout: boot.h g2_key_word / g2_row
 
-// signed forward NTT of two polynomials, layout A (|v| < B) -> C (|v| < B + 10 Q); tiles t0, t1
-FHE_DEV void fwd_wave2_s(uint32_t (&u)[16], uint32_t (&v)[16], uint32_t* t0, uint32_t* t1, int L,
-                         const uint32_t* __restrict__ twA, const uint32_t* s_tab, const Mod& m) {
+// signed forward NTT of NP polynomials, layout A (|v| < B) -> C (|v| < B + 10 Q); polynomial p
+// goes through the tile t + p kG2Tile
+template <int NP>
+FHE_DEV void fwd_wave_s(uint32_t (&v)[NP][16], uint32_t* t, int L, const uint32_t* __restrict__ twA,
+                        const uint32_t* s_tab, const Mod& m) {
     const int G = L >> 2, jj = L & 3;
 #pragma unroll
     for (int b = 9; b >= 6; --b) {
@@ -1756,22 +1763,20 @@ FHE_DEV void fwd_wave2_s(uint32_t (&u)[16], uint32_t (&v)[16], uint32_t* t0, uin
         for (int r = 0; r < 16; ++r) {
             if (r & (1 << rb)) continue;
             const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
-            ct_bf_s(u[r], u[r | (1 << rb)], w, m);
-            ct_bf_s(v[r], v[r | (1 << rb)], w, m);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
         }
     }
     // A -> B
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        t0[wt64((r << 6) | L)] = u[r];
-        t1[wt64((r << 6) | L)] = v[r];
-    }
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) t[p * kG2Tile + wt64((r << 6) | L)] = v[p][r];
     wave_lds_sync();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        u[r] = t0[wt64((G << 6) | (r << 2) | jj)];
-        v[r] = t1[wt64((G << 6) | (r << 2) | jj)];
-    }
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) v[p][r] = t[p * kG2Tile + wt64((G << 6) | (r << 2) | jj)];
 #pragma unroll
     for (int b = 5; b >= 2; --b) {
         const int rb = b - 2;
@@ -1779,46 +1784,74 @@ FHE_DEV void fwd_wave2_s(uint32_t (&u)[16], uint32_t (&v)[16], uint32_t* t0, uin
         for (int r = 0; r < 16; ++r) {
             if (r & (1 << rb)) continue;
             const uint32_t w = s_tab[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))];
-            ct_bf_s(u[r], u[r | (1 << rb)], w, m);
-            ct_bf_s(v[r], v[r | (1 << rb)], w, m);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
         }
     }
     // B -> C
     wave_lds_sync();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        t0[wt64((G << 6) | (r << 2) | jj)] = u[r];
-        t1[wt64((G << 6) | (r << 2) | jj)] = v[r];
-    }
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) t[p * kG2Tile + wt64((G << 6) | (r << 2) | jj)] = v[p][r];
     wave_lds_sync();
 #pragma unroll
-    for (int hh = 0; hh < 4; ++hh) {
-        const uint4 p = *reinterpret_cast<const uint4*>(t0 + wt64((hh << 8) | (L << 2)));
-        const uint4 q = *reinterpret_cast<const uint4*>(t1 + wt64((hh << 8) | (L << 2)));
-        u[4 * hh] = p.x; u[4 * hh + 1] = p.y; u[4 * hh + 2] = p.z; u[4 * hh + 3] = p.w;
-        v[4 * hh] = q.x; v[4 * hh + 1] = q.y; v[4 * hh + 2] = q.z; v[4 * hh + 3] = q.w;
-    }
+    for (int hh = 0; hh < 4; ++hh)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const uint4 q = *reinterpret_cast<const uint4*>(t + p * kG2Tile + wt64((hh << 8) | (L << 2)));
+            v[p][4 * hh] = q.x; v[p][4 * hh + 1] = q.y; v[p][4 * hh + 2] = q.z; v[p][4 * hh + 3] = q.w;
+        }
     wave_lds_sync();
 #pragma unroll
     for (int hh = 0; hh < 4; ++hh) {
         const uint32_t w1 = s_tab[256 + (hh << 6) + L];
-        ct_bf_s(u[4 * hh], u[4 * hh + 2], w1, m);
-        ct_bf_s(u[4 * hh + 1], u[4 * hh + 3], w1, m);
-        ct_bf_s(v[4 * hh], v[4 * hh + 2], w1, m);
-        ct_bf_s(v[4 * hh + 1], v[4 * hh + 3], w1, m);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            ct_bf_s(v[p][4 * hh], v[p][4 * hh + 2], w1, m);
+            ct_bf_s(v[p][4 * hh + 1], v[p][4 * hh + 3], w1, m);
+        }
         const uint2 w0 = *reinterpret_cast<const uint2*>(s_tab + 512 + (hh << 7) + (L << 1));
-        ct_bf_s(u[4 * hh], u[4 * hh + 1], w0.x, m);
-        ct_bf_s(u[4 * hh + 2], u[4 * hh + 3], w0.y, m);
-        ct_bf_s(v[4 * hh], v[4 * hh + 1], w0.x, m);
-        ct_bf_s(v[4 * hh + 2], v[4 * hh + 3], w0.y, m);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            ct_bf_s(v[p][4 * hh], v[p][4 * hh + 1], w0.x, m);
+            ct_bf_s(v[p][4 * hh + 2], v[p][4 * hh + 3], w0.y, m);
+        }
     }
+}
+
+// SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = ND + 1, as decompose2 with SG: the
+// balanced digits 1..ND of the centred value d are the signed bit fields j g of (d + C) ^ M,
+// C = 2^(g-1) sum_{j <= ND} 2^(jg), M = 2^(g-1) sum_{1 <= j <= ND} 2^(jg) (needs (ND + 1) g <= 32 and
+// C + Q < 2^32; Engine checks both)
+struct DecN {
+    uint32_t Qh, C, CmQ, g, M;
+};
+FHE_DEV DecN make_decn(uint32_t Q, uint32_t g, int nd) {
+    const uint32_t h = 1u << (g - 1);
+    uint32_t C = h, M = 0;
+    for (int j = 1; j <= nd; ++j) {
+        C += h << (j * g);
+        M |= h << (j * g);
+    }
+    return DecN{Q >> 1, C, C - Q, g, M};
+}
+template <int ND>
+FHE_DEV void decompose_n(uint32_t x, const DecN& c, uint32_t (&d)[ND][16], int r) {
+    const uint32_t u = x >= c.Qh ? x + c.CmQ : x + c.C;  // d + C, d = x or x - Q
+    const int32_t w  = (int32_t)(u ^ c.M);
+#pragma unroll
+    for (int j = 0; j < ND; ++j) d[j][r] = (uint32_t)__builtin_amdgcn_sbfe(w, (j + 1) * c.g, c.g);
 }
 }  // namespace
 
+template <int ND, typename OutT>
 __global__ void __launch_bounds__(128 * kG2Gates, 2)
     k_blind_rotate_ginx2(GateArgs g, BootTables T, const uint4* __restrict__ bsk2, const uint16_t* __restrict__ idx,
-                         const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
+                         const uint32_t* __restrict__ tvb, OutT* __restrict__ ext_a, OutT* __restrict__ ext_b,
                          const uint32_t* __restrict__ twAf) {
+    constexpr int kReg = g2_region(ND);
+    constexpr int kRows = 2 * ND;  // digit rows per slot: own ND, partner ND
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 1024;
@@ -1835,10 +1868,9 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
     const uint32_t gslot = blockIdx.x * kG2Gates + (wave >> 1);
     const bool live = gslot < g.count;
     const uint32_t gate = live ? gslot : g.count - 1;   // spare waves shadow the last gate: every wave meets every barrier
-    uint32_t* region  = s_reg + wave * kG2Region;
-    uint32_t* partner = s_reg + (wave ^ 1) * kG2Region;
+    uint32_t* region  = s_reg + wave * kReg;
+    uint32_t* partner = s_reg + (wave ^ 1) * kReg;
     uint32_t* t0 = region;
-    uint32_t* t1 = region + kG2Tile;
     const Mod m0 = make_mod(T);
     const Mod& m = m0;
     __syncthreads();
@@ -1847,7 +1879,7 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
     uint32_t acc[16];
     if (c == 1) {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
-        uint32_t dummy[16];
+        uint32_t tv[1][16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
@@ -1856,52 +1888,50 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
                 const uint32_t bx = (b - x / g.factor) & cm;
                 v = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
-            acc[r]   = v;
-            dummy[r] = 0;
+            tv[0][r] = v;
         }
-        fwd_wave2_s(acc, dummy, t0, t1, L, twAf, s_tab, m);
+        fwd_wave_s<1>(tv, t0, L, twAf, s_tab, m);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = smont_mul(acc[r], T.ninvR, m);   // (-Q, Q), N^-1 scaled
+        for (int r = 0; r < 16; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);   // (-Q, Q), N^-1 scaled
     } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0;
     }
 
     const uint16_t* gidx = idx + (size_t)gate * g.n;
-    const Dec dec = make_dec(m.Q, g.gbits);
+    const DecN dec = make_decn(m.Q, g.gbits, ND);
     // monomial index of slot x(L, r): f = a' (2 brv10(x) + 1) mod 2N in half-table units, split as a
     // per-lane part a' (8 brv6(L) + 1) and a per-register part a' (512 brv2(r & 3) + 2 brv2(r >> 2))
     const uint32_t lmul = 8 * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1;
-    const uint4* kc = bsk2 + (size_t)c * (4 * 8 * 64) + L;
+    const uint4* kc = bsk2 + (size_t)c * (kRows * 8 * 64) + L;
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m = fresh_nq(m0);
         const uint32_t a  = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
         const uint32_t as = a >> 1;                         // even exponents (ctmod = q < 2N)
-        const uint4* kb   = kc + (size_t)i * (2 * 4 * 8 * 64);
-        uint4 kq[2][4];
+        const uint4* kb   = kc + (size_t)i * (2 * kRows * 8 * 64);
+        uint4 kq[2][kRows];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) kq[0][p] = kb[(p * 8 + 0) * 64];
+        for (int p = 0; p < kRows; ++p) kq[0][p] = kb[(p * 8 + 0) * 64];
         __syncthreads();   // the partner wave has read this wave's digits of the previous index
-        uint32_t dA[16], dB[16];
+        uint32_t d[ND][16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dA[r] = acc[r];
-        inv_wave_s<kAccBoundLZ, true>(dA, t0, L, s_tabI, T.w1R, m.oneR, m);
+        for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
+        inv_wave_s<kAccBoundLZ, true>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
-        fwd_wave2_s(dA, dB, t0, t1, L, twAf, s_tab, m);
+        for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+        fwd_wave_s<ND>(d, t0, L, twAf, s_tab, m);
         wave_lds_sync();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            region[(r << 6) | L]        = dA[r];
-            region[1024 + ((r << 6) | L)] = dB[r];
-        }
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+            for (int j = 0; j < ND; ++j) region[j * 1024 + ((r << 6) | L)] = d[j][r];
         __syncthreads();   // both waves' digits are in LDS
         const uint32_t fl = (as * lmul) & 1023u;
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) {
             if (k2 + 1 < 8) {
 #pragma unroll
-                for (int p = 0; p < 4; ++p) kq[(k2 + 1) & 1][p] = kb[(p * 8 + k2 + 1) * 64];
+                for (int p = 0; p < kRows; ++p) kq[(k2 + 1) & 1][p] = kb[(p * 8 + k2 + 1) * 64];
             }
             asm volatile("" ::: "memory");
             // registers r = 2 k2, 2 k2 + 1 differ in x bit 0: the same monomial (even exponents)
@@ -1915,12 +1945,18 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = r0 + e;
-                const uint32_t pA = partner[(r << 6) | L], pB = partner[1024 + ((r << 6) | L)];
+                uint32_t pd[ND];
+#pragma unroll
+                for (int j = 0; j < ND; ++j) pd[j] = partner[j * 1024 + ((r << 6) | L)];
                 const uint4* q = kq[k2 & 1];
-                const int64_t S1 = (int64_t)mac4<true>(dA[r], dB[r], pA, pB, e ? q[0].y : q[0].x, e ? q[1].y : q[1].x,
-                                                       e ? q[2].y : q[2].x, e ? q[3].y : q[3].x, 0);
-                const int64_t S2 = (int64_t)mac4<true>(dA[r], dB[r], pA, pB, e ? q[0].w : q[0].z, e ? q[1].w : q[1].z,
-                                                       e ? q[2].w : q[2].z, e ? q[3].w : q[3].z, 0);
+                // digits x keys in row order (own digits, partner digits), unreduced 64-bit sums
+                int64_t S1 = 0, S2 = 0;
+#pragma unroll
+                for (int p = 0; p < kRows; ++p) {
+                    const int32_t dv = (int32_t)(p < ND ? d[p][r] : pd[p - ND]);
+                    S1 += (int64_t)dv * (int32_t)(e ? q[p].y : q[p].x);
+                    S2 += (int64_t)dv * (int32_t)(e ? q[p].w : q[p].z);
+                }
                 int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
                 S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
                 S += (int64_t)(int32_t)acc[r] * (int32_t)T.oneR;
@@ -1935,21 +1971,21 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
     inv_wave_s<kAccBoundLZ, true>(acc, t0, L, s_tabI, T.w1R, m.oneR, m);
     if (!live) return;
     if (c == 0) {
-        uint32_t* oa = ext_a + (size_t)gate * g.N;
+        OutT* oa = ext_a + (size_t)gate * g.N;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
             const uint32_t v = acc[r];
             const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
-            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+            oa[(g.N - x) & (g.N - 1)] = (OutT)(g.msb_out ? mod_switch(o, m.Q, g.qKS) : o);
         }
     } else if (L == 0) {
         const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
-        ext_b[gate] = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+        ext_b[gate] = (OutT)(g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb);
     }
 }
 
-// the resident GINX layout (ginx_u4_off, half-swapped rows) -> the k_blind_rotate_ginx2 layout
+// the resident GINX layout (ginx_u4_off, half-swapped rows) -> the k_blind_rotate_ginx2<2> layout
 __global__ void k_repack_ginx2(const uint32_t* __restrict__ src, uint32_t n, uint32_t* __restrict__ dst) {
     const uint64_t words = (uint64_t)n * 16384;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -1958,7 +1994,7 @@ __global__ void k_repack_ginx2(const uint32_t* __restrict__ src, uint32_t n, uin
         const uint32_t e4 = w & 3, L = (w >> 2) & 63, k2 = (w >> 8) & 7, p = (w >> 11) & 3, c = w >> 13;
         const uint32_t r = 2 * k2 + (e4 & 1), ks = e4 >> 1;
         const uint32_t x = ((r >> 2) << 8) | (L << 2) | (r & 3);          // EVAL slot
-        const uint32_t row = g2_row(c, p);
+        const uint32_t row = g2_row(c, p, 2);
         const uint32_t lane = c * 32 + (x >> 5), kk = (x & 31) >> 1, e = x & 1;
         const uint32_t dpos = kBskHalfSwap ? row ^ c : row;
         dst[t] = src[i * 16384 + ginx_u4_off(ks, dpos, kk, lane, e)];
@@ -1982,8 +2018,26 @@ hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, con
     if (g.count == 0) return hipSuccess;
     if (!ginx2_supported(g, t)) return hipErrorInvalidValue;
     const uint32_t blocks = (g.count + kG2Gates - 1) / kG2Gates;
-    hipLaunchKernelGGL(k_blind_rotate_ginx2, dim3(blocks), dim3(128 * kG2Gates), g2_lds(), s, g, t,
+    hipLaunchKernelGGL((k_blind_rotate_ginx2<2, uint32_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(2), s, g, t,
                        static_cast<const uint4*>(bsk2), idx, tvb, ext_a, ext_b, t.twA_fwd);
+    return hipGetLastError();
+}
+
+bool ginx3_supported(const GateArgs& g, const BootTables& t) {
+    return t.Q < (1u << 27) && g.N == 1024 && g.ctmod < 2 * g.N && g.tv == nullptr && g.tv64 == nullptr &&
+           g.acc_io == nullptr && g.gbits >= 2 && 4 * g.gbits <= 32 && g.qKS <= 65536;
+}
+
+hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, const void* bsk3, const uint16_t* idx,
+                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!ginx3_supported(g, t)) return hipErrorInvalidValue;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, uint64_t>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
+    (void)attr;
+    const uint32_t blocks = (g.count + kG2Gates - 1) / kG2Gates;
+    hipLaunchKernelGGL((k_blind_rotate_ginx2<3, uint64_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s, g, t,
+                       static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd);
     return hipGetLastError();
 }
 

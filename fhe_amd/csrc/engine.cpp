@@ -25,6 +25,40 @@ bool Engine::fast_path(const Params& p) {
            p.qKS <= 65536 && p.n < 1024;
 }
 
+bool Engine::g3_set(const Params& p) {
+    // digit fields of d + C in 32 bits (bootstrap.hip decompose_n): 4 g <= 32 and C + Q < 2^32
+    const uint64_t g = p.gBits, h = 1ull << (g - 1);
+    const uint64_t C = h * (1 + (1ull << g) + (1ull << (2 * g)) + (1ull << (3 * g)));
+    return !is_large(p.paramset) && !p.timeopt && p.method == M_GINX && p.N == 1024 && p.Q < (1ull << 27) &&
+           p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.qKS <= 65536;
+}
+
+// the split kernel's nd = 3 key layout (boot.h g2_key_word) from the raw BSK [n][2][dG2 = 8][2][N],
+// u32 Montgomery with N^-1 folded in (as the resident 32-bit layouts)
+void Engine::pack_ginx3(const uint64_t* bsk) {
+    const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
+    const uint64_t Q = p_.Q, ninv = invmod(N, Q);
+    const size_t per = 8192 * 3;
+    std::vector<uint32_t> dev((size_t)n * per);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i)
+        for (uint32_t c = 0; c < 2; ++c)
+            for (uint32_t p = 0; p < 6; ++p)
+                for (uint32_t k2 = 0; k2 < 8; ++k2)
+                    for (uint32_t L = 0; L < 64; ++L)
+                        for (uint32_t e4 = 0; e4 < 4; ++e4) {
+                            const uint32_t r = 2 * k2 + (e4 & 1), ks = e4 >> 1;
+                            const uint32_t x = ((r >> 2) << 8) | (L << 2) | (r & 3);
+                            const size_t src = ((((size_t)i * 2 + ks) * dG2 + g2_row(c, p, 3)) * 2 + c) * N + x;
+                            dev[(size_t)i * per + g2_key_word(3, c, p, k2, L, e4)] = to_mont(mulmod(bsk[src] % Q, ninv, Q), Q);
+                        }
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    if (d_bsk2_) FHE_HIP_CHECK(hipFree(d_bsk2_));
+    d_bsk2_ = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&d_bsk2_, dev.size() * 4));
+    FHE_HIP_CHECK(hipMemcpy(d_bsk2_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+}
+
 Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, method)), device_(device) {
     // Two accumulator kernels: the 32-bit one (bootstrap.hip) for N = 1024, Q < 2^28, digitsG = 3 (the
     // STD128 / MEDIUM / STD128*_LMKCDEY sets); the 64-bit one (bootstrap_wide.hip) for every other
@@ -41,6 +75,11 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         build_tables_wide();
         set_base(p_.baseG);
+        if (g3_set(p_)) {
+            const char* e = std::getenv("FHE_HIP_GINX3");
+            g3_ = !(e && std::string(e) == "0");
+            if (g3_) build_tables();
+        }
         if (method == M_LMKCDEY) {  // op lists (k_prep_lmk_w) for k_blind_rotate_wide_ops
             if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");
             build_loggen();
@@ -245,6 +284,7 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
         d_bsk_ = nullptr;
         FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * 8));
         FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), words * 8, hipMemcpyHostToDevice));
+        if (g3_) pack_ginx3(bsk);
         return;
     }
     const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
@@ -531,6 +571,10 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
             const bool dm = p_.method == M_AP;
             FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, bsk, dm ? bsk : bsk + (size_t)p_.n * p_.digitsG2 * 2 * p_.N,
                                                        d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, dm, s));
+            return;
+        }
+        if (g3_ && d_bsk2_ && ginx3_supported(g, tabs_) && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64) {
+            FHE_HIP_CHECK(launch_blind_rotate_ginx3(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_wext_a_, d_wext_b_, s));
             return;
         }
         FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_) + cur_off_, d_idx_, d_tvb_,

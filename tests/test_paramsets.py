@@ -75,3 +75,35 @@ def test_gpu_wider_paramset_gates_bit_exact_vs_reference(name):
     assert np.array_equal(np.concatenate(outs), g["out_a"].astype(np.uint64))
     assert np.array_equal(np.concatenate(outb), g["out_b"].astype(np.uint64))
     assert sha(np.concatenate(exts)) == str(g["ext_sha"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["std128_3", "std128q"])
+def test_gpu_digitsg4_split_kernel_matches_64bit_accumulator(name, monkeypatch):
+    """digitsG = 4 at N = 1024, Q < 2^27: the 32-bit split kernel with three digits per component
+    (launch_blind_rotate_ginx3, the default) against the 64-bit accumulator the set ran on before
+    (FHE_HIP_GINX3=0, bootstrap_wide.hip) on 777 gates of every 2-input type, final outputs and
+    extended ctExt; both also decrypt to the truth table"""
+    from fhe_amd import binfhe as bf
+    from make_golden import GATE_SETS
+    ps, m = GATE_SETS[name]
+    keys = bf.keygen(ps, m, 31)
+    B = 777
+    rng = np.random.default_rng(5)
+    x1, x2 = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 11)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 12)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FHE_HIP_GINX3", flag)
+        e = bf.GateEngine(ps, m, device=0)
+        e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        res[flag] = [(e.eval_gate(gate, a1, b1, a2, b2), e.eval_gate_extended(gate, a1, b1, a2, b2))
+                     for gate in GATES.values()]
+        e.close()
+    for (gname, gate), (fast, ref) in zip(GATES.items(), zip(res["1"], res["0"])):
+        for u, v in zip(fast, ref):
+            for s, t in zip(u, v):
+                assert np.array_equal(s, t), (name, gname)
+        dec = bf.decrypt(ps, m, keys.sk, fast[0][0], fast[0][1])
+        assert np.array_equal(dec, TRUTH[gate](x1, x2)), (name, gname)
