@@ -110,8 +110,9 @@ hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, con
                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 bool ginx2_supported(const GateArgs& g, const BootTables& t);
 // The same split kernel with three retained digits per component (digitsG = 4 at N = 1024, Q < 2^27:
-// STD128_3, STD128Q) for the sets whose keys otherwise live on the 64-bit accumulator: keys in the
-// g2_key_word layout (nd = 3), u64 ctExt into that path's workspace (launch_keyswitch_wide reads it)
+// STD128_3, STD128Q; with q = 2N: STD128_4, LPF_STD128, LPF_STD128Q) for the sets whose keys otherwise
+// live on the 64-bit accumulator: keys in the g2_key_word layout (nd = 3), u64 ctExt into that
+// path's workspace (launch_keyswitch_wide reads it)
 hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, const void* bsk3, const uint16_t* idx,
                                      const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
 bool ginx3_supported(const GateArgs& g, const BootTables& t);
@@ -166,6 +167,10 @@ hipError_t launch_lwe_reduce(const uint64_t* a, const uint64_t* b, uint64_t* ao,
 hipError_t launch_lwe_sub(const uint64_t* xa, const uint64_t* xb, const uint64_t* ya, const uint64_t* yb, uint64_t* oa,
                           uint64_t* ob, uint64_t m, uint32_t len, size_t count, hipStream_t s);
 hipError_t launch_lwe_addb(uint64_t* b, uint64_t c, uint64_t m, size_t count, hipStream_t s);
+// u64 [count][len] / [count] values below 2^32 -> u32 (the 64-bit path's ctExt mod qKS <= 2^16 into
+// the 32-bit key switch's input, for the digitsG = 4 sets of launch_blind_rotate_ginx3)
+hipError_t launch_narrow_u32(const uint64_t* a, const uint64_t* b, uint32_t* ao, uint32_t* bo, uint32_t len, size_t count,
+                             hipStream_t s);
 // ModSwitch on u64 vectors (lwe-pke.cpp:41-46, 254-261)
 hipError_t launch_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, uint32_t count, const uint64_t* a,
                             const uint64_t* b, uint64_t* a_out, uint64_t* b_out, hipStream_t s);

@@ -1734,7 +1734,8 @@ hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops
 // as in k_blind_rotate_ginx.  Half the registers of the one-wave kernel per wave, twice the waves.
 //   ND = 2 (digitsG = 3: STD128, MEDIUM ...): pinned by FHE_HIP_GINX_KERNEL=split (the one-wave kernel
 //          is faster at every batch size, DESIGN K1), u32 ctExt for the 32-bit key switch;
-//   ND = 3 (digitsG = 4 at N = 1024, Q < 2^27: STD128_3, STD128Q): the one-wave layout would need 96
+//   ND = 3 (digitsG = 4 at N = 1024, Q < 2^27: STD128_3, STD128Q, and with q = 2N STD128_4, LPF_STD128,
+//          LPF_STD128Q): the one-wave layout would need 96
 //          digit registers per lane, so these sets ran on the 64-bit accumulator (bootstrap_wide.hip);
 //          this instantiation runs them in 32-bit residues and writes the u64 ctExt of that path's
 //          workspace, which its key switch (keyswitch_wide) reads unchanged.
@@ -1845,7 +1846,9 @@ FHE_DEV void decompose_n(uint32_t x, const DecN& c, uint32_t (&d)[ND][16], int r
 }
 }  // namespace
 
-template <int ND, typename OutT>
+// MF: ciphertext modulus 2N (q = 2N sets: STD128_4, LPF_STD128, LPF_STD128Q): any exponent, the
+// full-resolution table psi^e - 1 restricted to e in [0, 2N] (the same LDS footprint as the half table)
+template <int ND, bool MF, typename OutT>
 __global__ void __launch_bounds__(128 * kG2Gates, 2)
     k_blind_rotate_ginx2(GateArgs g, BootTables T, const uint4* __restrict__ bsk2, const uint16_t* __restrict__ idx,
                          const uint32_t* __restrict__ tvb, OutT* __restrict__ ext_a, OutT* __restrict__ ext_b,
@@ -1861,7 +1864,8 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
         s_tab[i]  = T.tabF[i];
         s_tabI[i] = T.tabI[i];
     }
-    for (int i = threadIdx.x; i < kMonoHalfWords; i += blockDim.x) s_mono2[i] = make_uint2(T.monoP[i], T.mono[i]);
+    for (int i = threadIdx.x; i < kMonoHalfWords; i += blockDim.x)
+        s_mono2[i] = MF ? make_uint2(T.monoP_full[i], T.mono_full[i]) : make_uint2(T.monoP[i], T.mono[i]);
 
     const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
     const int c = wave & 1;  // RLWE component of this wave
@@ -1907,7 +1911,7 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m = fresh_nq(m0);
         const uint32_t a  = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
-        const uint32_t as = a >> 1;                         // even exponents (ctmod = q < 2N)
+        const uint32_t as = MF ? a : a >> 1;                // even exponents (ctmod = q < 2N) unless MF
         const uint4* kb   = kc + (size_t)i * (2 * kRows * 8 * 64);
         uint4 kq[2][kRows];
 #pragma unroll
@@ -1926,7 +1930,8 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
 #pragma unroll
             for (int j = 0; j < ND; ++j) region[j * 1024 + ((r << 6) | L)] = d[j][r];
         __syncthreads();   // both waves' digits are in LDS
-        const uint32_t fl = (as * lmul) & 1023u;
+        // MF: e = a (2 brv10(x) + 1) mod 2N = (el + ue) mod 2N, per-lane el and per-register ue
+        const uint32_t fl = (as * lmul) & (MF ? 2047u : 1023u);
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) {
             if (k2 + 1 < 8) {
@@ -1941,10 +1946,22 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
                        2u * (__builtin_bitreverse32((uint32_t)(r0 >> 2)) >> 30))) & 1023u);
             const uint32_t f  = fl + ur;                  // < 2N
             const uint32_t fn = 2048u - f;                // -a: 2N - f
-            const uint2 mp = s_mono2[f + (f >> 5)], mn = s_mono2[fn + (fn >> 5)];
+            uint2 mp, mn;
+            if (!MF) {
+                mp = s_mono2[f + (f >> 5)];
+                mn = s_mono2[fn + (fn >> 5)];
+            }
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = r0 + e;
+                if (MF) {  // x bit 0 adds 1024 a to the exponent: registers r0, r0 + 1 differ for odd a
+                    const uint32_t ue = __builtin_amdgcn_readfirstlane(
+                        (as * (512u * (__builtin_bitreverse32((uint32_t)(r & 3)) >> 30) +
+                               2u * (__builtin_bitreverse32((uint32_t)(r >> 2)) >> 30))) & 2047u);
+                    const uint32_t ef = (fl + ue) & 2047u, en = 2048u - ef;
+                    mp = s_mono2[ef + (ef >> 5)];
+                    mn = s_mono2[en + (en >> 5)];
+                }
                 uint32_t pd[ND];
 #pragma unroll
                 for (int j = 0; j < ND; ++j) pd[j] = partner[j * 1024 + ((r << 6) | L)];
@@ -2018,13 +2035,13 @@ hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, con
     if (g.count == 0) return hipSuccess;
     if (!ginx2_supported(g, t)) return hipErrorInvalidValue;
     const uint32_t blocks = (g.count + kG2Gates - 1) / kG2Gates;
-    hipLaunchKernelGGL((k_blind_rotate_ginx2<2, uint32_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(2), s, g, t,
+    hipLaunchKernelGGL((k_blind_rotate_ginx2<2, false, uint32_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(2), s, g, t,
                        static_cast<const uint4*>(bsk2), idx, tvb, ext_a, ext_b, t.twA_fwd);
     return hipGetLastError();
 }
 
 bool ginx3_supported(const GateArgs& g, const BootTables& t) {
-    return t.Q < (1u << 27) && g.N == 1024 && g.ctmod < 2 * g.N && g.tv == nullptr && g.tv64 == nullptr &&
+    return t.Q < (1u << 27) && g.N == 1024 && g.ctmod <= 2 * g.N && g.tv == nullptr && g.tv64 == nullptr &&
            g.acc_io == nullptr && g.gbits >= 2 && 4 * g.gbits <= 32 && g.qKS <= 65536;
 }
 
@@ -2032,12 +2049,21 @@ hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, con
                                      const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     if (!ginx3_supported(g, t)) return hipErrorInvalidValue;
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, uint64_t>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, false, uint64_t>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, true, uint64_t>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
+        return true;
+    }();
     (void)attr;
     const uint32_t blocks = (g.count + kG2Gates - 1) / kG2Gates;
-    hipLaunchKernelGGL((k_blind_rotate_ginx2<3, uint64_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s, g, t,
-                       static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd);
+    if (g.ctmod == 2 * g.N)
+        hipLaunchKernelGGL((k_blind_rotate_ginx2<3, true, uint64_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s,
+                           g, t, static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd);
+    else
+        hipLaunchKernelGGL((k_blind_rotate_ginx2<3, false, uint64_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s,
+                           g, t, static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd);
     return hipGetLastError();
 }
 

@@ -378,7 +378,8 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
         FHE_HIP_CHECK(hipMalloc(&d_wksk_, (nA + nB) * 8));
         FHE_HIP_CHECK(hipMemcpy(d_wksk_, A, nA * 8, hipMemcpyHostToDevice));
         FHE_HIP_CHECK(hipMemcpy(d_wksk_ + nA, B, nB * 8, hipMemcpyHostToDevice));
-        return;
+        if (!g3_) return;
+        // g3_: also the u16 rows of the 32-bit key switch (qKS <= 2^16, n < 1024; g3_set)
     }
     const size_t W = ksk_width(p_.n);
     std::vector<uint16_t> dev(rows * W, 0);
@@ -508,7 +509,8 @@ void Engine::ensure_work(size_t count) {
     if (wide_) {
         FHE_HIP_CHECK(hipMalloc(&d_wext_a_, count * p_.N * sizeof(uint64_t)));
         FHE_HIP_CHECK(hipMalloc(&d_wext_b_, count * sizeof(uint64_t)));
-    } else {
+    }
+    if (!wide_ || g3_) {  // g3_: the 32-bit key switch's input (keyswitch_ext)
         FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
         FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
     }
@@ -760,6 +762,15 @@ void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t*
 }
 
 void Engine::keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    if (wide_ && g3_ && d_ksk_ && d_ext_a_ && count <= cap_) {
+        // digitsG = 4 sets: the u64 ctExt mod qKS narrowed to u32, then the 32-bit (u16-row, gate-tiled
+        // for baseKS = 32) key switch instead of u64 row gathers
+        FHE_HIP_CHECK(launch_narrow_u32(d_wext_a_, d_wext_b_, d_ext_a_, d_ext_b_, p_.N, count, s));
+        GateArgs g = gate_args(G_AND, count);
+        FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, q_out, a_out, b_out, s,
+                                       ks_part(count), kKsPartWords));
+        return;
+    }
     if (wide_) {
         const size_t rows = p_.ksk_rows();
         FHE_HIP_CHECK(launch_keyswitch_wide(count, p_.n, p_.N, p_.baseKS, p_.digitsKS, p_.qKS, d_wksk_,

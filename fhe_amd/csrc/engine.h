@@ -179,9 +179,9 @@ private:
     static constexpr uint32_t kSplitBatch = 0;
     void* d_bsk2_ = nullptr;   // k_blind_rotate_ginx2 key layout (g3_: its nd = 3 layout)
     void repack_ginx2();
-    // digitsG = 4 GINX sets at N = 1024, Q < 2^27 (STD128_3, STD128Q): gates on the split kernel with
-    // three digits per component (launch_blind_rotate_ginx3) over the 32-bit tables tabs_, the rest
-    // of the 64-bit path unchanged.  FHE_HIP_GINX3=0 keeps them on the 64-bit accumulator (A/B, tests).
+    // digitsG = 4 GINX sets at N = 1024, Q < 2^27 (STD128_3, STD128Q, STD128_4, LPF_STD128, LPF_STD128Q):
+    // gates on the split kernel with three digits per component (launch_blind_rotate_ginx3) over the
+    // 32-bit tables tabs_, the rest of the 64-bit path unchanged.  FHE_HIP_GINX3=0 keeps them on the 64-bit accumulator (A/B, tests).
     bool g3_ = false;
     static bool g3_set(const Params& p);
     void pack_ginx3(const uint64_t* bsk);

@@ -35,6 +35,14 @@ __global__ void k_lwe_addb(uint64_t* b, uint64_t c, uint64_t m, size_t count) {
     }
 }
 
+__global__ void k_narrow_u32(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint32_t* __restrict__ ao,
+                             uint32_t* __restrict__ bo, uint64_t total, size_t count) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x)
+        ao[i] = (uint32_t)a[i];
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+        bo[i] = (uint32_t)b[i];
+}
+
 uint32_t grid_for(uint64_t work) { return (uint32_t)std::min<uint64_t>((work + 255) / 256, 8192); }
 }  // namespace
 
@@ -59,6 +67,14 @@ hipError_t launch_lwe_addb(uint64_t* b, uint64_t c, uint64_t m, size_t count, hi
     if (count == 0) return hipSuccess;
     if (c >= m) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_lwe_addb, dim3(grid_for(count)), dim3(256), 0, s, b, c, m, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow_u32(const uint64_t* a, const uint64_t* b, uint32_t* ao, uint32_t* bo, uint32_t len, size_t count,
+                             hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint64_t total = (uint64_t)count * len;
+    hipLaunchKernelGGL(k_narrow_u32, dim3(grid_for(total)), dim3(256), 0, s, a, b, ao, bo, total, count);
     return hipGetLastError();
 }
 

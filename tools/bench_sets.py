@@ -21,7 +21,7 @@ def dalloc(x):
     return d.value
 
 
-names = sys.argv[1:] or ["medium", "std128_3", "std128q", "lpf_std128", "std192", "std256", "std256q_4",
+names = sys.argv[1:] or ["medium", "std128_3", "std128q", "std128_4", "lpf_std128", "lpf_std128q", "std192", "std256", "std256q_4",
                          "std128_3_lmkcdey", "std128q_lmkcdey", "medium_ap"]
 for name in names:
     ps, m = GATE_SETS[name]
@@ -30,7 +30,7 @@ for name in names:
     keys = bf.keygen(ps, m, 7)
     e = bf.GateEngine(ps, m)
     e.load_keys(keys.bsk, keys.kskA, keys.kskB)
-    B = 8192 if bf.uses_fast_kernels(ps, m) else 2048
+    B = 8192 if P.N == 1024 and P.Q < (1 << 28) else 2048  # the 32-bit kernels (incl. the digitsG = 4 split one)
     x = np.random.default_rng(1).integers(0, 2, B)
     a1, b1 = bf.encrypt(ps, m, keys.sk, x, 1)
     a2, b2 = bf.encrypt(ps, m, keys.sk, x, 2)
