@@ -78,8 +78,8 @@ __global__ void __launch_bounds__(512)
 // staged in LDS once and every gate (one thread) subtracts the slice its digit
 // selects.  KSK gather traffic drops from 3 MB per gate to 12.6 MB per 256
 // gates; accumulation is packed u16 (v_pk_sub_u16: mod 2^16, hence exact mod
-// qKS = 2^14) with two columns per VGPR.  baseKS = 32 and digitsKS = 3 are
-// compile-time (both STD128 sets); a round covers 4 values of i (12 steps), so
+// qKS = 2^14) with two columns per VGPR.  baseKS = 32 or 64 and digitsKS = 3 are
+// compile-time (KsShape); at baseKS 32 a round covers 4 values of i (12 steps), so
 // the gate's a_i come as one 16-byte load per round, prefetched two rounds
 // ahead (a dependent a_i load per i was the kernel's critical path).
 // Below 4096 gates the per-gate kernel above fills the chip better.
@@ -102,46 +102,55 @@ constexpr int kKsCols  = FHE_KS_COLS;           // columns per workgroup (packed
 // 8-byte bank slot (17 d + k) mod 32, distinct for all 32 slices, so the random per-gate slice
 // choices never conflict (16-byte reads with a 144-B stride collide for slices d, d + 16).
 constexpr int kKsRowB  = kKsCols * 2 + (FHE_KS_B64 ? 8 : 16);
-constexpr int kKsParts = 32 * kKsCols * 2 / 16; // 16-byte parts staged per step (32 slices x 128 B)
 constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
-constexpr int kKsDigits = 3, kKsLogBase = 5;    // digitsKS, log2(baseKS)
+constexpr int kKsDigits = 3;                    // digitsKS
 #ifndef FHE_KS_IPR
 #define FHE_KS_IPR 4
 #endif
 #ifndef FHE_KS_G
 #define FHE_KS_G 256
 #endif
-constexpr int kKsIPR   = FHE_KS_IPR;            // values of i per round (4: one uint4 of a_i)
-constexpr int kKsStep  = kKsIPR * kKsDigits;    // (i, j) steps per round / LDS buffer / barrier
+constexpr int kKsIPR   = FHE_KS_IPR;            // values of i per round (4: one uint4 of a_i) at baseKS = 32
+// LOGB = log2(baseKS): 5 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 6 (STD128_3/4,
+// LPF_STD128Q: 64 slices, 2 values of i per round so that the double buffer keeps the same 104 KB;
+// slices d and d + 32 share a bank slot, a 2-way conflict)
+template <int LOGB> struct KsShape {
+    static constexpr int base  = 1 << LOGB;
+    static constexpr int ipr   = LOGB == 5 ? kKsIPR : 2;
+    static constexpr int step  = ipr * kKsDigits;                 // (i, j) steps per round / LDS buffer / barrier
+    static constexpr int parts = base * kKsCols * 2 / 16;         // 16-byte parts staged per step
+};
 
 // Row split (blockIdx.z, small batches): a workgroup sums the rounds [z R/S, (z+1) R/S) only and
 // writes its packed partial sums to part [S][count][W/2]; k_keyswitch_reduce adds the S partials
 // (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
 // 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
-template <int G, bool SPLIT>
+template <int G, bool SPLIT, int LOGB>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                       uint64_t* __restrict__ b_out, uint32_t* __restrict__ part) {
+    using S_ = KsShape<LOGB>;
+    constexpr int kKsParts = S_::parts, kKsStep = S_::step, kIPR = S_::ipr, kBase = S_::base;
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
-    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][32 * kKsRowB];
+    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][kBase * kKsRowB];
     const uint32_t t = threadIdx.x;
     const uint32_t gate = blockIdx.x * G + t;
     const bool valid = gate < g.count;
     const uint32_t col0 = blockIdx.y * kKsCols;
-    const uint32_t rounds = SPLIT ? g.N / kKsIPR / gridDim.z : g.N / kKsIPR;  // this workgroup's share
+    const uint32_t rounds = SPLIT ? g.N / kIPR / gridDim.z : g.N / kIPR;  // this workgroup's share
     const uint32_t r0 = SPLIT ? blockIdx.z * rounds : 0;
-    using AV = typename std::conditional<kKsIPR == 4, uint4, uint2>::type;
-    static_assert(kKsIPR == 4 || kKsIPR == 2, "a_i vector width");
+    using AV = typename std::conditional<kIPR == 4, uint4, uint2>::type;
+    static_assert(kIPR == 4 || kIPR == 2, "a_i vector width");
     const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N) + r0;
 
     // staging role: part x = t + G*r -> slice x / kKsPartsPerSlice, 16-byte part x % kKsPartsPerSlice
     auto slice_src = [&](uint32_t round, int q, int r) -> const uint4* {
         const uint32_t x = t + G * r, sd = x / kKsPartsPerSlice, sp = x % kKsPartsPerSlice;
-        const uint32_t i = (r0 + round) * kKsIPR + q / kKsDigits, j = q % kKsDigits;
-        const size_t row = ((size_t)i * (1u << kKsLogBase) + sd) * kKsDigits + j;
+        const uint32_t i = (r0 + round) * kIPR + q / kKsDigits, j = q % kKsDigits;
+        const size_t row = ((size_t)i * kBase + sd) * kKsDigits + j;
         return reinterpret_cast<const uint4*>(ksk + row * ksk_width(g.n) + col0) + sp;
     };
     auto slice_dst = [&](unsigned char* sb, int r) -> unsigned char* {
@@ -195,7 +204,7 @@ __global__ void __launch_bounds__(G)
         const uint32_t* as = reinterpret_cast<const uint32_t*>(&av);
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q) {
-            const uint32_t dig = (as[q / kKsDigits] >> (kKsLogBase * (q % kKsDigits))) & ((1u << kKsLogBase) - 1);
+            const uint32_t dig = (as[q / kKsDigits] >> (LOGB * (q % kKsDigits))) & (kBase - 1);
             if (FHE_KS_B64) {
                 const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kKsRowB);
                 uint2 w[kKsCols / 4];
@@ -298,16 +307,16 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     int tile = FHE_KS_TILE;
     // tiles need >= 16 x 8 workgroups to pay, or a row split (scratch) below 4096 gates
     if (tile == 0) tile = g.count >= 4096 || part ? 256 : 1;
-    if (tile > 1 && (logBase != (uint32_t)kKsLogBase || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
+    if (tile > 1 && ((logBase != 5 && logBase != 6) || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
     if (tile > 1) {
         const uint32_t S = part ? keyswitch_split(g.count, g.n, g.N, part_words) : 1;
         const dim3 grid((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols, S);
-        if (S > 1)
-            hipLaunchKernelGGL((k_keyswitch_tiled<FHE_KS_G, true>), grid, dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b,
-                               q_out, a_out, b_out, part);
-        else
-            hipLaunchKernelGGL((k_keyswitch_tiled<FHE_KS_G, false>), grid, dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b,
-                               q_out, a_out, b_out, nullptr);
+#define FHE_KS_LAUNCH(SP, LB)                                                                                   \
+    hipLaunchKernelGGL((k_keyswitch_tiled<FHE_KS_G, SP, LB>), grid, dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, \
+                       a_out, b_out, SP ? part : nullptr)
+        if (logBase == 5) { if (S > 1) FHE_KS_LAUNCH(true, 5); else FHE_KS_LAUNCH(false, 5); }
+        else { if (S > 1) FHE_KS_LAUNCH(true, 6); else FHE_KS_LAUNCH(false, 6); }
+#undef FHE_KS_LAUNCH
         if (S > 1) {
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

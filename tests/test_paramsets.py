@@ -107,3 +107,30 @@ def test_gpu_digitsg4_split_kernel_matches_64bit_accumulator(name, monkeypatch):
                 assert np.array_equal(s, t), (name, gname)
         dec = bf.decrypt(ps, m, keys.sk, fast[0][0], fast[0][1])
         assert np.array_equal(dec, TRUTH[gate](x1, x2)), (name, gname)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["std128_3", "std128q"])
+def test_gpu_digitsg4_keyswitch_vs_reference(name):
+    """the 32-bit key switch these sets now use (u16 rows of 1024 columns; gate-tiled with 64 staged
+    slices at baseKS = 64 (STD128_3), 32 at baseKS = 32 (STD128Q); row split below 4096) on uniform
+    inputs mod qKS, incl. a ragged last tile, vs the reference's own LWEEncryptionScheme::KeySwitch
+    (oracle/_ref, the restatement covers the STD128 sets only)"""
+    from fhe_amd import binfhe as bf
+    from make_golden import GATE_SETS
+    from oracle_lib import Ref
+    ps, m = GATE_SETS[name]
+    keys = bf.keygen(ps, m, 41)
+    O = Ref(ps, m)
+    O.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    e = bf.GateEngine(ps, m, device=0)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    P = e.params
+    rng = np.random.default_rng(78)
+    for count in (300, 4096 + 259):
+        a = rng.integers(0, P.qKS, (count, P.N), dtype=np.uint64)
+        b = rng.integers(0, P.qKS, count, dtype=np.uint64)
+        ga, gb = e.keyswitch(a, b)
+        oa, ob = O.keyswitch(a, b)
+        assert np.array_equal(ga, oa) and np.array_equal(gb, ob), count
+    e.close()
