@@ -116,6 +116,13 @@ bool ginx2_supported(const GateArgs& g, const BootTables& t);
 hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, const void* bsk3, const uint16_t* idx,
                                      const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
 bool ginx3_supported(const GateArgs& g, const BootTables& t);
+// LMKCDEY on the same split layout (k_blind_rotate_lmk3) for the digitsG = 4 LMKCDEY sets at N = 1024,
+// Q < 2^27 (STD128_4_LMKCDEY, STD128Q_3_LMKCDEY, LPF_STD128Q_LMKCDEY): op lists of launch_prep_lmk,
+// keys ek [n][c][p < 6][k4 < 4][64][4] (rows g2_row(c, p, 3)) and ak [numAutoKeys + 1][c][d < 3][k4][64][4]
+// (Engine::pack_ginx3), u64 ctExt into the 64-bit path's workspace
+hipError_t launch_blind_rotate_lmk3(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
+                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                    uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
 // split-kernel key layout, per index i (8192 nd words): [c][p < 2 nd][k2 < 8][64 lanes][4 words]
 // = (K+[r], K+[r+1], K-[r], K-[r+1]) of component c, digit row g2_row(c, p, nd), r = 2 k2, EVAL slot
 // x(L, r) = ((r >> 2) << 8) | (L << 2) | (r & 3): wave c multiplies (own digits D_c, D_{2+c}, ..,

@@ -2068,6 +2068,227 @@ hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, con
 }
 
 // ---------------------------------------------------------------------------
+// LMKCDEY on the split layout: k_blind_rotate_lmk3 (RingGSWAccumulatorLMKCDEY::EvalAcc,
+// rgsw-acc-lmkcdey.cpp:70-287) for the digitsG = 4 sets at N = 1024, Q < 2^27 (STD128_4_LMKCDEY,
+// STD128Q_3_LMKCDEY, LPF_STD128Q_LMKCDEY), which otherwise run K5's op-list form.  One gate per
+// 128-thread workgroup (op lists differ per gate, so a workgroup barrier may only join the two waves
+// of one gate); wave c owns component c in layout C as k_blind_rotate_ginx2.  The op list of
+// k_prep_lmk_w, per op:
+//   EXT(i)  (AddToAccLMKCDEY, :228-254): both waves decompose their component into 3 digits and
+//           forward-transform them, exchange through LDS, acc_c <- sum_{p<6} D_p ek[i][row p][c];
+//   AUTO(t) (Automorphism, :257-287): both components permuted in EVAL through the wave's region;
+//           wave 0 inverse-transforms acc0', decomposes it into 3 digits and forward-transforms
+//           them; acc0 <- sum_d D_d ak[t][d][0], acc1 <- acc1' + sum_d D_d ak[t][d][1].
+// Keys (Engine::pack_ginx3, u32 Montgomery with N^-1 folded in), one uint4 = 4 registers:
+//   ek: [i][c][p < 6][k4 < 4][64 lanes] rows g2_row(c, p, 3);  ak: [t][c][d < 3][k4 < 4][64 lanes].
+// Bounds (Q < 2^27): |D| < 10 Q + 2^6, |S| < 61 Q^2 < 2^60, acc < 61 Q / 32 + Q / 2 < 2.8 Q.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kL3Reg = 3 * kG2Tile;  // words per wave: 3 tiles / the 3 digit polynomials / a permutation
+constexpr size_t l3_lds() { return (size_t)(1024 + 1024 + 2 * kL3Reg) * 4; }
+// EVAL automorphism X -> X^k (as automorphism_eval) on layout C through this wave's region:
+// slot x(L, r) has brv10(x) = brv2(r & 3) << 8 | brv6(L) << 2 | brv2(r >> 2), so
+// (2 brv10(x) + 1) k = k (8 brv6(L) + 1) + k (512 brv2(r & 3) + 2 brv2(r >> 2))
+FHE_DEV void automorphism_c(uint32_t (&v)[16], uint32_t* region, int L, uint32_t k) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t x = ((uint32_t)(r >> 2) << 8) | ((uint32_t)L << 2) | (uint32_t)(r & 3);
+        region[x + (x >> 5)] = v[r];
+    }
+    wave_lds_sync();
+    const uint32_t cl = (8 * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1) * k;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t sr = (512u * (__builtin_bitreverse32((uint32_t)(r & 3)) >> 30) +
+                             2u * (__builtin_bitreverse32((uint32_t)(r >> 2)) >> 30)) * k;  // uniform
+        const uint32_t t  = ((cl + sr) & 2047u) >> 1;
+        const uint32_t sx = __builtin_bitreverse32(t) >> 22;  // source slot brv10(t)
+        v[r] = region[sx + (sx >> 5)];
+    }
+    wave_lds_sync();
+}
+}  // namespace
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
+    k_blind_rotate_lmk3(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
+                        const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
+                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
+                        const uint32_t* __restrict__ twAf) {
+    constexpr int ND = 3, kRows = 2 * ND;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_tab  = sm;
+    uint32_t* s_tabI = sm + 1024;
+    uint32_t* s_reg  = sm + 2048;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        s_tab[i]  = T.tabF[i];
+        s_tabI[i] = T.tabI[i];
+    }
+    const int c = threadIdx.x >> 6, L = threadIdx.x & 63;  // wave c: RLWE component c
+    const uint32_t gate = blockIdx.x;
+    uint32_t* region  = s_reg + c * kL3Reg;
+    uint32_t* partner = s_reg + (c ^ 1) * kL3Reg;
+    uint32_t* t0 = region;
+    const Mod m0 = make_mod(T);
+    const Mod& m = m0;
+    const uint32_t M = 2 * g.N;
+    __syncthreads();
+
+    // BootstrapGateCore (binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0; then
+    // acc1 <- acc1(X^(2N-5)) (:99; acc0 = 0 is invariant)
+    uint32_t acc[16];
+    if (c == 1) {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        uint32_t tv[1][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            uint32_t v = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            tv[0][r] = v;
+        }
+        fwd_wave_s<1>(tv, t0, L, twAf, s_tab, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);
+        automorphism_c(acc, region, L, M - 5);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0;
+    }
+
+    const DecN dec = make_decn(m.Q, g.gbits, ND);
+    const uint16_t* gops = ops + (size_t)gate * maxops;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(nops[gate]);
+    const uint32_t oneR1 = c ? m0.oneR : 0u;  // automorphism: acc1 accumulates, acc0 is replaced
+    for (uint32_t it = 0; it < cnt; ++it) {
+        const Mod m = fresh_nq(m0);
+        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+        __syncthreads();  // the partner wave has read this wave's region (previous op)
+        uint32_t d[ND][16];
+        if (!(op & 0x8000u)) {
+            // ---- AddToAccLMKCDEY: acc_c <- sum_p D_p ek[op][g2_row(c, p)][c]   (acc replaced)
+            const uint4* kb = ek + ((size_t)op * 2 + c) * (kRows * 4 * 64) + L;
+            uint4 kq[2][kRows];
+#pragma unroll
+            for (int p = 0; p < kRows; ++p) kq[0][p] = kb[(p * 4 + 0) * 64];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
+            inv_wave_s<kAccBoundLZ, true>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+            fwd_wave_s<ND>(d, t0, L, twAf, s_tab, m);
+            wave_lds_sync();
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+#pragma unroll
+                for (int j = 0; j < ND; ++j) region[j * 1024 + ((r << 6) | L)] = d[j][r];
+            __syncthreads();  // both waves' digits are in LDS
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+                if (k4 + 1 < 4) {
+#pragma unroll
+                    for (int p = 0; p < kRows; ++p) kq[(k4 + 1) & 1][p] = kb[(p * 4 + k4 + 1) * 64];
+                }
+                asm volatile("" ::: "memory");
+                const uint4* q = kq[k4 & 1];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * k4 + e;
+                    int64_t S = 0;
+#pragma unroll
+                    for (int p = 0; p < kRows; ++p) {
+                        const int32_t dv = (int32_t)(p < ND ? d[p][r] : partner[(p - ND) * 1024 + ((r << 6) | L)]);
+                        const uint32_t kv = e == 0 ? q[p].x : e == 1 ? q[p].y : e == 2 ? q[p].z : q[p].w;
+                        S += (int64_t)dv * (int32_t)kv;
+                    }
+                    acc[r] = smont_red(S, m);
+                }
+            }
+        } else {
+            // ---- Automorphism(5^t or 2N-5, ak[t])
+            const uint32_t t = op & 0x7fffu;
+            uint32_t kexp = M - 5;
+            if (t) {
+                kexp = 1;
+                for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
+            }
+            const uint4* kb = ak + ((size_t)t * 2 + c) * (ND * 4 * 64) + L;
+            uint4 kq[2][ND];
+#pragma unroll
+            for (int p = 0; p < ND; ++p) kq[0][p] = kb[(p * 4 + 0) * 64];
+            automorphism_c(acc, region, L, kexp);
+            if (c == 0) {  // acc0' -> COEF -> 3 digits -> EVAL, to this wave's region
+#pragma unroll
+                for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
+                inv_wave_s<kAccBoundLZ, true>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+                fwd_wave_s<ND>(d, t0, L, twAf, s_tab, m);
+                wave_lds_sync();
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) region[j * 1024 + ((r << 6) | L)] = d[j][r];
+            }
+            __syncthreads();  // acc0's digits are in wave 0's region
+            const uint32_t* src = c == 0 ? region : partner;
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+                if (k4 + 1 < 4) {
+#pragma unroll
+                    for (int p = 0; p < ND; ++p) kq[(k4 + 1) & 1][p] = kb[(p * 4 + k4 + 1) * 64];
+                }
+                asm volatile("" ::: "memory");
+                const uint4* q = kq[k4 & 1];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * k4 + e;
+                    int64_t S = (int64_t)(int32_t)acc[r] * (int32_t)oneR1;
+#pragma unroll
+                    for (int p = 0; p < ND; ++p) {
+                        const int32_t dv = (int32_t)src[p * 1024 + ((r << 6) | L)];
+                        const uint32_t kv = e == 0 ? q[p].x : e == 1 ? q[p].y : e == 2 ? q[p].z : q[p].w;
+                        S += (int64_t)dv * (int32_t)kv;
+                    }
+                    acc[r] = smont_red(S, m);
+                }
+            }
+        }
+    }
+
+    // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_ginx2
+    __syncthreads();
+    inv_wave_s<kAccBoundLZ, true>(acc, t0, L, s_tabI, T.w1R, m.oneR, m);
+    if (c == 0) {
+        uint64_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            const uint32_t v = acc[r];
+            const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
+            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+        }
+    } else if (L == 0) {
+        const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
+        ext_b[gate] = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+hipError_t launch_blind_rotate_lmk3(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
+                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                    uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!(t.Q < (1u << 27) && g.N == 1024 && g.tv == nullptr && g.tv64 == nullptr && g.acc_io == nullptr &&
+          g.gbits >= 2 && 4 * g.gbits <= 32 && g.qKS <= 65536))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_blind_rotate_lmk3, dim3(g.count), dim3(128), l3_lds(), s, g, t, static_cast<const uint4*>(ek),
+                       static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a, ext_b, t.twA_fwd);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // ExternalProduct seam (Backend::ExternalProduct[Batch], backend.h:141-146, 187-192): per-item
 // RGSW keys in the reference's raw EVAL layout [dG2 = 4][2][N] packed into the op-list kernel's
 // resident layout (the layout Engine::load_bsk writes), then one EXT op per item.

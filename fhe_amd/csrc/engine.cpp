@@ -29,17 +29,48 @@ bool Engine::g3_set(const Params& p) {
     // digit fields of d + C in 32 bits (bootstrap.hip decompose_n): 4 g <= 32 and C + Q < 2^32
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
     const uint64_t C = h * (1 + (1ull << g) + (1ull << (2 * g)) + (1ull << (3 * g)));
-    return !is_large(p.paramset) && !p.timeopt && p.method == M_GINX && p.N == 1024 && p.Q < (1ull << 27) &&
-           p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.qKS <= 65536;
+    return !is_large(p.paramset) && !p.timeopt && (p.method == M_GINX || p.method == M_LMKCDEY) && p.N == 1024 &&
+           p.Q < (1ull << 27) &&
+           p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.qKS <= 65536 && p.n < 1024;
 }
 
-// the split kernel's nd = 3 key layout (boot.h g2_key_word) from the raw BSK [n][2][dG2 = 8][2][N],
-// u32 Montgomery with N^-1 folded in (as the resident 32-bit layouts)
+// the split kernels' nd = 3 key layouts, u32 Montgomery with N^-1 folded in (as the resident 32-bit
+// layouts).  GINX (boot.h g2_key_word) from the raw BSK [n][2][dG2 = 8][2][N]; LMKCDEY
+// (launch_blind_rotate_lmk3) from [n][dG2][2][N] ++ [numAutoKeys + 1][3][2][N]
 void Engine::pack_ginx3(const uint64_t* bsk) {
     const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
     const uint64_t Q = p_.Q, ninv = invmod(N, Q);
-    const size_t per = 8192 * 3;
-    std::vector<uint32_t> dev((size_t)n * per);
+    const bool lmk = p_.method == M_LMKCDEY;
+    const size_t per = lmk ? 12288 : 8192 * 3, nauto = lmk ? (size_t)p_.numAutoKeys + 1 : 0;
+    std::vector<uint32_t> dev((size_t)n * per + nauto * 6144);
+    auto word = [&](uint64_t v) { return to_mont(mulmod(v % Q, ninv, Q), Q); };
+    if (lmk) {
+        // ek [i][c][p < 6][k4 < 4][64][4]: register r = 4 k4 + e of lane L is slot x(L, r)
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < (int64_t)n; ++i)
+            for (uint32_t c = 0; c < 2; ++c)
+                for (uint32_t p = 0; p < 6; ++p)
+                    for (uint32_t k4 = 0; k4 < 4; ++k4)
+                        for (uint32_t L = 0; L < 64; ++L)
+                            for (uint32_t e = 0; e < 4; ++e) {
+                                const uint32_t x = (k4 << 8) | (L << 2) | e;
+                                const size_t src = (((size_t)i * dG2 + g2_row(c, p, 3)) * 2 + c) * N + x;
+                                dev[(size_t)i * per + ((((c * 6 + p) * 4 + k4) * 64 + L) * 4 + e)] = word(bsk[src]);
+                            }
+        // ak [t][c][d < 3][k4][64][4]
+        const uint64_t* asrc = bsk + (size_t)n * dG2 * 2 * N;
+        uint32_t* adst = dev.data() + (size_t)n * per;
+        for (size_t t = 0; t < nauto; ++t)
+            for (uint32_t c = 0; c < 2; ++c)
+                for (uint32_t dd = 0; dd < 3; ++dd)
+                    for (uint32_t k4 = 0; k4 < 4; ++k4)
+                        for (uint32_t L = 0; L < 64; ++L)
+                            for (uint32_t e = 0; e < 4; ++e) {
+                                const uint32_t x = (k4 << 8) | (L << 2) | e;
+                                adst[t * 6144 + ((((c * 3 + dd) * 4 + k4) * 64 + L) * 4 + e)] =
+                                    word(asrc[((t * 3 + dd) * 2 + c) * N + x]);
+                            }
+    } else
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < (int64_t)n; ++i)
         for (uint32_t c = 0; c < 2; ++c)
@@ -213,6 +244,7 @@ void Engine::build_tables() {
 
 // logGen of rgsw-cryptoparameters.cpp:115-127 (k_prep_lmk_w's group positions)
 void Engine::build_loggen() {
+    if (d_logGen_) return;
     const uint32_t M = 2 * p_.N;
     std::vector<int16_t> lg(M, 0);
     uint32_t gp = 1;
@@ -568,6 +600,13 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.b_const = g.b64;
         w.qKS = p_.qKS;
         w.tv = g.tv64;
+        if (g3_ && p_.method == M_LMKCDEY && d_bsk2_ && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64 &&
+            !g.tv && !g.tv64 && !g.acc_io) {
+            const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);
+            FHE_HIP_CHECK(launch_blind_rotate_lmk3(g, tabs_, ek, ek + (size_t)p_.n * 12288, d_ops_, d_nops_, maxops_,
+                                                   d_tvb_, d_wext_a_, d_wext_b_, s));
+            return;
+        }
         if (p_.method == M_LMKCDEY || p_.method == M_AP) {
             const uint64_t* bsk = static_cast<const uint64_t*>(d_bsk_);
             const bool dm = p_.method == M_AP;

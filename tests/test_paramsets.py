@@ -78,10 +78,12 @@ def test_gpu_wider_paramset_gates_bit_exact_vs_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["std128_3", "std128q", "std128_4", "lpf_std128", "lpf_std128q"])
+@pytest.mark.parametrize("name", ["std128_3", "std128q", "std128_4", "lpf_std128", "lpf_std128q", "std128_4_lmkcdey",
+                                  "std128q_3_lmkcdey", "lpf_std128q_lmkcdey"])
 def test_gpu_digitsg4_split_kernel_matches_64bit_accumulator(name, monkeypatch):
     """digitsG = 4 at N = 1024, Q < 2^27 (q = 1024, and q = 2N: the full monomial table): the 32-bit
-    split kernel with three digits per component (launch_blind_rotate_ginx3, the default) against the 64-bit accumulator the set ran on before
+    split kernels with three digits per component (launch_blind_rotate_ginx3; LMKCDEY:
+    launch_blind_rotate_lmk3, the default) against the 64-bit accumulator the set ran on before
     (FHE_HIP_GINX3=0, bootstrap_wide.hip) on 777 gates of every 2-input type, final outputs and
     extended ctExt; both also decrypt to the truth table"""
     from fhe_amd import binfhe as bf
