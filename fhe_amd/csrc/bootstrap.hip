@@ -1743,7 +1743,10 @@ hipError_t launch_prep_dm(const GateArgs& g, const GateInputs& in, uint16_t* ops
 // |S+-| < 2 ND (10 Q + 2^(g-1)) Q < 2^60; S < 2 (2^32 Q + 2 ND 0.32 Q^2) + 2.8 Q^2, so the reduced
 // acc stays below 2.8 Q (kAccBoundLZ) for ND <= 3.
 namespace {
-constexpr int kG2Gates = 2;     // gates per workgroup (2 waves each)
+#ifndef FHE_G2_GATES
+#define FHE_G2_GATES 2
+#endif
+constexpr int kG2Gates = FHE_G2_GATES;  // gates per workgroup (2 waves each)
 constexpr int kG2Tile  = 1088;  // one tile (1024 + 64 pad, wt64 addressing)
 // words per wave: ND transpose tiles, which also hold the ND digit polynomials of the exchange
 constexpr int g2_region(int nd) { return nd * kG2Tile; }
