@@ -136,3 +136,33 @@ def test_gpu_digitsg4_keyswitch_vs_reference(name):
         oa, ob = O.keyswitch(a, b)
         assert np.array_equal(ga, oa) and np.array_equal(gb, ob), count
     e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["std128_3", "std128_4_lmkcdey"])
+def test_gpu_digitsg4_multi_input_gates_vs_reference(name):
+    """MAJORITY / AND3 / OR3 / AND4 / OR4 / CMUX (binfhe-base-scheme.cpp:129-187) on the split kernels
+    (K1s GINX, K1m LMKCDEY) over every input combination, against the reference's own
+    EvalBinGate(gate, ctvector) (oracle/_ref) on the same keys and ciphertexts"""
+    from fhe_amd import binfhe as bf
+    from make_golden import GATE_SETS, multi_inputs
+    from oracle_lib import Ref
+    truth = {"MAJORITY": lambda b: b.sum(1) >= 2, "AND3": lambda b: b.all(1), "OR3": lambda b: b.any(1),
+             "AND4": lambda b: b.all(1), "OR4": lambda b: b.any(1),
+             "CMUX": lambda b: np.where(b[:, 2] == 1, b[:, 1], b[:, 0])}
+    ps, m = GATE_SETS[name]
+    keys, cases = multi_inputs(ps, m, 0xD4 + ps)
+    ref = Ref(ps, m)
+    ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    e = bf.GateEngine(ps, m, device=0)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    for gname, (gate, k, p, bits, A, B) in cases.items():
+        if gname == "CMUX":
+            ao, bo = e.eval_cmux(A[0], B[0], A[1], B[1], A[2], B[2])
+        else:
+            ao, bo = e.eval_gate_multi(gate, A, B, p)
+        ra, rb = ref.eval_gate_multi(gate, A, B, p)
+        assert np.array_equal(ao, ra) and np.array_equal(bo, rb), (name, gname)
+        dec = bf.decrypt(ps, m, keys.sk, ao, bo, p=p)
+        assert np.array_equal(dec, truth[gname](bits).astype(np.int64)), (name, gname)
+    e.close()
