@@ -4,6 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--total T | --batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+With --gpus N > 1 and no launcher (WORLD_SIZE unset) bench.py starts the torch.distributed.run
+child itself (N ranks, one per GPU) and exits with its return code.
+
 A step = one EvalBinGate(AND) pass over BASELINE config 4's global batch of T = 65,536
 independent STD128 GINX gate pairs, sharded contiguously over the N ranks (strong
 scaling: T / N gates per GPU, no data-path collective), inputs resident in HBM:
@@ -114,9 +117,11 @@ def golden_check(name, lo, hi, total, ao, bo):
     return all(_sha(ao[s - lo:s - lo + S]) + _sha(bo[s - lo:s - lo + S]) == shards[s // S] for s in range(lo, hi, S))
 
 
-def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=True):
+def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None):
     """Times K steps of EvalBinGate(AND) over gates [lo, hi) of a `total`-gate batch on this
-    rank; returns the per-rank measurements (elapsed is max-reduced by the caller)."""
+    rank; returns the per-rank measurements (elapsed is max-reduced by the caller).  golden: the
+    tests/golden/full_<golden>.npz reference hashes the outputs are checked against (default: the
+    65,536-gate batch of the method)."""
     from fhe_amd.dist import barrier
     dev, stream, sp = ctx["dev"], ctx["stream"], ctx["stream"].cuda_stream
     ps, method = (bf.STD128, bf.GINX) if method_name == "ginx" else (bf.STD128_LMKCDEY, bf.LMKCDEY)
@@ -161,7 +166,7 @@ def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=True):
     bo = d_bo.cpu().numpy().view(np.uint64)
     dec = bf.decrypt(ps, method, keys.sk, ao, bo)
     verified = bool(np.array_equal(dec, (x1[lo:hi] & x2[lo:hi]).astype(np.int64)))
-    exact = golden_check("std128" if method_name == "ginx" else "lmkcdey", lo, hi, total, ao, bo) if golden else None
+    exact = golden_check(golden or ("std128" if method_name == "ginx" else "lmkcdey"), lo, hi, total, ao, bo)
     eng.close()
     return {"elapsed": elapsed, "br_ms": br_ms, "ks_ms": ks_ms, "verified": verified, "exact": exact, "B": B,
             "keys": keys, "inputs": (a1[lo:hi], b1[lo:hi], a2[lo:hi], b2[lo:hi]), "out": (ao, bo), "ps": ps,
@@ -197,15 +202,50 @@ def rooflines(method_name, B, br_ms, ks_ms):
     return roofline, valu
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args):
+    """`python bench.py --gpus N` (N > 1) without a launcher: run N ranks, one process per GPU, as a
+    torch.distributed.run child (started before anything touches the GPU: device_count() does not
+    initialise it), relay its output and exit with its return code.  Fewer than N devices is an
+    error unless FHE_BENCH_DEVICE_MAP places the ranks (the one-GPU rehearsal)."""
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    dmap = os.environ.get("FHE_BENCH_DEVICE_MAP")
+    if dmap:
+        devs = [int(x) for x in dmap.split(",")]
+        if len(devs) < args.gpus or max(devs) >= have:
+            log(f"error: FHE_BENCH_DEVICE_MAP={dmap} does not place {args.gpus} ranks on the {have} device(s)")
+            return 2
+    elif have < args.gpus:
+        log(f"error: --gpus {args.gpus} but only {have} GPU(s) are visible")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching", args.gpus, "ranks:", " ".join(cmd))
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
     from fhe_amd.dist import max_over_ranks, shard
     rank, world, local = env_rank()
     if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} differs from --gpus={args.gpus}; using WORLD_SIZE")
+        log(f"error: WORLD_SIZE={world} differs from --gpus={args.gpus}")
+        sys.exit(2)
     # rehearsal knobs (not used by the driver): FHE_BENCH_DEVICE_MAP="0,0" puts ranks on
     # chosen devices, FHE_BENCH_BACKEND=gloo for a one-GPU box
     dmap = os.environ.get("FHE_BENCH_DEVICE_MAP")
@@ -278,14 +318,15 @@ def main():
                 "roofline": lr, "valu_roofline": lv, "cpu_baseline": None,
             }
     if world == 1 and not args.no_config3 and args.method == "ginx":
-        c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden=False)
+        c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden="std128_b1024")
         r3, v3 = rooflines("ginx", 1024, c3["br_ms"], c3["ks_ms"])
         alg3 = BSK_BYTES["ginx"] + KSK_BYTES["ginx"] + 1024 * (IN_BYTES_PER_GATE["ginx"] + OUT_BYTES_PER_GATE["ginx"])
         step_s = c3["elapsed"] / args.steps
         result["config3"] = {
             "config": "BASELINE config 3: STD128 GINX EvalBinGate(AND), 1024 gates, 1 GPU",
             "value": round(1024 / step_s, 1), "unit": "bootstraps/s", "ms_per_step": round(step_s * 1e3, 3),
-            "verified": c3["verified"], "valu_roofline": v3, "blind_rotate_ms": r3["launch_ms"],
+            "verified": c3["verified"], "bit_exact_vs_reference": c3["exact"],
+            "valu_roofline": v3, "blind_rotate_ms": r3["launch_ms"],
             "keyswitch_ms": r3["keyswitch_ms"],
             "hbm_frac_compulsory": round(alg3 / step_s / 1e9 / HBM_PEAK_GBS, 6),
             "hbm_basis": "SURVEY 8(d) config 3: BSK + KSK + 1024 x I/O = 474,677,248 B per batch / step time",

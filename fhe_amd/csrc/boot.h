@@ -87,6 +87,11 @@ struct GateArgs {
     // instead of being built from the test vector, and the final one is written back there in the
     // same form instead of the extraction / ModSwitch epilogue.
     uint64_t* acc_io;
+    // with acc_io: 1 = the initial accumulator is BootstrapGateCore's test vector (0, NTT(m))
+    // (binfhe-base-scheme.cpp:556-575) from the gate window and tvb, as for a gate, instead of acc_io's
+    // contents -- the seam's null accumulators (BootstrapBatch, batch.cpp:77-86); the final
+    // accumulator still goes to acc_io
+    uint32_t acc_tv;
 };
 
 // The LWE ciphertext a gate bootstraps: ct = sum_j (-1)^{neg_j} ct_j + (0, boff) mod q, then

@@ -36,6 +36,11 @@ struct WideArgs {
     uint64_t b_const;            // added to acc1[0]
     uint64_t qKS;
     const uint64_t* tv;          // BootstrapFunc test vector (Q / fmod) f(x), x < ctmod; null: gate window
+    // Backend::BlindRotate / ExternalProduct seam (GateArgs::acc_io / acc_tv): non-null = the final
+    // accumulator goes to acc_io[count][2][N] (EVALUATION, canonical) instead of the extraction; the
+    // initial one is read from there too unless acc_tv (then the test vector above, as for a gate)
+    uint64_t* acc_io;
+    uint32_t acc_tv;
 };
 
 hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
@@ -47,6 +52,10 @@ hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, 
                                         const uint64_t* autok, const uint16_t* ops, const uint32_t* nops,
                                         uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
                                         bool dm, hipStream_t s);
+// ExternalProduct seam: raw RGSW words (< Q) -> the Montgomery form of the op-list kernel's keys;
+// R2 = 2^128 mod Q, qinv = -Q^-1 mod 2^64 (WideTables::qinv)
+hipError_t launch_pack_rgsw_wide(const uint64_t* raw, size_t words, uint64_t Q, uint64_t qinv, uint64_t R2, uint64_t* out,
+                                 hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) mod qKS = 2^k with u64 rows A [rows][n], B [rows], then
 // ModSwitch(qKS -> q_out) (q_out = 0: none); ms_a [count][N], ms_b [count] mod qKS
 hipError_t launch_keyswitch_wide(size_t count, uint32_t n, uint32_t N, uint32_t baseKS, uint32_t digitsKS, uint64_t qKS,

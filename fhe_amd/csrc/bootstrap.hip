@@ -669,7 +669,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 
     // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[32];
-    if (ACCIO) {
+    if (ACCIO && !g.acc_tv) {
         acc_load(acc, g, gate, h, l, T.ninvR, m);
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
@@ -1198,7 +1198,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
     const uint32_t M = 2 * g.N;
 
     uint32_t acc[32];
-    if (ACCIO) {
+    if (ACCIO && !g.acc_tv) {
         acc_load(acc, g, gate, h, l, T.ninvR, m);
         // acc1 <- acc1(X^(2N-5)) (:99) on half 1 only: X^1 (the identity) on half 0
         if (!DM) automorphism_eval(acc, tile, l, h ? M - 5 : 1u);

@@ -16,6 +16,8 @@
 // Keys are read straight from HBM, coalesced (consecutive threads, consecutive slots).
 #include "boot_wide.h"
 
+#include <algorithm>
+
 // waves per SIMD the blind-rotation kernel is compiled for (VGPR budget 512 / waves)
 #ifndef FHE_WIDE_WAVES
 #define FHE_WIDE_WAVES 4
@@ -233,7 +235,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
     // test vector (BootstrapGateCore binfhe-base-scheme.cpp:556-575 / BootstrapFuncCore :596-608):
     // acc1 = NTT(m), acc0 = 0
     uint64_t acc0[S], acc1[S];
-    {
+    if (g.acc_io && !g.acc_tv) {  // the seam's accumulator (EvalAcc on a given acc)
+        const uint64_t* src = g.acc_io + (size_t)gate * 2 * N;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            acc0[r] = src[t + T * r];
+            acc1[r] = src[N + t + T * r];
+        }
+    } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
@@ -336,6 +345,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
         }
     }
 
+    if (g.acc_io) {  // the seam: the accumulator itself (block-uniform branch)
+        uint64_t* dst = g.acc_io + (size_t)gate * 2 * N;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            dst[t + T * r]     = acc0[r];
+            dst[N + t + T * r] = acc1[r];
+        }
+        return;
+    }
     // extraction (binfhe-base-scheme.cpp:110-121, :616-626): Transpose(acc0) then COEF: coefficient
     // k of acc0(X^-1) is -a_(N-k) (k >= 1), a_0 for k = 0; b = b_const + acc1[0]
     __syncthreads();
@@ -394,7 +412,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
     const uint32_t dA = g.digitsG - 1, dG2 = 2 * dA, gb = g.gbits, sh = 64 - gb;
 
     uint64_t acc0[S], acc1[S];
-    {
+    if (g.acc_io && !g.acc_tv) {  // the seam's accumulator; LMKCDEY's acc1 <- sigma_(2N-5)(acc1) (:99)
+        const uint64_t* src = g.acc_io + (size_t)gate * 2 * N;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            acc0[r] = src[t + T * r];
+            acc1[r] = src[N + (DM ? t + T * r : auto_src<LOGN>(t + T * r, 2 * N - 5))];
+        }
+    } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
@@ -530,6 +555,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
         }
     }
 
+    if (g.acc_io) {
+        uint64_t* dst = g.acc_io + (size_t)gate * 2 * N;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            dst[t + T * r]     = acc0[r];
+            dst[N + t + T * r] = acc1[r];
+        }
+        return;
+    }
     // extraction as k_blind_rotate_wide
     __syncthreads();
 #pragma unroll
@@ -575,6 +609,24 @@ hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, 
         else FHE_WIDE_OPS(9, false);
     }
 #undef FHE_WIDE_OPS
+    return hipGetLastError();
+}
+
+// ExternalProduct seam: raw RGSW rows (canonical mod Q) -> Montgomery form x 2^64 mod Q, the form
+// k_blind_rotate_wide_ops reads its keys in: redc(x R2) with R2 = 2^128 mod Q (x R2 < Q^2 < Q 2^64)
+__global__ void k_pack_rgsw_wide(const uint64_t* __restrict__ raw, size_t words, uint64_t Q, uint64_t qinv, uint64_t R2,
+                                 uint64_t* __restrict__ out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t x = raw[i];
+        out[i] = redc(U128{x * R2, __umul64hi(x, R2)}, Q, qinv);
+    }
+}
+
+hipError_t launch_pack_rgsw_wide(const uint64_t* raw, size_t words, uint64_t Q, uint64_t qinv, uint64_t R2, uint64_t* out,
+                                 hipStream_t s) {
+    if (words == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<size_t>((words + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_pack_rgsw_wide, dim3(blocks), dim3(256), 0, s, raw, words, Q, qinv, R2, out);
     return hipGetLastError();
 }
 

@@ -48,17 +48,17 @@ int guarded(F&& f) {
     }
 }
 // device scratch for a synchronous host-buffer call (freed on every exit path)
+// (hipFreeAsync on the call's stream: an error path frees it after the work already enqueued there,
+// without waiting for other contexts' work on the device)
 struct DeviceScratch {
     uint64_t* p = nullptr;
-    DeviceScratch(int device, size_t bytes) {
+    hipStream_t s = nullptr;
+    DeviceScratch(int device, size_t bytes, hipStream_t stream) : s(stream) {
         FHE_HIP_CHECK(hipSetDevice(device));
-        FHE_HIP_CHECK(hipMalloc(&p, bytes));
+        FHE_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&p), bytes, s));
     }
     ~DeviceScratch() {
-        if (p) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(p);
-        }
+        if (p) (void)hipFreeAsync(p, s);
     }
     DeviceScratch(const DeviceScratch&) = delete;
     DeviceScratch& operator=(const DeviceScratch&) = delete;
@@ -83,6 +83,23 @@ static void fill_params(const Params& p, fhe_hip_params* o) {
 static hipStream_t ctx_stream(fhe_hip_ctx* ctx, void* stream) {
     return ctx->eng.use_stream(static_cast<hipStream_t>(stream));
 }
+
+// An asynchronous call's stream and its ordering point: the event a later call on another stream
+// waits for is recorded when the call's scope ends, on every exit path (work may have been enqueued
+// before an exception)
+struct CallOrder {
+    Engine& eng;
+    hipStream_t s;
+    CallOrder(fhe_hip_ctx* ctx, void* stream) : eng(ctx->eng), s(ctx_stream(ctx, stream)) {}
+    ~CallOrder() {
+        try {
+            eng.end_call(s);
+        } catch (...) {
+        }
+    }
+    CallOrder(const CallOrder&) = delete;
+    CallOrder& operator=(const CallOrder&) = delete;
+};
 
 struct fhe_hip_multi {
     MultiEngine eng;
@@ -428,10 +445,10 @@ int fhe_hip_eval_bingate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, 
     if (!ctx || !io_ok(count, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out))
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.eval_gate_device(gate, count, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
                                   s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -440,10 +457,10 @@ int fhe_hip_blind_rotate_batch_device(fhe_hip_ctx* ctx, int gate, size_t count, 
                                       const uint64_t* d_b1, const uint64_t* d_a2, const uint64_t* d_b2, void* stream) {
     if (!ctx || !io_ok(count, d_a1, d_b1, d_a2, d_b2, d_a1, d_b1)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.bootstrap_device(gate, count, d_a1, d_b1, d_a2, d_b2, true,
                                   s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -452,10 +469,10 @@ int fhe_hip_keyswitch_workspace_device(fhe_hip_ctx* ctx, size_t count, uint64_t*
                                        void* stream) {
     if (!ctx || (count && (!d_a_out || !d_b_out))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.keyswitch_workspace_device(count, d_a_out, d_b_out,
                                             s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -489,10 +506,10 @@ int fhe_hip_eval_gate_multi_batch_device(fhe_hip_ctx* ctx, int gate, uint32_t k,
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (k < 2 || k > 4) return fail(FHE_HIP_ERR_INVALID_PARAM, "k must be 2..4");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.eval_gate_multi_device(gate, count, k, d_a_in, d_b_in, ptmod, d_a_out, d_b_out,
                                         s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -515,10 +532,10 @@ int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
     if (!ctx || !io_ok(count, d_a0, d_b0, d_a1, d_b1, d_a_out, d_b_out) || (count && (!d_a2 || !d_b2)))
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.eval_cmux_device(count, d_a0, d_b0, d_a1, d_b1, d_a2, d_b2, d_a_out, d_b_out,
                                   s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -536,7 +553,7 @@ int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_
         for (size_t i = 0; i < accw; ++i)
             if (acc[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "accumulator not reduced mod Q");
         hipStream_t s = ctx_stream(ctx, nullptr);
-        DeviceScratch d(ctx->eng.device(), (aw + accw) * 8);
+        DeviceScratch d(ctx->eng.device(), (aw + accw) * 8, s);
         FHE_HIP_CHECK(hipMemcpyAsync(d.p, a, aw * 8, hipMemcpyHostToDevice, s));
         FHE_HIP_CHECK(hipMemcpyAsync(d.p + aw, acc, accw * 8, hipMemcpyHostToDevice, s));
         ctx->eng.blind_rotate_acc_device(count, d.p, (uint32_t)ctmod, d.p + aw, s);
@@ -551,9 +568,41 @@ int fhe_hip_blind_rotate_acc_batch_device(fhe_hip_ctx* ctx, size_t count, const 
     if (!ctx || (count && (!d_a || !d_acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (ctmod == 0 || ctmod > 0xffffffffull) return fail(FHE_HIP_ERR_INVALID_PARAM, "bad ciphertext modulus");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.blind_rotate_acc_device(count, d_a, (uint32_t)ctmod, d_acc, s);
-        ctx->eng.end_call(s);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_blind_rotate_init_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b,
+                                    uint64_t* acc) {
+    if (!ctx || (count && (!a || !b || !acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        if (count == 0) return FHE_HIP_OK;
+        const Params& p = ctx->eng.params();
+        const size_t aw = count * p.n, accw = count * 2 * (size_t)p.N;
+        for (size_t i = 0; i < aw; ++i)
+            if (a[i] >= p.q) return fail(FHE_HIP_ERR_INVALID_PARAM, "a not reduced mod q");
+        for (size_t i = 0; i < count; ++i)
+            if (b[i] >= p.q) return fail(FHE_HIP_ERR_INVALID_PARAM, "b not reduced mod q");
+        hipStream_t s = ctx_stream(ctx, nullptr);
+        DeviceScratch d(ctx->eng.device(), (aw + count + accw) * 8, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(d.p, a, aw * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(d.p + aw, b, count * 8, hipMemcpyHostToDevice, s));
+        ctx->eng.blind_rotate_init_device(count, d.p, d.p + aw, d.p + aw + count, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(acc, d.p + aw + count, accw * 8, hipMemcpyDeviceToHost, s));
+        FHE_HIP_CHECK(hipStreamSynchronize(s));
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_blind_rotate_init_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                           uint64_t* d_acc, void* stream) {
+    if (!ctx || (count && (!d_a || !d_b || !d_acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const CallOrder order(ctx, stream);
+        ctx->eng.blind_rotate_init_device(count, d_a, d_b, d_acc, order.s);
         return FHE_HIP_OK;
     });
 }
@@ -570,7 +619,7 @@ int fhe_hip_external_product_batch(fhe_hip_ctx* ctx, size_t count, const uint64_
         for (size_t i = 0; i < rw; ++i)
             if (rlwe[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "RLWE ciphertext not reduced mod Q");
         hipStream_t s = ctx_stream(ctx, nullptr);
-        DeviceScratch d(ctx->eng.device(), (kw + rw) * 8);
+        DeviceScratch d(ctx->eng.device(), (kw + rw) * 8, s);
         FHE_HIP_CHECK(hipMemcpyAsync(d.p, rgsw, kw * 8, hipMemcpyHostToDevice, s));
         FHE_HIP_CHECK(hipMemcpyAsync(d.p + kw, rlwe, rw * 8, hipMemcpyHostToDevice, s));
         ctx->eng.external_product_device(count, d.p, d.p + kw, d.p + kw, s);
@@ -584,9 +633,9 @@ int fhe_hip_external_product_batch_device(fhe_hip_ctx* ctx, size_t count, const 
                                           const uint64_t* d_rlwe, uint64_t* d_result, void* stream) {
     if (!ctx || (count && (!d_rgsw || !d_rlwe || !d_result))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.external_product_device(count, d_rgsw, d_rlwe, d_result, s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }
@@ -649,10 +698,10 @@ int fhe_hip_eval_func_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
     return guarded([&]() -> int {
-        hipStream_t s = ctx_stream(ctx, stream);
+        const CallOrder order(ctx, stream);
+        const hipStream_t s = order.s;
         ctx->eng.eval_func_device(count, d_a, d_b, q_in, lut, d_a_out, d_b_out,
                                   s);
-        ctx->eng.end_call(s);
         return FHE_HIP_OK;
     });
 }

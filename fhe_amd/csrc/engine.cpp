@@ -146,9 +146,13 @@ Engine::~Engine() {
 
 hipStream_t Engine::use_stream(hipStream_t s) {
     if (!s) s = stream_;
-    if (pending_ && s != last_stream_) {  // order after the previous call's work on its stream
+    if (last_stream_ && s != last_stream_) {  // order after the previous call's work on its stream
         FHE_HIP_CHECK(hipSetDevice(device_));
-        FHE_HIP_CHECK(hipStreamWaitEvent(s, order_ev_, 0));
+        // the context's own stream is alive for the context's lifetime: its ordering point is taken
+        // now (it covers a synchronous call that threw after enqueueing work); a caller's stream was
+        // marked by that call's end_call (capi CallOrder, on every exit path)
+        if (last_stream_ == stream_) end_call(stream_);
+        if (pending_) FHE_HIP_CHECK(hipStreamWaitEvent(s, order_ev_, 0));
     }
     last_stream_ = s;
     return s;
@@ -600,6 +604,8 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.b_const = g.b64;
         w.qKS = p_.qKS;
         w.tv = g.tv64;
+        w.acc_io = g.acc_io;
+        w.acc_tv = g.acc_tv;
         if (g3_ && p_.method == M_LMKCDEY && d_bsk2_ && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64 &&
             !g.tv && !g.tv64 && !g.acc_io) {
             const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);
@@ -655,7 +661,6 @@ void Engine::bootstrap_device(int gate, size_t count, const uint64_t* a1, const 
 
 void Engine::blind_rotate_acc_device(size_t count, const uint64_t* a, uint32_t ctmod, uint64_t* acc, hipStream_t s) {
     if (!d_bsk_) throw std::logic_error("bootstrapping key not loaded");
-    if (wide_) throw std::invalid_argument("BlindRotate seam: 32-bit parameter sets only");
     if (ctmod < 2 || (ctmod & (ctmod - 1)) || ctmod > 2 * p_.N)
         throw std::invalid_argument("BlindRotate: ciphertext modulus must be a power of two <= 2N");
     if (p_.method == M_AP && ctmod != p_.q)  // EvalAcc DM reads a_i modulo q (rgsw-acc-dm.cpp:64-69)
@@ -684,34 +689,69 @@ void Engine::blind_rotate_acc_device(size_t count, const uint64_t* a, uint32_t c
     rot_count_ = 0;  // no ctExt left in the workspace
 }
 
+void Engine::blind_rotate_init_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* acc, hipStream_t s) {
+    if (!d_bsk_) throw std::logic_error("bootstrapping key not loaded");
+    if (count == 0) return;
+    if (!a || !b || !acc) throw std::invalid_argument("null argument");
+    GateArgs g = gate_args(G_AND, count);  // BootstrapGateCore's AND window (Bootstrap, :205)
+    ensure_work(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    g.acc_io = acc;
+    g.acc_tv = 1;
+    // ct + q/4 (EvalAddConstEq, binfhe-base-scheme.cpp:201): the b offset of the prep
+    GateInputs in{{a, nullptr, nullptr, nullptr}, {b, nullptr, nullptr, nullptr}, 1, 0, p_.q >> 2};
+    prep_device(g, in, 0, s);
+    rotate_device(g, s);
+    rot_count_ = 0;
+}
+
 void Engine::external_product_device(size_t count, const uint64_t* rgsw, const uint64_t* rlwe, uint64_t* result,
                                      hipStream_t s) {
-    if (wide_) throw std::invalid_argument("ExternalProduct seam: 32-bit parameter sets only");
-    if (p_.digitsG2 != 4) throw std::invalid_argument("device path expects digitsG = 3");
+    if (!wide_ && p_.digitsG2 != 4) throw std::invalid_argument("device path expects digitsG = 3");
     if (count == 0) return;
     if (!rgsw || !rlwe || !result) throw std::invalid_argument("null argument");
     FHE_HIP_CHECK(hipSetDevice(device_));
     constexpr size_t kChunk = 0x8000;   // op codes hold key indices < 0x8000
     const size_t keyw = (size_t)p_.digitsG2 * 2 * p_.N;
+    const size_t wpk = wide_ ? 2 : 1;   // u32 words per packed key word (u64 Montgomery on the 64-bit path)
     const size_t cap = std::min(count, kChunk);
     if (cap > epcap_) {
         sync_streams();
         for (void* ptr : {(void*)d_epk_, (void*)d_epops_, (void*)d_epn_})
             if (ptr) FHE_HIP_CHECK(hipFree(ptr));
         d_epk_ = nullptr; d_epops_ = nullptr; d_epn_ = nullptr; epcap_ = 0;
-        FHE_HIP_CHECK(hipMalloc(&d_epk_, cap * keyw * sizeof(uint32_t)));
+        FHE_HIP_CHECK(hipMalloc(&d_epk_, cap * keyw * wpk * sizeof(uint32_t)));
         FHE_HIP_CHECK(hipMalloc(&d_epops_, cap * sizeof(uint16_t)));
         FHE_HIP_CHECK(hipMalloc(&d_epn_, cap * sizeof(uint32_t)));
         epcap_ = cap;
     }
-    const uint32_t ninv_mont = to_mont(invmod(p_.N, p_.Q), p_.Q);
+    const uint32_t ninv_mont = wide_ ? 0u : to_mont(invmod(p_.N, p_.Q), p_.Q);
+    const uint64_t R = (uint64_t)(((u128)1 << 64) % p_.Q), R2 = mulmod(R, R, p_.Q);
     for (size_t off = 0; off < count; off += kChunk) {
         const size_t c = std::min(kChunk, count - off);
         if (result + off * 2 * p_.N != rlwe + off * 2 * p_.N)
             FHE_HIP_CHECK(hipMemcpyAsync(result + off * 2 * p_.N, rlwe + off * 2 * p_.N, c * 2 * p_.N * 8,
                                          hipMemcpyDeviceToDevice, s));
-        FHE_HIP_CHECK(launch_pack_rgsw(rgsw + off * keyw, c, p_.N, (uint32_t)p_.Q, ninv_mont, d_epk_, s));
         FHE_HIP_CHECK(launch_single_ops(d_epops_, d_epn_, (uint32_t)c, 1, s));
+        if (wide_) {
+            // the 64-bit DM op loop (k_blind_rotate_wide_ops): one EXT op per item with its own key
+            uint64_t* k64 = reinterpret_cast<uint64_t*>(d_epk_);
+            FHE_HIP_CHECK(launch_pack_rgsw_wide(rgsw + off * keyw, c * keyw, p_.Q, wtabs_.qinv, R2, k64, s));
+            WideArgs w{};
+            w.count = (uint32_t)c;
+            w.n = p_.n;
+            w.N = p_.N;
+            w.ctmod = p_.q;
+            w.factor = 1;
+            w.digitsG = p_.digitsG;
+            w.gbits = p_.gBits;
+            w.qKS = p_.qKS;
+            w.acc_io = result + off * 2 * p_.N;
+            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, k64, k64, d_epops_, d_epn_, 1, nullptr, nullptr,
+                                                       nullptr, true, s));
+            continue;
+        }
+        FHE_HIP_CHECK(launch_pack_rgsw(rgsw + off * keyw, c, p_.N, (uint32_t)p_.Q, ninv_mont, d_epk_, s));
         GateArgs g{};
         g.count = (uint32_t)c;
         g.n = p_.n;

@@ -80,6 +80,11 @@ public:
     // rgsw-acc-dm.cpp:62-77): acc [count][2][N] (EVALUATION, canonical mod Q) in/out, a [count][n]
     // mod ctmod (a power of two <= 2N; EvalAcc reads a_i with the ciphertext's modulus)
     void blind_rotate_acc_device(size_t count, const uint64_t* a, uint32_t ctmod, uint64_t* acc, hipStream_t s);
+    // the seam's null accumulators (BootstrapBatch, batch.cpp:77-86): BinFHEScheme::Bootstrap's
+    // accumulator, BootstrapGateCore(AND, ct + q/4) (binfhe-base-scheme.cpp:190-205, 525-583) on
+    // ciphertexts (a [count][n], b [count]) mod q -- the test vector of the AND window at b + q/4,
+    // EvalAcc over a -- written to acc [count][2][N] (EVALUATION, canonical mod Q)
+    void blind_rotate_init_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* acc, hipStream_t s);
     // ExternalProduct[Batch] = AddToAccLMKCDEY / AddToAccDM (rgsw-acc-lmkcdey.cpp:228-254,
     // rgsw-acc-dm.cpp:119-145): result[g] = rgsw[g] (x) rlwe[g]; rgsw [count][digitsG2][2][N] and
     // rlwe / result [count][2][N], EVALUATION, canonical mod Q; result may alias rlwe

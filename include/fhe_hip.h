@@ -226,10 +226,19 @@ int fhe_hip_bootstrap_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t*
  * (rgsw-acc-cggi.cpp:59-68, rgsw-acc-lmkcdey.cpp:70-158, rgsw-acc-dm.cpp:62-77) on `count` pairs:
  * a[count][n] mod ctmod (the LWE ciphertext's modulus: a power of two <= 2N; 2N for LMKCDEY, q for
  * AP), acc[count][2][N] in/out (RLWECiphertext elements 0 and 1, EVALUATION, bit-reversed as the
- * reference stores them, canonical mod Q).  32-bit parameter sets (STD128, STD128_LMKCDEY, ...). */
+ * reference stores them, canonical mod Q).  Every parameter set and method of the context. */
 int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, uint64_t ctmod, uint64_t* acc);
 int fhe_hip_blind_rotate_acc_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, uint64_t ctmod,
                                           uint64_t* d_acc, void* stream);
+/* BlindRotateBatch with null accumulators -- what BootstrapBatch (batch/batch.cpp:53-104) passes
+ * ("initialize accumulators with LUT (identity for bootstrap)", :77-86): the accumulator of
+ * BinFHEScheme::Bootstrap (binfhe-base-scheme.cpp:190-205), i.e. BootstrapGateCore(AND, ct + q/4)
+ * (:525-583): the AND window's test vector at b + q/4, NTT'd, then EvalAcc over a.  Ciphertexts
+ * a[count][n], b[count] mod q; acc[count][2][N] out (EVALUATION, canonical mod Q). */
+int fhe_hip_blind_rotate_init_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b,
+                                    uint64_t* acc);
+int fhe_hip_blind_rotate_init_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                           uint64_t* d_acc, void* stream);
 /* Backend::ExternalProduct / ExternalProductBatch (backend.h:141-146, 187-192): RGSW x RLWE -> RLWE,
  * result[g] = sum_d D_d(rlwe[g]) * rgsw[g][d] with D = SignedDigitDecompose (rgsw-acc.cpp:54-91) --
  * AddToAccLMKCDEY / AddToAccDM (rgsw-acc-lmkcdey.cpp:228-254, rgsw-acc-dm.cpp:119-145) under the

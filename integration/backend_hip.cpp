@@ -77,8 +77,9 @@ void BackendHIP::Release() {
     std::lock_guard<std::mutex> lock(mu_);
     if (ctx_)
         fhe_hip_destroy(ctx_);
-    ctx_    = nullptr;
-    bsk_id_ = ksk_id_ = nullptr;
+    ctx_ = nullptr;
+    bsk_id_.reset();
+    ksk_id_.reset();
 }
 
 void BackendHIP::Check(int rc, const char* what) const {
@@ -192,16 +193,26 @@ std::vector<uint64_t> BackendHIP::RawBSK(const RingGSWACCKey& ek) const {
     return raw;
 }
 
+namespace {
+// the same live object as the one the weak reference was taken from (owner and address)
+template <typename T>
+bool same_key(const std::weak_ptr<const void>& w, const std::shared_ptr<T>& k) {
+    const auto held = w.lock();
+    return held && k && held.get() == static_cast<const void*>(k.get()) && !held.owner_before(k) &&
+           !k.owner_before(held);
+}
+}  // namespace
+
 void BackendHIP::EnsureBSK(const RingGSWACCKey& ek) {
-    if (ek.get() == bsk_id_)
+    if (same_key(bsk_id_, ek))
         return;
     const auto raw = RawBSK(ek);
     Check(fhe_hip_load_bsk(ctx_, raw.data(), raw.size()), "load bootstrapping key");
-    bsk_id_ = ek.get();
+    bsk_id_ = std::shared_ptr<const void>(ek);
 }
 
 void BackendHIP::EnsureKSK(const LWESwitchingKey& ks) {
-    if (ks.get() == ksk_id_)
+    if (same_key(ksk_id_, ks))
         return;
     if (!ks)
         throw std::invalid_argument("BackendHIP: null switching key");
@@ -221,7 +232,7 @@ void BackendHIP::EnsureKSK(const LWESwitchingKey& ks) {
                 rB[row] = B[i][j][k].ConvertToInt();
             }
     Check(fhe_hip_load_ksk(ctx_, rA.data(), rA.size(), rB.data(), rB.size()), "load switching key");
-    ksk_id_ = ks.get();
+    ksk_id_ = std::shared_ptr<const void>(ks);
 }
 
 // ---- single ops: batches of one --------------------------------------------------------------------
@@ -267,19 +278,33 @@ void BackendHIP::BlindRotateBatch(const std::shared_ptr<RingGSWCryptoParams>& pa
     EnsureBSK(ek);
     const uint32_t n = p_.n, N = p_.N;
     const uint64_t ctmod = cts[0]->GetModulus().ConvertToInt();
-    std::vector<uint64_t> a(B * n), acc(B * 2 * N);
+    // null accumulators (BootstrapBatch, batch.cpp:77-86): all of them or none
+    const bool init = !accs[0];
+    std::vector<uint64_t> a(B * n), b(init ? B : 0), acc(B * 2 * N);
     for (size_t g = 0; g < B; ++g) {
         const auto& v = cts[g]->GetA();
         if (v.GetLength() != n || cts[g]->GetModulus().ConvertToInt() != ctmod)
             throw std::invalid_argument("BackendHIP::BlindRotateBatch: ciphertexts of one dimension and modulus");
         for (uint32_t i = 0; i < n; ++i)
             a[g * n + i] = v[i].ConvertToInt();
+        if (init) {
+            if (accs[g])
+                throw std::invalid_argument("BackendHIP::BlindRotateBatch: accumulators all given or all null");
+            b[g] = cts[g]->GetB().ConvertToInt();
+            continue;
+        }
         if (!accs[g] || accs[g]->GetElements().size() != 2)
             throw std::invalid_argument("BackendHIP::BlindRotateBatch: accumulators must hold two polynomials");
         for (uint32_t c = 0; c < 2; ++c)
             poly_to(accs[g]->GetElements()[c], acc.data() + (g * 2 + c) * N, N);
     }
-    Check(fhe_hip_blind_rotate_acc_batch(ctx_, B, a.data(), ctmod, acc.data()), "BlindRotateBatch");
+    if (init) {
+        if (ctmod != p_.q)
+            throw std::invalid_argument("BackendHIP::BlindRotateBatch: bootstrapped ciphertexts must be mod q");
+        Check(fhe_hip_blind_rotate_init_batch(ctx_, B, a.data(), b.data(), acc.data()), "BlindRotateBatch");
+    } else {
+        Check(fhe_hip_blind_rotate_acc_batch(ctx_, B, a.data(), ctmod, acc.data()), "BlindRotateBatch");
+    }
     const auto pp = params->GetPolyParams();
     const NativeInteger Q(p_.Q);
     for (size_t g = 0; g < B; ++g) {
@@ -388,7 +413,7 @@ DeviceBuffer BackendHIP::PackBootstrappingKey(const RingGSWACCKey& ek) {
           "PackBootstrappingKey");
     // resident for the blind rotations, and the packed bytes in device memory for the caller
     Check(fhe_hip_load_bsk(ctx_, raw.data(), raw.size()), "load bootstrapping key");
-    bsk_id_ = ek.get();
+    bsk_id_ = std::shared_ptr<const void>(ek);
     DeviceBuffer buf;
     Check(fhe_hip_alloc(device_, bsize, &buf.ptr), "Allocate");
     buf.size   = bsize;
@@ -511,6 +536,28 @@ void BackendHIP::EvalBinGateBatch(BINGATE gate, const RingGSWBTKey& keys, const 
     const NativeInteger q(p_.q);
     for (size_t g = 0; g < B; ++g)
         out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
+}
+
+BatchResult EvalBinGateBatchHIP(BinFHEContext& cc, BINGATE gate, const std::vector<LWECiphertext>& ct1,
+                                const std::vector<LWECiphertext>& ct2, std::vector<LWECiphertext>& ct_out,
+                                uint32_t flags) {
+    auto* hip = dynamic_cast<BackendHIP*>(BackendRegistry::Instance().GetDefault());
+    if (!hip)
+        return lux::fhe::EvalBinGateBatch(cc, gate, ct1, ct2, ct_out, flags);
+    if (ct1.size() != ct2.size())
+        return BatchResult{false, 0, ct1.size(), "Input size mismatch"};
+    if (ct1.empty())
+        return BatchResult{true, 0, 0, ""};
+    try {
+        RingGSWBTKey keys;
+        keys.BSkey = cc.GetRefreshKey();
+        keys.KSkey = cc.GetSwitchKey();
+        hip->EvalBinGateBatch(gate, keys, ct1, ct2, ct_out);
+        return BatchResult{true, ct1.size(), 0, ""};
+    }
+    catch (const std::exception& e) {
+        return BatchResult{false, 0, ct1.size(), e.what()};
+    }
 }
 
 }  // namespace lux::fhe::backend

@@ -14,6 +14,8 @@
 #include <vector>
 
 #include "backend/backend.h"
+#include "batch/binfhe-batch.h"
+#include "binfhecontext.h"
 #include "lwe-keyswitchkey.h"
 #include "rlwe-ciphertext.h"
 #include "fhe_hip.h"
@@ -57,7 +59,10 @@ public:
                    LWECiphertext& result) override;
 
     // batch ops (backend.h:177-211): one device call per batch
-    //   BlindRotateBatch    = EvalAcc of the method (accs in/out, EVALUATION)
+    //   BlindRotateBatch    = EvalAcc of the method (accs in/out, EVALUATION); null accumulators
+    //                         (what BootstrapBatch passes, batch.cpp:77-86) are initialised as
+    //                         BinFHEScheme::Bootstrap's: BootstrapGateCore(AND, ct + q/4)
+    //                         (binfhe-base-scheme.cpp:190-205, 525-583)
     //   ExternalProductBatch= AddToAccLMKCDEY / AddToAccDM (rgsw (x) rlwe)
     //   KeySwitchBatch      = LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372)
     //   ModSwitchBatch      = LWEEncryptionScheme::ModSwitch to the next modulus of SwitchCTtoqn:
@@ -103,10 +108,22 @@ private:
     int device_ = 0;
     BINFHE_PARAMSET set_;
     BINFHE_METHOD method_;
-    const void* bsk_id_ = nullptr;
-    const void* ksk_id_ = nullptr;
+    // the key objects resident on the device, held weakly: a key that was freed (and an unrelated
+    // one allocated at its address) or replaced forces a reload; in-place edits of a live key object
+    // are not detected (call PackBootstrappingKey to reload explicitly)
+    std::weak_ptr<const void> bsk_id_;
+    std::weak_ptr<const void> ksk_id_;
     std::mutex mu_;  // one context, one workspace: calls are serialized
 };
+
+// The routing INTEGRATION.md proposes for lux::fhe::EvalBinGateBatch (batch/batch.cpp:176-210): with a
+// BackendHIP as the registry's default the whole batch goes through its fused gate path (two device
+// launches) under the context's keys (cc.GetRefreshKey / GetSwitchKey); with any other default it is
+// the reference's own OpenMP loop over cc.EvalBinGate.  Same BatchResult semantics as the reference
+// (size mismatch, empty batch, exceptions caught into the result).
+BatchResult EvalBinGateBatchHIP(BinFHEContext& cc, BINGATE gate, const std::vector<LWECiphertext>& ct1,
+                                const std::vector<LWECiphertext>& ct2, std::vector<LWECiphertext>& ct_out,
+                                uint32_t flags = 0);
 
 }  // namespace lux::fhe::backend
 

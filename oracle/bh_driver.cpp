@@ -11,7 +11,11 @@
 //                        public SignedDigitDecompose (rgsw-acc.cpp:54-91) and NativePoly products
 //   KeySwitchBatch       LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372)
 //   ModSwitchBatch       LWEEncryptionScheme::ModSwitch (lwe-pke.cpp:254-261)
-//   EvalBinGateBatch     lux::fhe::EvalBinGateBatch (batch/batch.cpp:176-210)
+//   EvalBinGateBatch     lux::fhe::EvalBinGateBatch (batch/batch.cpp:176-210), directly and routed
+//                        through the registry (EvalBinGateBatchHIP)
+//   null accumulators    BootstrapGateCore(AND, ct + q/4) (binfhe-base-scheme.cpp:190-205, 525-583),
+//                        and lux::fhe::BootstrapBatch / KeySwitchBatch / ModSwitchBatch (batch.cpp:53-104,
+//                        251-314) with BackendHIP as the registry's default
 #include <omp.h>
 
 #include <cstdint>
@@ -308,6 +312,143 @@ int bh_eval_gates(void* h, int gate, size_t count, const uint64_t* a1, const uin
         BatchResult r = EvalBinGateBatch(cc, static_cast<BINGATE>(gate), c1, c2, ref, 0);
         if (!r.success)
             throw std::runtime_error("reference EvalBinGateBatch: " + r.error);
+        lwe_out(ref, ra, rb);
+    });
+}
+
+// BlindRotateBatch with null accumulators -- the call BootstrapBatch makes (batch.cpp:77-86) --
+// through CurrentBackend() vs the reference's BootstrapGateCore(AND, ct + q/4) (binfhe-base-scheme.cpp:
+// 190-205, 525-583; private there, so its test-vector set-up :535-575 is restated here and EvalAcc is
+// the reference's own).  The restatement is pinned by the reference's public Bootstrap: *flags bit 0 =
+// the extraction of Bootstrap (:206-213) applied to the reference accumulator equals
+// cc.Bootstrap(ct, true) for every ciphertext; bit 1 = lux::fhe::BootstrapBatch (batch.cpp:53-104) on
+// the same ciphertexts with BackendHIP as the default returned success with every ciphertext processed
+int bh_bootstrap_init(void* h, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* acc_gpu,
+                      uint64_t* acc_ref, int* flags) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto rg           = cc.GetParams()->GetRingGSWParams();
+        auto lp           = cc.GetParams()->GetLWEParams();
+        const uint32_t n = lp->Getn(), N = rg->GetN();
+        const NativeInteger Q = rg->GetQ(), q = lp->Getq();
+        const auto pp         = rg->GetPolyParams();
+        const auto& ek        = cc.GetRefreshKey();
+        auto cts              = lwe_vec(a, b, count, n, q.ConvertToInt());
+        std::vector<RLWECiphertext> accs(count);  // null, as BootstrapBatch passes them
+        CurrentBackend()->BlindRotateBatch(rg, cts, ek, accs);
+        for (size_t g = 0; g < count; ++g)
+            rlwe_out(accs[g], acc_gpu + g * 2 * N, N);
+        bool ext_ok = true;
+        std::string err;
+#pragma omp parallel for schedule(dynamic)
+        for (size_t g = 0; g < count; ++g) {
+            try {
+                // ct + q/4 (EvalAddConstEq, :201), then BootstrapGateCore's window and test vector
+                const uint32_t qHalf = q.ConvertToInt<uint32_t>() >> 1;
+                NativeInteger bb    = NativeInteger(b[g]).ModAddFast(q >> 2, q);
+                const NativeInteger q1 = rg->GetGateConst()[static_cast<size_t>(AND)];
+                const NativeInteger q2 = q1.ModAddFast(NativeInteger(qHalf), q);
+                const bool swap        = q1 >= q2;
+                const NativeInteger lb = swap ? q2 : q1, ub = swap ? q1 : q2;
+                const NativeInteger Q2p = Q / (cts[g]->GetptModulus() * 2) + 1, Q2pNeg = Q - Q2p;
+                const NativeInteger lv = swap ? Q2p : Q2pNeg, uv = swap ? Q2pNeg : Q2p;
+                NativeVector m(N, Q);
+                for (uint32_t i = 0; i < N; i += N / qHalf) {
+                    m[i] = (bb >= lb && bb < ub) ? lv : uv;
+                    bb.ModSubFastEq(1, q);
+                }
+                std::vector<NativePoly> res(2);
+                res[0] = NativePoly(pp, Format::EVALUATION, true);
+                res[1] = NativePoly(pp, Format::COEFFICIENT, false);
+                res[1].SetValues(std::move(m), Format::COEFFICIENT);
+                res[1].SetFormat(Format::EVALUATION);
+                auto acc = std::make_shared<RLWECiphertextImpl>(std::move(res));
+                const NativeVector& av = cts[g]->GetA();
+                switch (rg->GetMethod()) {
+                    case GINX: RingGSWAccumulatorCGGI().EvalAcc(rg, ek, acc, av); break;
+                    case LMKCDEY: RingGSWAccumulatorLMKCDEY().EvalAcc(rg, ek, acc, av); break;
+                    default: RingGSWAccumulatorDM().EvalAcc(rg, ek, acc, av); break;
+                }
+                rlwe_out(acc, acc_ref + g * 2 * N, N);
+                // Bootstrap's extraction (:206-213) vs the reference's own Bootstrap(ct, extended)
+                auto el = acc->GetElements();
+                el[0]   = el[0].Transpose();
+                el[0].SetFormat(Format::COEFFICIENT);
+                el[1].SetFormat(Format::COEFFICIENT);
+                NativeInteger eb = Q / (cts[g]->GetptModulus() * 2) + 1;
+                eb.ModAddFastEq(el[1][0], Q);
+                const auto want = cc.Bootstrap(cts[g], true);
+                const bool same = want->GetB() == eb && want->GetA() == el[0].GetValues();
+                if (!same) {
+#pragma omp critical
+                    ext_ok = false;
+                }
+            }
+            catch (const std::exception& e) {
+#pragma omp critical
+                err = e.what();
+            }
+        }
+        if (!err.empty())
+            throw std::runtime_error(err);
+        std::vector<LWECiphertext> out;
+        const BatchResult r = BootstrapBatch(cc, cts, out, 0);
+        *flags = (ext_ok ? 1 : 0) | (r.success && r.processed == count && out.size() == count ? 2 : 0);
+        if (!r.success)
+            g_err = "BootstrapBatch: " + r.error;
+    });
+}
+
+// the reference's own batch callers of the seam (batch.cpp:251-314) with BackendHIP as the default:
+// KeySwitchBatch on (N, qKS) ciphertexts and ModSwitchBatch on (N, Q) ciphertexts, vs
+// LWEEncryptionScheme::KeySwitch / ModSwitch(qKS, .) on the CPU; *ok = both BatchResults successful
+int bh_batch_callers(void* h, size_t count, const uint64_t* ka, const uint64_t* kb, uint64_t* gka, uint64_t* gkb,
+                     uint64_t* rka, uint64_t* rkb, const uint64_t* ma, const uint64_t* mb, uint64_t* gma, uint64_t* gmb,
+                     uint64_t* rma, uint64_t* rmb, int* ok) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        const uint32_t N  = lp->GetN();
+        auto kcts = lwe_vec(ka, kb, count, N, lp->GetqKS().ConvertToInt());
+        auto mcts = lwe_vec(ma, mb, count, N, lp->GetQ().ConvertToInt());
+        std::vector<LWECiphertext> ko, mo;
+        const BatchResult r1 = KeySwitchBatch(cc, kcts, ko, 0);
+        const BatchResult r2 = ModSwitchBatch(cc, mcts, mo, 0);
+        *ok = r1.success && r2.success && r1.processed == count && r2.processed == count;
+        if (!*ok)
+            throw std::runtime_error("batch callers: " + r1.error + " / " + r2.error);
+        lwe_out(ko, gka, gkb);
+        lwe_out(mo, gma, gmb);
+        const LWEEncryptionScheme lwe;
+        std::vector<LWECiphertext> kr(count), mr(count);
+#pragma omp parallel for
+        for (size_t g = 0; g < count; ++g) {
+            kr[g] = lwe.KeySwitch(lp, cc.GetSwitchKey(), kcts[g]);
+            mr[g] = lwe.ModSwitch(lp->GetqKS(), mcts[g]);
+        }
+        lwe_out(kr, rka, rkb);
+        lwe_out(mr, rma, rmb);
+    });
+}
+
+// EvalBinGateBatch routed through the registry (EvalBinGateBatchHIP, integration/backend_hip.h) vs
+// the reference's EvalBinGateBatch; *ok = the routed BatchResult reports success for every gate
+int bh_eval_gates_routed(void* h, int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
+                         const uint64_t* b2, uint64_t* ga, uint64_t* gb, uint64_t* ra, uint64_t* rb, int* ok) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        const uint64_t q  = lp->Getq().ConvertToInt();
+        auto c1 = lwe_vec(a1, b1, count, lp->Getn(), q), c2 = lwe_vec(a2, b2, count, lp->Getn(), q);
+        std::vector<LWECiphertext> out, ref;
+        const BatchResult r = EvalBinGateBatchHIP(cc, static_cast<BINGATE>(gate), c1, c2, out, 0);
+        *ok = r.success && r.processed == count;
+        if (!r.success)
+            throw std::runtime_error("EvalBinGateBatchHIP: " + r.error);
+        lwe_out(out, ga, gb);
+        const BatchResult rr = EvalBinGateBatch(cc, static_cast<BINGATE>(gate), c1, c2, ref, 0);
+        if (!rr.success)
+            throw std::runtime_error("reference EvalBinGateBatch: " + rr.error);
         lwe_out(ref, ra, rb);
     });
 }

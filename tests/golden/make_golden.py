@@ -333,7 +333,30 @@ def make_full(names=("std128", "lmkcdey"), nthreads=8):
         print(name, "full ok", FULL_GATES, f"{dt:.0f} s on {nthreads} threads", flush=True)
 
 
+# BASELINE config 3 (1024 STD128 GINX AND gates on one GPU): the first 1024 gates of full_inputs drawn
+# at count = 1024 (bench.py's config-3 object uses the same seeds), one shard
+C3_GATES = 1024
+
+
+def make_config3(nthreads=8):
+    ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2 = full_inputs("std128", C3_GATES)
+    ref = Ref(ps, m)
+    ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    ao, bo = ref.eval_gate(GATES["AND"], a1, b1, a2, b2, nthreads=nthreads)
+    dec = np.array([ref.decrypt(keys.sk, ao[i], bo[i], ref.q) for i in range(C3_GATES)])
+    assert np.array_equal(dec, bits1 & bits2), "reference AND outputs do not decrypt"
+    np.savez_compressed(os.path.join(HERE, "full_std128_b1024.npz"), paramset=ps, method=m,
+                        key_seed=np.uint64(key_seed), count=C3_GATES, shard=C3_GATES, gate=GATES["AND"],
+                        out_sha=np.array(sha(ao) + sha(bo)), shard_sha=np.array([sha(ao) + sha(bo)]),
+                        out_a_head=ao[:16].astype(np.uint16), out_b_head=bo[:16].astype(np.uint16),
+                        keys_sha=np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB)),
+                        in_sha=np.array(sha(a1) + sha(b1) + sha(a2) + sha(b2)), ref_threads=nthreads)
+    print("config3 ok", C3_GATES, flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "config3":
+        make_config3()
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what == "full":   # ~15 min per set on 8 cores
         make_full(sys.argv[2:] or ("std128", "lmkcdey"))

@@ -4,13 +4,20 @@ registered in the reference's BackendRegistry and every seam operation is run th
 CurrentBackend() on the GPU and through the reference's CPU path on the same objects
 (oracle/bh_driver.cpp):
 
-  BlindRotateBatch      vs RingGSWAccumulator{CGGI,LMKCDEY}::EvalAcc on arbitrary accumulators
+  BlindRotateBatch      vs RingGSWAccumulator{CGGI,LMKCDEY,DM}::EvalAcc on arbitrary accumulators
+  BlindRotateBatch with null accumulators (what BootstrapBatch passes) vs BootstrapGateCore(AND,
+                        ct + q/4), the restated test vector pinned by the reference's Bootstrap(ct, true);
+                        lux::fhe::BootstrapBatch itself with BackendHIP as the default
   ExternalProductBatch  vs AddToAccLMKCDEY (SignedDigitDecompose + NativePoly products)
+  lux::fhe::KeySwitchBatch / ModSwitchBatch (batch.cpp:251-314) with BackendHIP as the default
   KeySwitchBatch        vs LWEEncryptionScheme::KeySwitch
   ModSwitchBatch        vs LWEEncryptionScheme::ModSwitch (Q -> qKS, qKS -> q)
-  EvalBinGateBatch      vs lux::fhe::EvalBinGateBatch (batch.cpp)
+  EvalBinGateBatch      vs lux::fhe::EvalBinGateBatch (batch.cpp), directly and routed through the registry
   Pack/Unpack{BootstrappingKey,Ciphertexts}, memory calls, info calls.
-Keys: our seeded keys (as the goldens use) and, for GINX, keys the reference generated itself."""
+Parameter sets: STD128 / STD128_LMKCDEY / STD128_AP on the 32-bit kernels, STD128_3 (GINX, digitsG = 4)
+and STD128_4_LMKCDEY (the split-layout sets, whose seam calls run on the 64-bit accumulator), STD192 and
+STD192_LMKCDEY (N = 2048).  Keys: our seeded keys (as the goldens use) and, for STD128 GINX, keys the
+reference generated itself."""
 import ctypes
 import os
 import subprocess
@@ -27,7 +34,13 @@ sz = ctypes.c_size_t
 u64 = ctypes.c_uint64
 STD128, STD128_LMKCDEY, GINX, LMKCDEY = 3, 21, 2, 3
 BH = ["bh_register", "bh_unregister", "bh_info", "bh_memory_roundtrip", "bh_blind_rotate", "bh_external_product",
-      "bh_keyswitch", "bh_modswitch", "bh_eval_gates", "bh_pack_roundtrip", "bh_last_error"]
+      "bh_keyswitch", "bh_modswitch", "bh_eval_gates", "bh_pack_roundtrip", "bh_last_error", "bh_bootstrap_init",
+      "bh_batch_callers", "bh_eval_gates_routed"]
+STD128_AP, AP = 2, 1
+# name -> (paramset, method) (binfhe-constants.h:49-95); "_refkeys": keys from the reference's BTKeyGen
+BACKEND_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "std128_refkeys": (STD128, GINX),
+                "ap": (STD128_AP, AP), "std128_3": (4, GINX), "std128_4_lmkcdey": (23, LMKCDEY),
+                "std192": (9, GINX), "std192_lmkcdey": (27, LMKCDEY)}
 
 needs_backend = pytest.mark.skipif(not backend_available(), reason="oracle/_ref/libbackend_hip.so not built")
 
@@ -110,7 +123,7 @@ def backend(name):
         for b in _backends.values():
             b.close()
         _backends.clear()
-        ps, m = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "std128_refkeys": (STD128, GINX)}[name]
+        ps, m = BACKEND_SETS[name]
         keys = None if name.endswith("refkeys") else bf.keygen(ps, m, 0xB0070000 + ps)
         _backends[name] = Backend(ps, m, keys)
     return _backends[name]
@@ -124,13 +137,24 @@ def _release():
     _backends.clear()
 
 
-SETS = ["std128", "lmkcdey", "std128_refkeys"]
+SETS = list(BACKEND_SETS)
+
+
+@pytest.fixture(scope="module", params=SETS)
+def bset(request):
+    """the parameter set under test; module scope with params makes pytest run every test of one set
+    before the next set is set up (one key generation and registration per set)"""
+    return request.param
+
+
+NOREF = [x for x in SETS if x != "std128_refkeys"]
 
 
 @pytest.mark.gpu
 @needs_backend
-@pytest.mark.parametrize("name", SETS[:2])
-def test_gpu_backend_registered_info_and_memory(name):
+@pytest.mark.parametrize("bset", ("std128", "lmkcdey"), indirect=True)
+def test_gpu_backend_registered_info_and_memory(bset):
+    name = bset
     b = backend(name)
     out = np.zeros(5, np.uint64)
     buf = ctypes.create_string_buffer(256)
@@ -146,13 +170,13 @@ def test_gpu_backend_registered_info_and_memory(name):
 
 @pytest.mark.gpu
 @needs_backend
-@pytest.mark.parametrize("name", SETS)
-def test_gpu_backend_blind_rotate_equals_evalacc(name):
+def test_gpu_backend_blind_rotate_equals_evalacc(bset):
+    name = bset
     """BlindRotateBatch on arbitrary accumulators (uniform mod Q, EVALUATION) and ragged counts"""
     b = backend(name)
     r = b.ref
     rng = np.random.default_rng(11)
-    mods = [r.q, 2 * r.N] if r.method_is_ginx else [2 * r.N]
+    mods = [r.q, 2 * r.N] if r.method_is_ginx else [r.q] if b.m == AP else [2 * r.N]
     for ctmod in mods:
         for count in (1, 6):
             a = rng.integers(0, ctmod, (count, r.n), dtype=np.uint64)
@@ -164,8 +188,9 @@ def test_gpu_backend_blind_rotate_equals_evalacc(name):
 
 @pytest.mark.gpu
 @needs_backend
-@pytest.mark.parametrize("name", SETS[:2])
-def test_gpu_backend_external_product_equals_reference(name):
+@pytest.mark.parametrize("bset", NOREF, indirect=True)
+def test_gpu_backend_external_product_equals_reference(bset):
+    name = bset
     b = backend(name)
     r = b.ref
     rng = np.random.default_rng(12)
@@ -180,8 +205,9 @@ def test_gpu_backend_external_product_equals_reference(name):
 
 @pytest.mark.gpu
 @needs_backend
-@pytest.mark.parametrize("name", SETS)
-def test_gpu_backend_keyswitch_and_modswitch_equal_reference(name):
+@pytest.mark.parametrize("bset", NOREF, indirect=True)
+def test_gpu_backend_keyswitch_and_modswitch_equal_reference(bset):
+    name = bset
     b = backend(name)
     r = b.ref
     rng = np.random.default_rng(13)
@@ -206,8 +232,8 @@ def test_gpu_backend_keyswitch_and_modswitch_equal_reference(name):
 
 @pytest.mark.gpu
 @needs_backend
-@pytest.mark.parametrize("name", SETS)
-def test_gpu_backend_gate_batch_equals_reference_evalbingatebatch(name):
+def test_gpu_backend_gate_batch_equals_reference_evalbingatebatch(bset):
+    name = bset
     from fhe_amd import binfhe as bf
     b = backend(name)
     r = b.ref
@@ -226,8 +252,9 @@ def test_gpu_backend_gate_batch_equals_reference_evalbingatebatch(name):
 
 @pytest.mark.gpu
 @needs_backend
-@pytest.mark.parametrize("name", SETS[:2])
-def test_gpu_backend_pack_roundtrips(name):
+@pytest.mark.parametrize("bset", ("std128", "lmkcdey"), indirect=True)
+def test_gpu_backend_pack_roundtrips(bset):
+    name = bset
     b = backend(name)
     r = b.ref
     rng = np.random.default_rng(15)
@@ -237,3 +264,77 @@ def test_gpu_backend_pack_roundtrips(name):
     ok = ctypes.c_int()
     b.chk(b.L.bh_pack_roundtrip(b.h, sz(count), P(a), P(bb), ctypes.byref(ok)))
     assert ok.value == 3, ok.value
+
+
+@pytest.mark.gpu
+@needs_backend
+def test_gpu_backend_null_accumulators_and_bootstrapbatch(bset):
+    name = bset
+    """BlindRotateBatch with null accumulators (BootstrapBatch, batch.cpp:77-86) ==
+    BootstrapGateCore(AND, ct + q/4); its extraction == the reference's Bootstrap(ct, true); and the
+    reference's BootstrapBatch succeeds with BackendHIP as the default"""
+    from fhe_amd import binfhe as bf
+    b = backend(name)
+    r = b.ref
+    for count, seed in ((1, 21), (5, 22)):
+        bits = np.random.default_rng(seed).integers(0, 2, count)
+        a, bb = bf.encrypt(b.ps, b.m, b.sk, bits, 700 + seed)
+        g = np.zeros((count, 2, r.N), np.uint64)
+        ref = np.zeros_like(g)
+        flags = ctypes.c_int()
+        b.chk(b.L.bh_bootstrap_init(b.h, sz(count), P(a), P(bb), P(g), P(ref), ctypes.byref(flags)))
+        assert flags.value == 3, (name, flags.value)
+        assert np.array_equal(g, ref), (name, count)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("bset", NOREF, indirect=True)
+def test_gpu_backend_reference_batch_callers(bset):
+    name = bset
+    """lux::fhe::KeySwitchBatch / ModSwitchBatch (batch.cpp:251-314) through the registry == the
+    reference's LWEEncryptionScheme::KeySwitch / ModSwitch"""
+    b = backend(name)
+    r = b.ref
+    rng = np.random.default_rng(16)
+    count = 7
+    ka = rng.integers(0, r.qKS, (count, r.N), dtype=np.uint64)
+    kb = rng.integers(0, r.qKS, count, dtype=np.uint64)
+    ma = rng.integers(0, r.Q, (count, r.N), dtype=np.uint64)
+    mb = rng.integers(0, r.Q, count, dtype=np.uint64)
+    gka, gkb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+    rka, rkb = np.zeros_like(gka), np.zeros_like(gkb)
+    gma, gmb = np.zeros_like(ma), np.zeros_like(mb)
+    rma, rmb = np.zeros_like(ma), np.zeros_like(mb)
+    ok = ctypes.c_int()
+    b.chk(b.L.bh_batch_callers(b.h, sz(count), P(ka), P(kb), P(gka), P(gkb), P(rka), P(rkb), P(ma), P(mb), P(gma),
+                               P(gmb), P(rma), P(rmb), ctypes.byref(ok)))
+    assert ok.value == 1
+    assert np.array_equal(gka, rka) and np.array_equal(gkb, rkb), name
+    assert np.array_equal(gma, rma) and np.array_equal(gmb, rmb), name
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("bset", ["std128", "lmkcdey", "std128_3", "std192"], indirect=True)
+def test_gpu_backend_routed_gate_batch_equals_reference(bset):
+    name = bset
+    """EvalBinGateBatchHIP (the routing INTEGRATION.md proposes for batch.cpp:176-210) with BackendHIP as the
+    default == the reference's EvalBinGateBatch"""
+    from fhe_amd import binfhe as bf
+    b = backend(name)
+    r = b.ref
+    count = 9
+    rng = np.random.default_rng(17)
+    x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+    a1, b1 = bf.encrypt(b.ps, b.m, b.sk, x1, 601)
+    a2, b2 = bf.encrypt(b.ps, b.m, b.sk, x2, 602)
+    for gate, truth in ((0, x1 | x2), (5, 1 - (x1 ^ x2))):
+        ga, gb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+        ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+        ok = ctypes.c_int()
+        b.chk(b.L.bh_eval_gates_routed(b.h, gate, sz(count), P(a1), P(b1), P(a2), P(b2), P(ga), P(gb), P(ra), P(rb),
+                                       ctypes.byref(ok)))
+        assert ok.value == 1
+        assert np.array_equal(ga, ra) and np.array_equal(gb, rb), (name, gate)
+        assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), truth), (name, gate)

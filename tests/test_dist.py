@@ -71,3 +71,59 @@ def test_gloo_world2_sharded_gates(tmp_path, restatement):
     fa, fb = Restatement(bf.STD128, bf.GINX).eval_gate(keys.bsk, keys.kskA, keys.kskB, 1, a1, b1, a2, b2)
     assert np.array_equal(ao, fa) and np.array_equal(bo, fb)
     assert np.array_equal(bf.decrypt(bf.STD128, bf.GINX, keys.sk, ao, bo), (x1 & x2).astype(np.int64))
+
+
+def test_bench_refuses_more_ranks_than_devices():
+    """`bench.py --gpus N` without a launcher starts N ranks itself; with fewer than N devices visible
+    (none here) it fails loudly instead of measuring one rank"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "FHE_BENCH_DEVICE_MAP")}
+    import torch
+    n = torch.cuda.device_count()      # counts without initialising the GPU
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(max(n + 1, 2)), "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "GPU(s) are visible" in r.stderr
+
+
+def _engine_worker(rank, world, port, outdir):
+    """one rank of the sharded run: the HIP engine on its contiguous 8192-gate shard of config 4's
+    batch (device 0 for both ranks), gloo for the control plane as bench.py's rehearsal"""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, gold)
+    from fhe_amd import binfhe as bf
+    from fhe_amd.dist import barrier, max_over_ranks
+    from make_golden import full_inputs
+    ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2 = full_inputs("std128")
+    lo, hi = rank * 8192, (rank + 1) * 8192          # shards 0 and 1 of the 8-GPU split
+    eng = bf.GateEngine(ps, m, device=0)
+    eng.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    barrier()
+    ao, bo = eng.eval_gate(1, a1[lo:hi], b1[lo:hi], a2[lo:hi], b2[lo:hi])
+    t = max_over_ranks([float(rank + 1)])
+    barrier()
+    eng.close()
+    np.savez(os.path.join(outdir, f"e{rank}.npz"), ao=ao, bo=bo, t=t[0])
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_gloo_world2_engine_shards_bit_exact(tmp_path):
+    """two processes, each a GateEngine on its contiguous shard (both on device 0), reassemble to the
+    reference's outputs: shard hashes of tests/golden/full_std128.npz"""
+    import hashlib
+    world = 2
+    mp.spawn(_engine_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_std128.npz"))
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a, np.uint64).tobytes()).hexdigest()  # noqa: E731
+    for r in range(world):
+        p = np.load(tmp_path / f"e{r}.npz")
+        assert float(p["t"]) == float(world)
+        assert sha(p["ao"]) + sha(p["bo"]) == str(g["shard_sha"][r]), r

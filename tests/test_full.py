@@ -77,3 +77,36 @@ def test_gpu_full_batch_eight_shards_bit_exact(name):
     ao, bo = me.eval_gate(int(g["gate"]), a1, b1, a2, b2)
     me.close()
     assert sha(ao) + sha(bo) == str(g["out_sha"])
+
+
+# ---- BASELINE config 3: 1024 STD128 GINX AND gates (the batch bench.py's config3 object runs) ----
+def config3():
+    if "c3" not in _cache:
+        sys.path.insert(0, GOLD)
+        from make_golden import full_inputs
+        g = np.load(os.path.join(GOLD, "full_std128_b1024.npz"))
+        _cache["c3"] = (g, full_inputs("std128", int(g["count"])))
+    return _cache["c3"]
+
+
+def test_config3_inputs_match_golden_and_head_decrypts():
+    from fhe_amd import binfhe as bf
+    g, (ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2) = config3()
+    assert int(g["count"]) == 1024 and int(g["paramset"]) == ps
+    assert sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB) == str(g["keys_sha"])
+    assert sha(a1) + sha(b1) + sha(a2) + sha(b2) == str(g["in_sha"])
+    dec = bf.decrypt(ps, m, keys.sk, g["out_a_head"].astype(np.uint64), g["out_b_head"].astype(np.uint64))
+    assert np.array_equal(dec, (bits1 & bits2)[:16])
+
+
+@pytest.mark.gpu
+def test_gpu_config3_batch_bit_exact():
+    """the 1024-gate batch at its own size (row-split key switch, one wave per gate) == the reference"""
+    from fhe_amd import binfhe as bf
+    g, (ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2) = config3()
+    eng = bf.GateEngine(ps, m, device=0)
+    eng.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    ao, bo = eng.eval_gate(int(g["gate"]), a1, b1, a2, b2)
+    eng.close()
+    assert sha(ao) + sha(bo) == str(g["out_sha"])
+    assert np.array_equal(ao[:16], g["out_a_head"].astype(np.uint64))
