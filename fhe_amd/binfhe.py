@@ -46,7 +46,7 @@ MULTI_GATES = (MAJORITY, AND3, OR3, AND4, OR4)
 
 class _Params(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint32) for f in ("paramset", "method", "n", "N", "q", "baseKS", "digitsKS",
-                                               "baseG", "digitsG", "numAutoKeys", "keyDist", "reserved")] + \
+                                               "baseG", "digitsG", "numAutoKeys", "keyDist", "kernel")] + \
                [(f, ctypes.c_uint64) for f in ("Q", "psi", "qKS", "bsk_words", "ksk_rows")]
 
 
@@ -113,7 +113,7 @@ def _setup(L):
     L.fhe_hip_external_product_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
     L.fhe_hip_max_batch_size.argtypes = [vp, vp]
     L.fhe_hip_device_memory.argtypes = [ctypes.c_int, vp, vp]
-    L.fhe_hip_unpack_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, vp, sz, vp, vp]
+    L.fhe_hip_unpack_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, sz, vp, sz, vp, sz, vp, sz]
     L._binfhe_ready = True
     return L
 
@@ -135,7 +135,7 @@ class Params:
     digitsG: int
     numAutoKeys: int
     keyDist: int
-    reserved: int
+    kernel: int
     Q: int
     psi: int
     qKS: int
@@ -149,11 +149,15 @@ def params(paramset, method):
     return Params(**{f: int(getattr(p, f)) for f, _ in _Params._fields_})
 
 
+def kernel_path(paramset, method):
+    """the accumulator kernels (paramset, method) runs on, as the engine chooses them
+    (fhe_hip_params.kernel): 1 = 32-bit one-wave, 2 = 32-bit split (digitsG = 4), 0 = 64-bit"""
+    return params(paramset, method).kernel
+
+
 def uses_fast_kernels(paramset, method):
-    """True when (paramset, method) runs on the 32-bit kernels (N = 1024, Q < 2^28, digitsG = 3, ...)"""
-    P = params(paramset, method)
-    return (not paramset & LARGE and P.N == 1024 and P.Q < (1 << 28) and P.digitsG == 3 and P.qKS <= 65536
-            and P.n < 1024)
+    """True when (paramset, method) runs on one of the 32-bit accumulator kernels"""
+    return kernel_path(paramset, method) != 0
 
 
 def _u64(a):
@@ -249,6 +253,17 @@ def pack_keys(paramset, method, keys):
     check(L().fhe_hip_pack_keys(paramset, method, ptr(bsk), bsk.size, ptr(A), ptr(B), ptr(ob), ob.size,
                                 ctypes.byref(s1), ptr(ok), ok.size, ctypes.byref(s2)))
     return ob, ok
+
+
+def unpack_keys(paramset, method, bsk_packed, ksk_packed):
+    """the raw KeySet (sk = None) of packed keys (Backend::UnpackBootstrappingKey)"""
+    P = params(paramset, method)
+    ob, ok = _buf(bsk_packed), _buf(ksk_packed)
+    bsk = np.zeros(P.bsk_words, np.uint64)
+    A, B = np.zeros(P.ksk_rows * P.n, np.uint64), np.zeros(P.ksk_rows, np.uint64)
+    check(L().fhe_hip_unpack_keys(paramset, method, ptr(ob), ob.size, ptr(bsk), bsk.size, ptr(ok), ok.size, ptr(A),
+                                  A.size, ptr(B), B.size))
+    return KeySet(None, bsk, A, B)
 
 
 # ---- the reference's serialized objects (Serial::Serialize(..., SerType::BINARY)) ----

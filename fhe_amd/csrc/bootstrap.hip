@@ -1129,14 +1129,24 @@ FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* 
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
+#if defined(FHE_ABL) && (FHE_ABL & 256)
+            v[r] = region[(uint32_t)r * 32 + l];   // ablation (wrong results): linear reads
+            (void)cl; (void)sr;
+#else
             v[r]              = region[at(((cl + sr) >> 1) & 1023)];
+#endif
         }
         const uint32_t cL = (((__builtin_bitreverse32((uint32_t)L) >> 26) << 3) + 1) * k;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t H = (uint32_t)r >> 2, j = (uint32_t)r & 3;
             const uint32_t su = ((((j & 1) << 1 | j >> 1) << 9) + (((H & 1) << 1 | H >> 1) << 1)) * k;  // uniform
+#if defined(FHE_ABL) && (FHE_ABL & 512)
+            a0[r] = region0[(uint32_t)r * 64 + L];   // ablation (wrong results): linear reads
+            (void)cL; (void)su;
+#else
             a0[r]             = region0[at(((cL + su) >> 1) & 1023)];
+#endif
         }
         wave_lds_sync();
         return;

@@ -71,10 +71,11 @@ struct fhe_hip_ctx {
 };
 
 static void fill_params(const Params& p, fhe_hip_params* o) {
-    o->paramset = p.paramset; o->method = p.method; o->n = p.n; o->N = p.N; o->q = p.q; o->qKS = p.qKS; o->reserved = 0;
+    o->paramset = p.paramset; o->method = p.method; o->n = p.n; o->N = p.N; o->q = p.q; o->qKS = p.qKS;
+    o->kernel = Engine::fast_path(p) ? 1u : Engine::g3_set(p) ? 2u : 0u;
     o->baseKS = p.baseKS; o->digitsKS = p.digitsKS; o->baseG = p.baseG; o->digitsG = p.digitsG;
     o->numAutoKeys = p.numAutoKeys; o->keyDist = p.keyDist; o->Q = p.Q; o->psi = p.psi;
-    o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows();
+    o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows_all();
 }
 
 // The stream a context's call runs on: the caller's (or the context's own).  A context has one
@@ -326,7 +327,7 @@ int fhe_hip_pack_keys(int paramset, int method, const uint64_t* bsk, size_t bsk_
     return guarded([&]() -> int {
         const Params p = make_params(paramset, method);
         *bsk_size = sizeof(PackedBskHdr) + p.bsk_words() * 8;
-        *ksk_size = sizeof(PackedKskHdr) + p.ksk_rows() * ((size_t)p.n + 1) * 8;
+        *ksk_size = sizeof(PackedKskHdr) + p.ksk_rows_all() * ((size_t)p.n + 1) * 8;
         if (bsk_out) {
             if (!bsk || bsk_cap < *bsk_size) return fail(FHE_HIP_ERR_INVALID_PARAM, "bsk buffer missing or too small");
             auto v = pack_bsk(p, bsk, bsk_words);
@@ -351,7 +352,7 @@ int fhe_hip_load_keys_packed(fhe_hip_ctx* ctx, const uint8_t* bsk, size_t bsk_si
         const uint64_t *A = nullptr, *B = nullptr;
         unpack_ksk(p, ksk, ksk_size, &A, &B);
         ctx->eng.load_bsk(raw, words);
-        ctx->eng.load_ksk(A, p.ksk_rows() * p.n, B, p.ksk_rows());
+        ctx->eng.load_ksk(A, p.ksk_rows_all() * p.n, B, p.ksk_rows_all());
         return FHE_HIP_OK;
     });
 }
@@ -660,20 +661,23 @@ int fhe_hip_device_memory(int device, size_t* free_bytes, size_t* total_bytes) {
 }
 
 int fhe_hip_unpack_keys(int paramset, int method, const uint8_t* bsk_packed, size_t bsk_size, uint64_t* bsk,
-                        const uint8_t* ksk_packed, size_t ksk_size, uint64_t* kskA, uint64_t* kskB) {
-    if ((!bsk_packed || !bsk) && (!ksk_packed || !kskA || !kskB)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+                        size_t bsk_cap, const uint8_t* ksk_packed, size_t ksk_size, uint64_t* kskA, size_t kskA_cap,
+                        uint64_t* kskB, size_t kskB_cap) {
     return guarded([&]() -> int {
         const Params p = make_params(paramset, method);
         if (bsk_packed && bsk) {
             size_t words = 0;
             const uint64_t* raw = unpack_bsk(p, bsk_packed, bsk_size, &words);
+            if (bsk_cap < words) return fail(FHE_HIP_ERR_INVALID_PARAM, "bsk buffer too small");
             std::copy(raw, raw + words, bsk);
         }
         if (ksk_packed && kskA && kskB) {
             const uint64_t *A = nullptr, *B = nullptr;
             unpack_ksk(p, ksk_packed, ksk_size, &A, &B);
-            std::copy(A, A + p.ksk_rows() * p.n, kskA);
-            std::copy(B, B + p.ksk_rows(), kskB);
+            const size_t rows = p.ksk_rows_all();
+            if (kskA_cap < rows * p.n || kskB_cap < rows) return fail(FHE_HIP_ERR_INVALID_PARAM, "ksk buffers too small");
+            std::copy(A, A + rows * p.n, kskA);
+            std::copy(B, B + rows, kskB);
         }
         return FHE_HIP_OK;
     });

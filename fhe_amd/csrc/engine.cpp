@@ -265,6 +265,7 @@ void Engine::build_loggen() {
 void Engine::set_base(uint32_t bg) {
     cur_ = p_.timeopt ? p_.with_base(bg) : p_;
     cur_off_ = p_.bsk_offset(bg);
+    cur_ksk_off_ = p_.ksk_index(bg) * p_.ksk_rows() * ((size_t)p_.n + 1);
 }
 
 void Engine::build_tables_wide() {
@@ -401,8 +402,10 @@ void Engine::repack_ginx2() {
 void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB) {
     if (!A || !B) throw std::invalid_argument("ksk is null");
     const size_t rows = p_.ksk_rows();
-    if (nA != rows * p_.n || nB != rows) throw std::invalid_argument("ksk has wrong length");
-    if (wide_) {  // u64 A [rows][n] ++ B [rows] as given
+    if (nA != p_.ksk_rows_all() * p_.n || nB != p_.ksk_rows_all())
+        throw std::invalid_argument(p_.timeopt ? "ksk has wrong length (timeOptimization: the map's three switching keys)"
+                                               : "ksk has wrong length");
+    if (wide_) {  // u64 A [rows][n] ++ B [rows] as given, per key of the map
         bool bad = false;
 #pragma omp parallel for schedule(static) reduction(|| : bad)
         for (int64_t r = 0; r < (int64_t)nA; ++r) bad = bad || A[r] >= p_.qKS;
@@ -412,8 +415,11 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
         if (d_wksk_) FHE_HIP_CHECK(hipFree(d_wksk_));
         d_wksk_ = nullptr;
         FHE_HIP_CHECK(hipMalloc(&d_wksk_, (nA + nB) * 8));
-        FHE_HIP_CHECK(hipMemcpy(d_wksk_, A, nA * 8, hipMemcpyHostToDevice));
-        FHE_HIP_CHECK(hipMemcpy(d_wksk_ + nA, B, nB * 8, hipMemcpyHostToDevice));
+        const size_t one = rows * ((size_t)p_.n + 1);
+        for (size_t k = 0; k < p_.ksk_keys(); ++k) {
+            FHE_HIP_CHECK(hipMemcpy(d_wksk_ + k * one, A + k * rows * p_.n, rows * p_.n * 8, hipMemcpyHostToDevice));
+            FHE_HIP_CHECK(hipMemcpy(d_wksk_ + k * one + rows * p_.n, B + k * rows, rows * 8, hipMemcpyHostToDevice));
+        }
         if (!g3_) return;
         // g3_: also the u16 rows of the 32-bit key switch (qKS <= 2^16, n < 1024; g3_set)
     }
@@ -852,8 +858,9 @@ void Engine::keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64
     }
     if (wide_) {
         const size_t rows = p_.ksk_rows();
-        FHE_HIP_CHECK(launch_keyswitch_wide(count, p_.n, p_.N, p_.baseKS, p_.digitsKS, p_.qKS, d_wksk_,
-                                            d_wksk_ + rows * p_.n, d_wext_a_, d_wext_b_, q_out, a_out, b_out, s));
+        const uint64_t* ksk = d_wksk_ + cur_ksk_off_;  // timeOptimization: the switching key of the current base
+        FHE_HIP_CHECK(launch_keyswitch_wide(count, p_.n, p_.N, p_.baseKS, p_.digitsKS, p_.qKS, ksk, ksk + rows * p_.n,
+                                            d_wext_a_, d_wext_b_, q_out, a_out, b_out, s));
         return;
     }
     GateArgs g = gate_args(G_AND, count);

@@ -55,6 +55,8 @@ public:
     bool wide() const { return wide_; }
     // the 32-bit kernels' range: N = 1024, Q < 2^28, digitsG = 3, power-of-two q, qKS <= 2^16, n < 1024
     static bool fast_path(const Params& p);
+    // the digitsG = 4 sets at N = 1024, Q < 2^27 the split kernels take (K1s / K1m)
+    static bool g3_set(const Params& p);
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -188,7 +190,6 @@ private:
     // gates on the split kernel with three digits per component (launch_blind_rotate_ginx3) over the
     // 32-bit tables tabs_, the rest of the 64-bit path unchanged.  FHE_HIP_GINX3=0 keeps them on the 64-bit accumulator (A/B, tests).
     bool g3_ = false;
-    static bool g3_set(const Params& p);
     void pack_ginx3(const uint64_t* bsk);
     // cross-stream ordering (use_stream)
     hipStream_t last_stream_ = nullptr;
@@ -227,6 +228,7 @@ private:
     // one EvalSign / EvalDecomp switched to (set_base); word offset into d_bsk_ and its digits
     Params cur_;
     size_t cur_off_ = 0;
+    size_t cur_ksk_off_ = 0;   // word offset of the current base's switching key in d_wksk_
     void set_base(uint32_t bg);
     void dynamic_base(uint64_t mod);
     struct BaseGuard {  // Change_BaseG(curBase) when EvalSign / EvalDecomp end (:453, :518)

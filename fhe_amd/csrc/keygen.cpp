@@ -3,6 +3,7 @@
 
 #include <omp.h>
 
+#include <cmath>
 #include <stdexcept>
 
 #include "nt.h"
@@ -17,17 +18,9 @@ struct Rng {
         s = rng_state(seed, tag, stream);
         next();
     }
-    uint64_t next() {
-        uint64_t z = (s += kRngGamma);
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        return z ^ (z >> 31);
-    }
+    uint64_t next() { return mix64(s += kRngGamma); }
     uint64_t uniform(uint64_t m) { return (uint64_t)(((u128)next() * m) >> 64); }
-    int64_t cbd() {  // centred binomial, k = 20: variance 10
-        uint64_t r = next();
-        return (int64_t)__builtin_popcountll(r & 0xFFFFFull) - (int64_t)__builtin_popcountll((r >> 20) & 0xFFFFFull);
-    }
+    int64_t dgg() { return dgg_sample(next(), dgg_table()); }  // the reference's DGG, sigma 3.19
     int64_t ternary() { return (int64_t)uniform(3) - 1; }
 };
 
@@ -39,6 +32,25 @@ inline uint64_t lift(int64_t v, uint64_t m) {
 inline int64_t signed_of(uint64_t x, uint64_t m) { return x > (m >> 1) ? (int64_t)x - (int64_t)m : (int64_t)x; }
 
 }  // namespace
+
+const DggTable& dgg_table() {
+    static const DggTable t = [] {
+        DggTable d{};
+        const double M = 12.00610553538285;
+        d.fin = (int)std::ceil(kDggSigma * M);
+        if (d.fin > kDggMaxFin) throw std::logic_error("DGG table size");
+        const double variance = 2 * kDggSigma * kDggSigma;
+        double cusum = 0.0;
+        for (int x = 1; x <= d.fin; ++x) {
+            cusum += std::exp(-((double)(x * x) / variance));
+            d.vals[x - 1] = cusum;
+        }
+        d.a = 1.0 / (2 * cusum + 1.0);
+        for (int x = 0; x < d.fin; ++x) d.vals[x] *= d.a;
+        return d;
+    }();
+    return t;
+}
 
 void auto_eval(const Params& p, uint32_t k, const uint64_t* in, uint64_t* out) {
     // AutomorphismTransform(k) in EVALUATION (poly-impl.h:350-356)
@@ -52,14 +64,14 @@ void auto_eval(const Params& p, uint32_t k, const uint64_t* in, uint64_t* out) {
 void keygen_ring_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& skN) {
     skN.assign(p.N, 0);
     Rng r(seed, T_SKN, 0);
-    for (uint32_t i = 0; i < p.N; ++i) skN[i] = lift(p.keyDist == KD_GAUSSIAN ? r.cbd() : r.ternary(), p.Q);
+    for (uint32_t i = 0; i < p.N; ++i) skN[i] = lift(p.keyDist == KD_GAUSSIAN ? r.dgg() : r.ternary(), p.Q);
 }
 
 void keygen_secret(const Params& p, uint64_t seed, std::vector<uint64_t>& sk) {
     sk.assign(p.n, 0);
     Rng r(seed, T_SK, 0);
     for (uint32_t i = 0; i < p.n; ++i)
-        sk[i] = lift(p.keyDist == KD_GAUSSIAN ? r.cbd() : r.ternary(), p.qKS);
+        sk[i] = lift(p.keyDist == KD_GAUSSIAN ? r.dgg() : r.ternary(), p.qKS);
 }
 
 namespace {
@@ -67,27 +79,32 @@ void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed,
                 KeySet& out);
 }
 
-// timeOptimization (BTKeyGen, binfhecontext.cpp:285-307): one key per baseG of the map, all under
-// one RLWE secret skN and sharing one switching key; the key of the context's own baseG is the
-// one keygen without timeOptimization makes from the same seed
+// timeOptimization (BTKeyGen, binfhecontext.cpp:285-307): one whole key per baseG of the map, as the
+// reference's KeyGen per base makes it -- its own RLWE secret skN, bootstrapping key and switching
+// key; the key of the context's own baseG is the one keygen without timeOptimization makes from the
+// same seed (out.skN is that base's secret)
 void keygen_bootstrap(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed, KeySet& out) {
     if (!p.timeopt) {
         keygen_one(p, sk, seed, seed, true, out);
         return;
     }
     out.bsk.assign(p.bsk_words(), 0);
+    out.kskA.assign(p.ksk_rows_all() * p.n, 0);
+    out.kskB.assign(p.ksk_rows_all(), 0);
     for (uint32_t bg : kSignBases) {
         Params pb = p.with_base(bg);
         pb.timeopt = false;
         KeySet t;
         const bool own = bg == p.baseG;
-        keygen_one(pb, sk, seed, own ? seed : seed ^ ((uint64_t)bg * kRngGamma), own, t);
+        const uint64_t sb = own ? seed : seed ^ ((uint64_t)bg * kRngGamma);
+        keygen_one(pb, sk, sb, sb, true, t);
+        const size_t k = p.ksk_index(bg), rows = p.ksk_rows();
         std::copy(t.bsk.begin(), t.bsk.end(), out.bsk.begin() + p.bsk_offset(bg));
+        std::copy(t.kskA.begin(), t.kskA.end(), out.kskA.begin() + k * rows * p.n);
+        std::copy(t.kskB.begin(), t.kskB.end(), out.kskB.begin() + k * rows);
         if (own) {
             out.sk = std::move(t.sk);
             out.skN = std::move(t.skN);
-            out.kskA = std::move(t.kskA);
-            out.kskB = std::move(t.kskB);
         }
     }
 }
@@ -114,7 +131,7 @@ void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed,
         // row0 = A (+msg), row1 = A*S + NTT(e) (+msg)   (KeyGenCGGI/KeyGenLMKCDEY structure)
         std::vector<uint64_t> e(N);
         for (uint32_t j = 0; j < N; ++j) row0[j] = r.uniform(Q);
-        for (uint32_t j = 0; j < N; ++j) e[j] = lift(r.cbd(), Q);
+        for (uint32_t j = 0; j < N; ++j) e[j] = lift(r.dgg(), Q);
         ntt.forward(e.data());
         for (uint32_t j = 0; j < N; ++j) row1[j] = addmod(mulmod(row0[j], S[j], Q), e[j], Q);
         if (msg_eval) {
@@ -200,7 +217,7 @@ void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed,
                 uint64_t* r0 = key + (size_t)row * 2 * N;
                 uint64_t* r1 = r0 + N;
                 for (uint32_t j = 0; j < N; ++j) r0[j] = r.uniform(Q);
-                for (uint32_t j = 0; j < N; ++j) e[j] = lift(r.cbd(), Q);
+                for (uint32_t j = 0; j < N; ++j) e[j] = lift(r.dgg(), Q);
                 ntt.forward(e.data());
                 const uint64_t g = p.gpow[row + 1];
                 for (uint32_t j = 0; j < N; ++j)
@@ -234,7 +251,7 @@ void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed,
                     a[t] = r.uniform(qk);
                     acc += (u128)a[t] * sv[t];
                 }
-                uint64_t b = lift(r.cbd(), qk);
+                uint64_t b = lift(r.dgg(), qk);
                 b = addmod(b, mulmod(svN, (j * digitsKS[k]) % qk, qk), qk);
                 b = addmod(b, (uint64_t)(acc % qk), qk);
                 out.kskB[row] = b;
@@ -258,7 +275,7 @@ void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count,
         }
         // b = (m mod p) (q / p) + e + <a, s>   (lwe-pke.cpp:103-128)
         uint64_t m = ((uint64_t)(uint32_t)bits[g] % ptmod) * (q / ptmod);
-        b[g] = (m + lift(r.cbd(), q) + (uint64_t)(acc % q)) % q;
+        b[g] = (m + lift(r.dgg(), q) + (uint64_t)(acc % q)) % q;
     }
 }
 

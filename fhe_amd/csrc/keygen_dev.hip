@@ -8,7 +8,7 @@
 // u16 KSK rows), with the reference raw layouts as an optional export.
 //
 // Per RGSW row pair (row0 = A + msg?, row1 = A * S + NTT(e) + msg?):
-//   k_kg_sample  A uniform mod Q (drawn in EVALUATION), e centred binomial, message monomial
+//   k_kg_sample  A uniform mod Q (drawn in EVALUATION), e the reference's discrete Gaussian, message monomial
 //                folded into e (row1 message) or kept as M (row0 message)  -> [E, M] per pair
 //   ntt1024      forward NTT of every E and M (the batched kernel of ntt.hip)
 //   k_kg_finish  row1 = A*S + E (- skAuto*g for automorphism keys), row0 = A + M
@@ -39,30 +39,25 @@ struct KgDesc {
 };
 static_assert(sizeof(KgDesc) == 40, "descriptor layout");
 
-__device__ __forceinline__ uint64_t draw(uint64_t s0, uint64_t k) {
-    uint64_t z = s0 + (k + 2) * kRngGamma;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
+__device__ __forceinline__ uint64_t draw(uint64_t s0, uint64_t k) { return mix64(s0 + (k + 2) * kRngGamma); }
 __device__ __forceinline__ uint64_t draw_uniform(uint64_t s0, uint64_t k, uint64_t m) {
     return __umul64hi(draw(s0, k), m);
 }
-__device__ __forceinline__ uint64_t draw_cbd(uint64_t s0, uint64_t k, uint64_t m) {  // lifted mod m
-    const uint64_t r = draw(s0, k);
-    const int64_t v = (int64_t)__popcll(r & 0xFFFFFull) - (int64_t)__popcll((r >> 20) & 0xFFFFFull);
+// the reference's discrete Gaussian (keygen.h dgg_sample) on the host's table, lifted mod m
+__device__ __forceinline__ uint64_t draw_dgg(uint64_t s0, uint64_t k, uint64_t m, const DggTable& t) {
+    const int64_t v = dgg_sample(draw(s0, k), t);
     return v < 0 ? (uint64_t)(v + (int64_t)m) : (uint64_t)v;
 }
 
 __global__ void __launch_bounds__(256) k_kg_sample(const KgDesc* __restrict__ D, uint32_t N, uint64_t Q,
-                                                   uint64_t* __restrict__ A, uint64_t* __restrict__ T) {
+                                                   uint64_t* __restrict__ A, uint64_t* __restrict__ T, DggTable dg) {
     const KgDesc k = D[blockIdx.x];
     uint64_t* a = A + (size_t)blockIdx.x * N;
     uint64_t* e = T + (size_t)blockIdx.x * 2 * N;
     uint64_t* m = e + N;
     for (uint32_t j = threadIdx.x; j < N; j += blockDim.x) {
         a[j] = draw_uniform(k.s0, k.call + j, Q);
-        uint64_t ev = draw_cbd(k.s0, k.call + N + j, Q);
+        uint64_t ev = draw_dgg(k.s0, k.call + N + j, Q, dg);
         uint64_t mv = (k.mval && j == k.mm) ? k.mval : 0;
         if (k.odd) {
             ev += mv;
@@ -122,10 +117,10 @@ __global__ void __launch_bounds__(256) k_kg_ksk(uint64_t seed, uint32_t rows, ui
                                                 uint64_t qk, const uint64_t* __restrict__ sv,
                                                 const uint64_t* __restrict__ svN, const uint64_t* __restrict__ dig,
                                                 uint16_t* __restrict__ ksk, uint64_t* __restrict__ rawA,
-                                                uint64_t* __restrict__ rawB) {
+                                                uint64_t* __restrict__ rawB, DggTable dg) {
     const uint32_t row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= rows) return;
-    const uint64_t s0 = seed * kRngGamma ^ ((uint64_t)T_KSK << 56) ^ ((uint64_t)row * 0xD1B54A32D192ED03ull);
+    const uint64_t s0 = rng_state(seed, T_KSK, row);
     uint64_t acc = 0;
     const uint32_t W = ksk_width(n);
     for (uint32_t t = lane; t < W; t += 64) {
@@ -137,7 +132,7 @@ __global__ void __launch_bounds__(256) k_kg_ksk(uint64_t seed, uint32_t rows, ui
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (lane == 0) {
         const uint32_t i = row / (bKS * dKS), j = (row / dKS) % bKS, kk = row % dKS;
-        uint64_t b = draw_cbd(s0, n, qk);
+        uint64_t b = draw_dgg(s0, n, qk, dg);
         b = (b + svN[i] * ((j * dig[kk]) % qk)) % qk;
         b = (b + acc % qk) % qk;
         ksk[(size_t)row * W + n] = (uint16_t)b;
@@ -264,7 +259,7 @@ void keygen_bootstrap_device(const Params& p, const std::vector<uint64_t>& sk, u
     DevBuf<uint64_t> dA(chunk * N), dT(chunk * 2 * N);
     for (size_t c0 = 0; c0 < desc.size(); c0 += chunk) {
         const uint32_t nc = (uint32_t)std::min(chunk, desc.size() - c0);
-        k_kg_sample<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dA.p, dT.p);
+        k_kg_sample<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dA.p, dT.p, dgg_table());
         FHE_HIP_CHECK(hipGetLastError());
         FHE_HIP_CHECK(ntt1024_launch(plan, dT.p, dT.p, 2 * nc, false, s));
         k_kg_finish<<<nc, 256, 0, s>>>(dd.p + c0, N, Q, dS.p, dAuto.p, dA.p, dT.p, invmod(N, Q), d_bsk, raw_bsk,
@@ -285,7 +280,7 @@ void keygen_bootstrap_device(const Params& p, const std::vector<uint64_t>& sk, u
     FHE_HIP_CHECK(hipMemcpyAsync(dsvN.p, svN.data(), N * 8, hipMemcpyHostToDevice, s));
     FHE_HIP_CHECK(hipMemcpyAsync(ddig.p, dig.data(), dig.size() * 8, hipMemcpyHostToDevice, s));
     k_kg_ksk<<<(rows + 3) / 4, 256, 0, s>>>(seed, rows, n, p.baseKS, p.digitsKS, qk, dsv.p, dsvN.p, ddig.p, d_ksk,
-                                            raw_kskA, raw_kskB);
+                                            raw_kskA, raw_kskB, dgg_table());
     FHE_HIP_CHECK(hipGetLastError());
     FHE_HIP_CHECK(hipStreamSynchronize(s));  // temporaries are freed on return
 }

@@ -14,6 +14,9 @@ struct NttPlan {
     void* d_tab_fwd = nullptr;
     void* d_tab_inv = nullptr;
     uint64_t ninv = 0, ninv_pre = 0, w1ninv = 0, w1ninv_pre = 0;
+    // Q = 2^60 - (2^S - 1) (the poly-benchmark prime, S = 14): S, which selects the Sol60 butterflies
+    // of k_ntt1024w64 (shift-only q Q); 0 for any other 64-bit modulus
+    uint32_t sol_shift = 0;
     // Q < 2^27: Table / TableI in Montgomery form (u32, x 2^32 mod Q) for the signed kernel
     void* d_tabm_fwd = nullptr;
     void* d_tabm_inv = nullptr;

@@ -624,12 +624,19 @@ __global__ void __launch_bounds__(512)
 
 // ---------------------------------------------------------------------------------------------
 // One polynomial per wave64 for 64-bit moduli (2^30 <= Q < 2^62): the layouts A / B / C of
-// k_ntt1024w with 16 u64 coefficients per lane, Harvey-lazy butterflies in 64 bits (forward values
-// in [0, 4Q), inverse in [0, 2Q): 4Q < 2^64) around Shoup's lazy product x w - hi(x w') Q in
-// [0, 2Q).  The transposes move the low and the high words as two 32-bit planes through the same
-// conflict-free tile (word address x + 4 (x >> 6)).
+// k_ntt1024w with 16 u64 coefficients per lane.  The transposes move the low and the high words as
+// two 32-bit planes through the same conflict-free tile (word address x + 4 (x >> 6)).  Two
+// arithmetic policies:
+//   Lazy64 (any Q < 2^62): Harvey-lazy butterflies (forward values in [0, 4Q), inverse in [0, 2Q))
+//          around Shoup's lazy product x w - hi(x w') Q in [0, 2Q);
+//   Sol60  (Q = 2^60 - (2^S - 1): the poly-benchmark prime LastPrime(60, 2048) = 2^60 - 2^14 + 1):
+//          Shoup's quotient without its low partial product (short by at most 2, product in
+//          [0, 4Q)), q Q = (q << 60) - (q << S) + q by shifts, no reduction inside a butterfly: values
+//          grow below 16 Q < 2^64 and a compile-time plan (Plan64) folds x -> x mod 2^60 + (x >> 60) c
+//          only where a bound would pass 16 Q.  6 multiplies per butterfly instead of 10.
 // ---------------------------------------------------------------------------------------------
 struct Lazy64 {
+    static constexpr bool kPlanned = false;
     uint64_t Q, Q2;
     ulonglong2 lo, hi;  // (N^-1, pre), (w1 N^-1, pre)
     FHE_DEV static uint64_t csub(uint64_t x, uint64_t m) { return x >= m ? x - m : x; }
@@ -643,18 +650,114 @@ struct Lazy64 {
         y = x + Q2 - t;
         x = x + t;
     }
-    FHE_DEV void gs(uint64_t& x, uint64_t& y, ulonglong2 w) const {
+    FHE_DEV void gs(uint64_t& x, uint64_t& y, ulonglong2 w, int) const {
         const uint64_t d = x + Q2 - y;
         x = csub(x + y, Q2);
         y = lazy_mul(d, w);
     }
-    FHE_DEV void gs_last(uint64_t& x, uint64_t& y) const {
+    FHE_DEV void gs_last(uint64_t& x, uint64_t& y, int) const {
         const uint64_t d = x + Q2 - y;
         x = csub(lazy_mul(x + y, lo), Q);
         y = csub(lazy_mul(d, hi), Q);
     }
     FHE_DEV uint64_t fwd_out(uint64_t x) const { return csub(csub(x, Q2), Q); }
+    FHE_DEV uint64_t fold(uint64_t x) const { return x; }
 };
+
+struct Sol60 {
+    static constexpr bool kPlanned = true;
+    uint64_t Q;
+    uint32_t S;         // c = 2^S - 1
+    ulonglong2 lo, hi;  // (N^-1, pre), (w1 N^-1, pre)
+    // y w mod Q in [0, 4Q) for any y < 2^64 (w < Q, w.y = floor(w 2^64 / Q))
+    FHE_DEV uint64_t mul(uint64_t y, ulonglong2 w) const {
+        if (FHE_NTT_COPY) return y;
+        const uint32_t yl = (uint32_t)y, yh = (uint32_t)(y >> 32);
+        const uint32_t pl = (uint32_t)w.y, ph = (uint32_t)(w.y >> 32);
+        // y w' / 2^64 = yh ph + (yl ph + yh pl) / 2^32 + yl pl / 2^64: the high words of the middle
+        // products and yh ph; the dropped fractions are < 3
+        const uint64_t q = (uint64_t)yh * ph + __umulhi(yl, ph) + __umulhi(yh, pl);  // floor(y w' / 2^64) - {0, 1, 2}
+        const uint32_t wl = (uint32_t)w.x, wh = (uint32_t)(w.x >> 32);
+        const uint64_t p  = (uint64_t)yl * wl;
+        // y w - q Q = y w - (q << 60) + (q << S) - q  (mod 2^64; the true value is in [0, 4Q))
+        const uint32_t rh = (uint32_t)(p >> 32) + yl * wh + yh * wl - ((uint32_t)q << 28);
+        return ((((uint64_t)rh) << 32) | (uint32_t)p) + (q << S) - q;
+    }
+    // any x < 2^64 -> x mod 2^60 + (x >> 60) c < Q + 16 c < 2Q (bound 2 in the plan)
+    FHE_DEV uint64_t fold(uint64_t x) const {
+        const uint32_t k = (uint32_t)(x >> 60);
+        return (x & ((1ull << 60) - 1)) + (uint64_t)((k << S) - k);
+    }
+    FHE_DEV uint64_t canon(uint64_t x) const {
+        const uint64_t f = fold(x);
+        return f >= Q ? f - Q : f;
+    }
+    FHE_DEV void ct(uint64_t& x, uint64_t& y, ulonglong2 w) const {
+        const uint64_t t = mul(y, w);
+        y = x + 4 * Q - t;
+        x = x + t;
+    }
+    // k: the plan's bound of y (y < k Q), so x - y + k Q >= 0
+    FHE_DEV void gs(uint64_t& x, uint64_t& y, ulonglong2 w, int k) const {
+        const uint64_t d = x + (uint64_t)k * Q - y;
+        x = x + y;
+        y = mul(d, w);
+    }
+    FHE_DEV void gs_last(uint64_t& x, uint64_t& y, int k) const {
+        const uint64_t d = x + (uint64_t)k * Q - y;
+        x = canon(mul(x + y, lo));
+        y = canon(mul(d, hi));
+    }
+    FHE_DEV uint64_t fwd_out(uint64_t x) const { return canon(x); }
+};
+
+// Sol60's bound plan, per stage (execution order) and register: fold before the stage, and the
+// GS offset multiple.  Bounds are in units of Q (canonical 1, fold output 2, products 4); every value
+// stays below 16 Q.  In a layout every element of a register has the same bound; a transpose mixes
+// all registers (the maximum carries over).
+struct Plan64 {
+    bool fold[10][16];
+    int k[10][16];
+    bool fold_out[16];
+};
+// stage st's register bit and whether a transpose precedes it
+constexpr int kFwdBit[10] = {3, 2, 1, 0, 3, 2, 1, 0, 1, 0};   // A 9..6, B 5..2, C 1, 0
+constexpr int kInvBit[10] = {0, 1, 0, 1, 2, 3, 0, 1, 2, 3};   // C 0, 1, B 2..5, A 6..8, last
+constexpr Plan64 make_plan64(bool inv) {
+    Plan64 p{};
+    int B[16] = {};
+    for (int r = 0; r < 16; ++r) B[r] = 1;
+    for (int st = 0; st < 10; ++st) {
+        if ((!inv && (st == 4 || st == 8)) || (inv && (st == 2 || st == 6))) {
+            int U = 0;
+            for (int r = 0; r < 16; ++r) U = B[r] > U ? B[r] : U;
+            for (int r = 0; r < 16; ++r) B[r] = U;
+        }
+        const int bt = inv ? kInvBit[st] : kFwdBit[st];
+        for (int r = 0; r < 16; ++r) {
+            if (r & (1 << bt)) continue;
+            const int q = r | (1 << bt);
+            if (!inv) {            // CT: x' = x + t, y' = x + 4Q - t, t < 4Q
+                if (B[r] + 4 > 16) {
+                    p.fold[st][r] = true;
+                    B[r] = 2;
+                }
+                B[r] += 4;
+                B[q] = B[r];
+            } else {               // GS: x' = x + y, y' = (x + kQ - y) w < 4Q
+                while (B[r] + B[q] > 16) {
+                    const int e = B[r] >= B[q] ? r : q;
+                    p.fold[st][e] = true;
+                    B[e] = 2;
+                }
+                p.k[st][r] = B[q];
+                B[r] = st == 9 ? 1 : B[r] + B[q];
+                B[q] = st == 9 ? 1 : 4;
+            }
+        }
+    }
+    return p;
+}
 
 FHE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -664,21 +767,20 @@ FHE_DEV void wave_sync() {
 FHE_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
 FHE_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
 
-#ifndef FHE_NTT64_PF
-#define FHE_NTT64_PF 1   // k_ntt1024w64: the next polynomial's rows loaded during this one
-#endif
 #ifndef FHE_NTT64_WPS
 #define FHE_NTT64_WPS 4  // k_ntt1024w64: waves per SIMD (register budget and grid size)
 #endif
 
-template <bool INV>
+// PF: a persistent wave's next polynomial is loaded during the current one (batches larger than
+// the resident grid); without it a wave holds one polynomial's registers (no spills)
+template <bool INV, class M, bool PF>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NTT64_WPS)))
     k_ntt1024w64(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
-                 const ulonglong2* __restrict__ tab, Lazy64 m) {
+                 const ulonglong2* __restrict__ tab, M m) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ulonglong2* s_tw = reinterpret_cast<ulonglong2*>(smem);                            // 1024 entries
     uint32_t* tiles  = reinterpret_cast<uint32_t*>(smem + 1024 * sizeof(ulonglong2));  // 8 x kWTile
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) s_tw[i] = tab[i];
+    constexpr Plan64 P = make_plan64(INV);
 
     const int L    = threadIdx.x & 63;
     const int wv   = threadIdx.x >> 6;
@@ -686,7 +788,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
     const int G = L >> 2, j = L & 3;  // layout B lane fields
     const uint32_t W = gridDim.x * (blockDim.x >> 6);
     uint32_t poly    = blockIdx.x * (blockDim.x >> 6) + wv;
-    auto rowp        = [&](uint32_t p) -> uint32_t { return p < count ? p : count - 1; };
 
     // A (word address (r << 6) | L) <-> B ((G << 6) | (r << 2) | j), one 32-bit plane at a time
     auto a_to_b = [&](uint64_t (&v)[16]) {
@@ -764,11 +865,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
         for (int r = 0; r < 16; ++r) v[r] |= (uint64_t)tile[wt((G << 6) | (r << 2) | j)] << 32;
         wave_sync();
     };
+    // fold plan of stage st (Sol60)
+    auto plan = [&](uint64_t (&v)[16], int st) {
+        if (M::kPlanned) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (P.fold[st][r]) v[r] = m.fold(v[r]);
+        }
+    };
     // Global I/O needs no third transpose: the forward transform reads rows in layout A and writes
     // layout C (4 consecutive u64 per lane and x9x8: 32-byte runs), the inverse reads C and writes A
     using Raw = uint64_t[16];
     auto load = [&](Raw& buf, uint32_t p) {
-        const uint64_t* src = in + (size_t)rowp(p) * 1024;
+        const uint64_t* src = in + (size_t)p * 1024;
         if (!INV) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) buf[r] = src[(r << 6) + L];
@@ -782,12 +891,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
         }
     };
     auto step = [&](Raw& v, uint32_t p) {
-        uint64_t* dst = out + (size_t)rowp(p) * 1024;
+        uint64_t* dst = out + (size_t)p * 1024;
         if (!INV) {
             // A: stages 9..6 (uniform twiddles)
 #pragma unroll
             for (int b = 9; b >= 6; --b) {
                 const int rb = b - 6;
+                plan(v, 9 - b);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     if (r & (1 << rb)) continue;
@@ -798,6 +908,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
 #pragma unroll
             for (int b = 5; b >= 2; --b) {
                 const int rb = b - 2;
+                plan(v, 9 - b);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     if (r & (1 << rb)) continue;
@@ -805,11 +916,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
                 }
             }
             b_to_c(v);
+            plan(v, 8);
 #pragma unroll
             for (int hh = 0; hh < 4; ++hh) {
                 const ulonglong2 w1 = s_tw[256 + (hh << 6) + L];
                 m.ct(v[4 * hh], v[4 * hh + 2], w1);
                 m.ct(v[4 * hh + 1], v[4 * hh + 3], w1);
+            }
+            plan(v, 9);
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
                 m.ct(v[4 * hh], v[4 * hh + 1], s_tw[512 + (hh << 7) + (L << 1)]);
                 m.ct(v[4 * hh + 2], v[4 * hh + 3], s_tw[512 + (hh << 7) + (L << 1) + 1]);
             }
@@ -821,57 +937,68 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
                     ulonglong2{m.fwd_out(v[4 * hh + 2]), m.fwd_out(v[4 * hh + 3])};
             }
         } else {
+            plan(v, 0);
 #pragma unroll
             for (int hh = 0; hh < 4; ++hh) {
-                m.gs(v[4 * hh], v[4 * hh + 1], s_tw[512 + (hh << 7) + (L << 1)]);
-                m.gs(v[4 * hh + 2], v[4 * hh + 3], s_tw[512 + (hh << 7) + (L << 1) + 1]);
+                m.gs(v[4 * hh], v[4 * hh + 1], s_tw[512 + (hh << 7) + (L << 1)], P.k[0][0]);
+                m.gs(v[4 * hh + 2], v[4 * hh + 3], s_tw[512 + (hh << 7) + (L << 1) + 1], P.k[0][2]);
+            }
+            plan(v, 1);
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
                 const ulonglong2 w1 = s_tw[256 + (hh << 6) + L];
-                m.gs(v[4 * hh], v[4 * hh + 2], w1);
-                m.gs(v[4 * hh + 1], v[4 * hh + 3], w1);
+                m.gs(v[4 * hh], v[4 * hh + 2], w1, P.k[1][0]);
+                m.gs(v[4 * hh + 1], v[4 * hh + 3], w1, P.k[1][1]);
             }
             c_to_b(v);
 #pragma unroll
             for (int b = 2; b <= 5; ++b) {
                 const int rb = b - 2;
+                plan(v, b);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     if (r & (1 << rb)) continue;
-                    m.gs(v[r], v[r | (1 << rb)], s_tw[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))]);
+                    m.gs(v[r], v[r | (1 << rb)], s_tw[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))], P.k[b][r]);
                 }
             }
             b_to_a(v);
 #pragma unroll
             for (int b = 6; b <= 8; ++b) {
                 const int rb = b - 6;
+                plan(v, b);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     if (r & (1 << rb)) continue;
-                    m.gs(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
+                    m.gs(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))], P.k[b][r]);
                 }
             }
+            plan(v, 9);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) m.gs_last(v[r], v[r | 8]);
+            for (int r = 0; r < 8; ++r) m.gs_last(v[r], v[r | 8], P.k[9][r]);
 #pragma unroll
             for (int r = 0; r < 16; ++r) dst[(r << 6) + L] = v[r];
         }
     };
+    // the first polynomial's rows are requested before the twiddle table is staged
+    Raw bufA;
+    if (poly < count) load(bufA, poly);
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) s_tw[i] = tab[i];
     __syncthreads();  // s_tw ready
-    if (!FHE_NTT64_PF) {
+    if (!PF) {
         for (; poly < count; poly += W) {
-            Raw v;
-            load(v, poly);
-            step(v, poly);
+            step(bufA, poly);
+            if (poly + W < count) load(bufA, poly + W);
         }
         return;
     }
-    Raw bufA, bufB;
-    if (poly < count) load(bufA, poly);
+    Raw bufB;
     for (; poly < count; poly += 2 * W) {
-        load(bufB, poly + W);
+        const bool more = poly + W < count;   // wave-uniform
+        if (more) load(bufB, poly + W);
         __builtin_amdgcn_sched_barrier(0);
         step(bufA, poly);
-        if (poly + W >= count) break;
-        load(bufA, poly + 2 * W);
+        if (!more) break;
+        if (poly + 2 * W < count) load(bufA, poly + 2 * W);
         __builtin_amdgcn_sched_barrier(0);
         step(bufB, poly + W);
     }
@@ -948,6 +1075,9 @@ static hipError_t launch_wave(const NttPlan& p, const uint64_t* in, uint64_t* ou
 #ifndef FHE_NTT64_WAVE
 #define FHE_NTT64_WAVE 1   // 64-bit path: one polynomial per wave (k_ntt1024w64)
 #endif
+#ifndef FHE_NTT64_SOL
+#define FHE_NTT64_SOL 1    // k_ntt1024w64: the Sol60 policy for Q = 2^60 - (2^S - 1)
+#endif
 static hipError_t launch_wave64(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                                 hipStream_t s) {
     if (count == 0) return hipSuccess;
@@ -956,10 +1086,20 @@ static hipError_t launch_wave64(const NttPlan& p, const uint64_t* in, uint64_t* 
     const uint32_t groups = (count + 7) / 8;
     const uint32_t cap    = (uint32_t)p.cus * 4 * FHE_NTT64_WPS / 8;
     dim3 grid(groups < cap ? groups : cap), block(512);
-    Lazy64 m{p.Q, 2 * p.Q, ulonglong2{p.ninv, p.ninv_pre}, ulonglong2{p.w1ninv, p.w1ninv_pre}};
     const ulonglong2* tab = reinterpret_cast<const ulonglong2*>(inverse ? p.d_tab_inv : p.d_tab_fwd);
-    if (inverse) hipLaunchKernelGGL((k_ntt1024w64<true>), grid, block, sm, s, in, out, count, tab, m);
-    else hipLaunchKernelGGL((k_ntt1024w64<false>), grid, block, sm, s, in, out, count, tab, m);
+    const ulonglong2 lo{p.ninv, p.ninv_pre}, hi{p.w1ninv, p.w1ninv_pre};
+    const bool pf = count > grid.x * 8u;   // more polynomials than resident waves
+#define FHE_NTT64_LAUNCH(MT, PF_)                                                                              \
+    if (inverse) hipLaunchKernelGGL((k_ntt1024w64<true, MT, PF_>), grid, block, sm, s, in, out, count, tab, m); \
+    else hipLaunchKernelGGL((k_ntt1024w64<false, MT, PF_>), grid, block, sm, s, in, out, count, tab, m)
+    if (FHE_NTT64_SOL && p.sol_shift) {
+        const Sol60 m{p.Q, p.sol_shift, lo, hi};
+        if (pf) { FHE_NTT64_LAUNCH(Sol60, true); } else { FHE_NTT64_LAUNCH(Sol60, false); }
+    } else {
+        const Lazy64 m{p.Q, 2 * p.Q, lo, hi};
+        if (pf) { FHE_NTT64_LAUNCH(Lazy64, true); } else { FHE_NTT64_LAUNCH(Lazy64, false); }
+    }
+#undef FHE_NTT64_LAUNCH
     return hipGetLastError();
 }
 

@@ -59,6 +59,8 @@ hipError_t ntt_plan_init(NttPlan& p, uint64_t Q, uint64_t psi, uint32_t N, int d
         }
         p.ninv_pre = shoup64(p.ninv, Q);
         p.w1ninv_pre = shoup64(p.w1ninv, Q);
+        for (uint32_t S = 1; S < 20; ++S)
+            if (Q == (1ull << 60) - ((1ull << S) - 1)) p.sol_shift = S;
         if ((e = hipMalloc(&p.d_tab_fwd, f.size() * 8)) != hipSuccess) return e;
         if ((e = hipMalloc(&p.d_tab_inv, iv.size() * 8)) != hipSuccess) return e;
         if ((e = hipMemcpy(p.d_tab_fwd, f.data(), f.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return e;

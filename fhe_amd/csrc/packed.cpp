@@ -121,7 +121,7 @@ const uint64_t* unpack_bsk(const Params& p, const uint8_t* data, size_t size, si
 }
 
 std::vector<uint8_t> pack_ksk(const Params& p, const uint64_t* A, const uint64_t* B) {
-    const size_t rows = p.ksk_rows();
+    const size_t rows = p.ksk_rows_all();
     std::vector<uint8_t> out(sizeof(PackedKskHdr) + rows * ((size_t)p.n + 1) * 8);
     PackedKskHdr h{};
     h.h = header(PT_KSK, out.size(), rows, 0);
@@ -129,6 +129,7 @@ std::vector<uint8_t> pack_ksk(const Params& p, const uint64_t* A, const uint64_t
     h.output_n = p.n;
     h.decomp_levels = p.digitsKS;
     h.decomp_base_log = log2u(p.baseKS);
+    h.reserved[0] = p.baseKS;   // the base itself (not a power of two for TOY / SIGNED_MOD_TEST / STD256Q_3)
     h.Q = p.qKS;
     memcpy(out.data(), &h, sizeof(h));
     memcpy(out.data() + sizeof(h), A, rows * p.n * 8);
@@ -139,9 +140,10 @@ std::vector<uint8_t> pack_ksk(const Params& p, const uint64_t* A, const uint64_t
 void unpack_ksk(const Params& p, const uint8_t* data, size_t size, const uint64_t** A, const uint64_t** B) {
     check_header(data, size, PT_KSK, sizeof(PackedKskHdr));
     const auto* h = reinterpret_cast<const PackedKskHdr*>(data);
-    const size_t rows = p.ksk_rows();
+    const size_t rows = p.ksk_rows_all();
     if (h->input_n != p.N || h->output_n != p.n || h->decomp_levels != p.digitsKS ||
-        (1u << h->decomp_base_log) != p.baseKS || h->Q != p.qKS)
+        h->decomp_base_log != log2u(p.baseKS) || h->reserved[0] != p.baseKS || h->Q != p.qKS ||
+        h->h.element_count != rows)
         throw std::invalid_argument("packed switching key does not match the context's parameters");
     if (size < sizeof(PackedKskHdr) + rows * ((size_t)p.n + 1) * 8) throw std::invalid_argument("packed switching key: truncated");
     *A = reinterpret_cast<const uint64_t*>(data + sizeof(PackedKskHdr));

@@ -11,9 +11,10 @@
 //                           decomp_base_log = log2 baseG, key_size = bytes of key data,
 //                           key_layout = KEY_LAYOUT_NTT; then the raw u64 key (include/fhe_hip.h).
 //   SWITCHING_KEY (6):      64-byte block (input_n = N, output_n = n, decomp_levels = digitsKS,
-//                           decomp_base_log = log2 baseKS, Q = qKS); then A [N][baseKS][digitsKS][n]
-//                           and B [N][baseKS][digitsKS] u64 (the reference's packer is a TODO,
-//                           packed.cpp:313-328).
+//                           decomp_base_log = floor(log2 baseKS), reserved[0] = baseKS, Q = qKS,
+//                           header.element_count = rows); then A [N][baseKS][digitsKS][n] and
+//                           B [N][baseKS][digitsKS] u64 (timeOptimization: the map's three keys, A
+//                           then B) (the reference's packer is a TODO, packed.cpp:313-328).
 #pragma once
 #include <stddef.h>
 #include <stdint.h>

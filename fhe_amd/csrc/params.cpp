@@ -28,6 +28,13 @@ size_t Params::bsk_offset(uint32_t bg) const {
     throw std::invalid_argument("no bootstrapping key for this baseG");
 }
 
+size_t Params::ksk_index(uint32_t bg) const {
+    if (!timeopt) return 0;
+    for (size_t k = 0; k < 3; ++k)
+        if (kSignBases[k] == bg) return k;
+    throw std::invalid_argument("no switching key for this baseG");
+}
+
 Params Params::with_base(uint32_t bg) const {
     Params p = *this;
     p.baseG = bg;

@@ -50,7 +50,13 @@ struct Params {
     size_t bsk_offset(uint32_t bg) const;    // timeopt: first word of the key for baseG bg
     // RingGSWCryptoParams::Change_BaseG (rgsw-cryptoparameters.h:222-229): baseG, digitsG, Gpow
     Params with_base(uint32_t bg) const;
-    size_t ksk_rows() const { return (size_t)N * baseKS * digitsKS; }
+    size_t ksk_rows() const { return (size_t)N * baseKS * digitsKS; }   // rows of one switching key
+    // timeOptimization: BTKeyGen's map holds one whole key per base (binfhecontext.cpp:292-296 calls
+    // KeyGen per base: its own RLWE secret and switching key); the raw layouts concatenate the three
+    // switching keys (A rows then B per key array, kSignBases order)
+    size_t ksk_keys() const { return timeopt ? 3 : 1; }
+    size_t ksk_rows_all() const { return ksk_rows() * ksk_keys(); }
+    size_t ksk_index(uint32_t bg) const;   // timeopt: which of the map's switching keys baseG bg uses
     uint64_t gate_const(int gate) const;  // rgsw-cryptoparameters.cpp:78-92
 };
 

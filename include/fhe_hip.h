@@ -86,8 +86,11 @@ void* fhe_hip_ntt_plan_stream(fhe_hip_ntt_plan* plan);
 typedef struct fhe_hip_ctx fhe_hip_ctx;
 
 typedef struct {
-    uint32_t paramset, method, n, N, q, baseKS, digitsKS, baseG, digitsG, numAutoKeys, keyDist, reserved;
-    uint64_t Q, psi, qKS, bsk_words, ksk_rows;
+    uint32_t paramset, method, n, N, q, baseKS, digitsKS, baseG, digitsG, numAutoKeys, keyDist;
+    uint32_t kernel;  /* the accumulator kernels the set runs on: 1 = 32-bit, one wave per gate (N = 1024,
+                         Q < 2^28, digitsG = 3); 2 = 32-bit split, two waves per gate (digitsG = 4, N = 1024,
+                         Q < 2^27); 0 = 64-bit accumulator (every other set, the large-precision family) */
+    uint64_t Q, psi, qKS, bsk_words, ksk_rows;  /* ksk_rows: of the raw layout (timeOptimization: 3 keys) */
 } fhe_hip_params;
 /* The large-precision family GenerateBinFHEContext(set, arbFunc, logQ, N, GINX, false)
  * (binfhecontext.cpp:55-104: Q = LastPrime(54, 2N), N = 2048, qKS = 2^35, n = 1305 (TOY: 32),
@@ -251,9 +254,11 @@ int fhe_hip_external_product_batch_device(fhe_hip_ctx* ctx, size_t count, const 
 /* Backend::MaxBatchSize (backend.h:86): gates one call can take given the device's free memory */
 int fhe_hip_max_batch_size(fhe_hip_ctx* ctx, size_t* max_count);
 /* Backend::UnpackBootstrappingKey (backend.h:229-233): packed keys (fhe_hip_pack_keys) back to the
- * raw layouts; either key may be skipped (NULL) */
+ * raw layouts; either key may be skipped (NULL); *_cap = the output buffers' sizes in u64 words
+ * (FHE_HIP_ERR_INVALID_PARAM when too small) */
 int fhe_hip_unpack_keys(int paramset, int method, const uint8_t* bsk_packed, size_t bsk_size, uint64_t* bsk,
-                        const uint8_t* ksk_packed, size_t ksk_size, uint64_t* kskA, uint64_t* kskB);
+                        size_t bsk_cap, const uint8_t* ksk_packed, size_t ksk_size, uint64_t* kskA, size_t kskA_cap,
+                        uint64_t* kskB, size_t kskB_cap);
 
 /* LWEEncryptionScheme::KeySwitch (lwe-pke.cpp:348-372): (N, qKS) -> (n, qKS) */
 int fhe_hip_keyswitch_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,

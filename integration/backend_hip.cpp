@@ -426,7 +426,8 @@ void BackendHIP::UnpackBootstrappingKey(const DeviceBuffer& packed, RingGSWACCKe
     std::vector<uint8_t> bytes(packed.size);
     Check(fhe_hip_copy_to_host(bytes.data(), packed.ptr, packed.size), "CopyToHost");
     std::vector<uint64_t> raw(p_.bsk_words);
-    Check(fhe_hip_unpack_keys(set_, method_, bytes.data(), bytes.size(), raw.data(), nullptr, 0, nullptr, nullptr),
+    Check(fhe_hip_unpack_keys(set_, method_, bytes.data(), bytes.size(), raw.data(), raw.size(), nullptr, 0, nullptr, 0,
+                              nullptr, 0),
           "UnpackBootstrappingKey");
     // rebuild with the key's own layout (rgsw-acc-cggi.cpp:39-57, rgsw-acc-lmkcdey.cpp:39-68,
     // rgsw-acc-dm.cpp:39-58); ring parameters from a context of the same set

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REF_SO = os.path.join(ROOT, "oracle", "_ref", "libfhe_ref.so")
+# FHE_REF_SO: a private copy of the reference library (long golden regenerations, tools/regen_goldens.sh)
+REF_SO = os.environ.get("FHE_REF_SO") or os.path.join(ROOT, "oracle", "_ref", "libfhe_ref.so")
 RESTATE_SO = os.path.join(ROOT, "oracle", "_ref", "libtfhe_oracle.so")
 # the reference + our BackendHIP (integration/backend_hip.cpp) registered in its BackendRegistry
 BACKEND_SO = os.path.join(ROOT, "oracle", "_ref", "libbackend_hip.so")
@@ -145,6 +146,8 @@ class Ref:
             (self.n, self.N, self.q, self.Q, self.qKS, self.baseKS, self.digitsKS, self.baseG,
              self.digitsG, self.psi, self.numAutoKeys, self.keyDist) = [int(x) for x in info]
             self.method_is_ginx = method == GINX
+            # timeOptimization (paramset code bit 14, logQ != 11): three switching keys in the raw layout
+            self.ksk_keys = 3 if (paramset & (1 << 30) and paramset & (1 << 14) and (paramset & 0xff) != 11) else 1
 
     def err(self):
         return self.L.ref_last_error().decode()
@@ -174,7 +177,7 @@ class Ref:
     def keygen(self):
         sk = np.zeros(self.n, np.uint64)
         bsk = np.zeros(self.bsk_len(), np.uint64)
-        rows = self.N * self.baseKS * self.digitsKS
+        rows = self.N * self.baseKS * self.digitsKS * self.ksk_keys
         A = np.zeros(rows * self.n, np.uint64)
         B = np.zeros(rows, np.uint64)
         self._chk(self.L.ref_keygen(self.h, _p(sk), _p(bsk), _p(A), _p(B)))

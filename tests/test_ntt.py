@@ -130,10 +130,12 @@ def test_gpu_ntt_empty_and_bad_params():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Q", [1073707009, 2147473409])
+@pytest.mark.parametrize("Q", [1073707009, 2147473409, 1152921504606830593, 4611686018427322369])
 def test_gpu_ntt_lazy_bound_moduli(Q, restatement):
     """moduli at the edge of the 32-bit lazy path (4Q < 2^32 needs Q < 2^30; larger Q
-    takes the 64-bit path), with all-(Q-1) rows as the worst case for lazy bounds."""
+    takes the 64-bit path), the 60-bit poly-benchmark prime 2^60 - 2^14 + 1 (the Sol60 butterflies:
+    values grow to just below 16 Q between planned folds) and a 62-bit prime (Lazy64), with
+    all-(Q-1) rows as the worst case for lazy bounds."""
     from fhe_amd import NttPlan
     plan = NttPlan(Q)
     rng = np.random.default_rng(17)
@@ -147,13 +149,13 @@ def test_gpu_ntt_lazy_bound_moduli(Q, restatement):
 
 
 @pytest.mark.gpu
-def test_gpu_ntt_multi_iteration_out_of_place(restatement):
+@pytest.mark.parametrize("Q", [134215681, 1152921504606830593])
+def test_gpu_ntt_multi_iteration_out_of_place(restatement, Q):
     """a batch larger than the persistent grid (every wave loops, odd tail pair),
     out-of-place on device buffers == in-place host path; sampled rows vs the oracle."""
     import ctypes
     from fhe_amd import NttPlan
     from fhe_amd._lib import check, lib, ptr, vp
-    Q = 134215681
     plan = NttPlan(Q)
     count = 20001
     rng = np.random.default_rng(23)

@@ -84,3 +84,23 @@ def test_gpu_gates_from_reference_packed_batches(flags):
         out = e.eval_gate_packed(int(gate), pack(a1[sl], b1[sl], flags), pack(a2[sl], b2[sl], flags), flags)
         oa, ob = ref_unpack_lwe_batch(out, 503, pg) if ref_available() else bf.unpack_lwe_batch(out)
         assert np.array_equal(oa, g["out_a"][sl]) and np.array_equal(ob, g["out_b"][sl]), int(gate)
+
+
+@pytest.mark.parametrize("ps,m", [(0, 2), (19, 2), (43, 2), (3, 2), (21, 3)])
+def test_packed_keys_roundtrip(ps, m):
+    """pack / unpack of the keys for sets with a non-power-of-two baseKS (TOY 25, STD256Q_3 21,
+    SIGNED_MOD_TEST 25) and the STD128 sets; a short output buffer is refused"""
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import FheHipError
+    keys = bf.keygen(ps, m, 0x9AC0 + ps)
+    pb, pk = bf.pack_keys(ps, m, keys)
+    back = bf.unpack_keys(ps, m, pb, pk)
+    assert np.array_equal(back.bsk, keys.bsk)
+    assert np.array_equal(back.kskA, keys.kskA) and np.array_equal(back.kskB, keys.kskB)
+    import ctypes
+    short = np.zeros(len(keys.kskB) - 1, np.uint64)
+    A = np.zeros_like(keys.kskA)
+    with pytest.raises(FheHipError):
+        bf.check(bf.L().fhe_hip_unpack_keys(ps, m, None, 0, None, 0, pk.ctypes.data_as(ctypes.c_void_p), pk.size,
+                                            A.ctypes.data_as(ctypes.c_void_p), A.size,
+                                            short.ctypes.data_as(ctypes.c_void_p), short.size))

@@ -3,6 +3,6 @@
 m=$1; b=$2; shift 2
 for round in 1 2; do
   for v in "$@"; do
-    echo -n "$v r$round: "; FHE_AMD_LIB=build/variants/$v.so timeout -k 10 120 python tools/gate_time.py $m $b 2>&1 | grep "B=" || exit 1
+    echo -n "$v r$round: "; FHE_AMD_LIB=abv/$v.so timeout -k 10 120 python tools/gate_time.py $m $b 2>&1 | grep "B=" || exit 1
   done
 done

@@ -12,6 +12,7 @@ from fhe_amd import binfhe as bf  # noqa: E402
 from fhe_amd._lib import check, lib, ptr, vp  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+NTT = not (len(sys.argv) > 2 and sys.argv[2] == "nontt")   # "nontt": the gate batches only
 
 
 def dalloc(x):
@@ -35,7 +36,7 @@ for ps, m in ((bf.STD128, bf.GINX), (bf.STD128_LMKCDEY, bf.LMKCDEY)):
     check(lib().fhe_hip_synchronize(0))
     e.close()
 
-for Q in (134215681, 1152921504606830593):
+for Q in ((134215681, 1152921504606830593) if NTT else ()):
     plan = NttPlan(Q)
     xs = np.random.default_rng(2).integers(0, Q, size=(4096, 1024), dtype=np.uint64)
     dx = dalloc(xs)

@@ -1,0 +1,3 @@
+set -o pipefail
+bash tools/r03_b.sh || exit 1
+bash tools/r03_a.sh || exit 1
