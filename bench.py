@@ -32,6 +32,7 @@ gate prep + blind rotation (k_blind_rotate_ginx), then key switch + ModSwitch
                       outputs for the same 65,536 gates (tests/golden/full_*.npz).
 """
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -74,7 +75,7 @@ def parse():
     ap.add_argument("--no-lmkcdey", action="store_true", help="skip the config-5 sub-object")
     ap.add_argument("--no-config3", action="store_true")
     ap.add_argument("--ntt-count", type=int, default=4096)
-    ap.add_argument("--cpu-sample", type=int, default=2048, help="gates in the all-cores CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=8192, help="gates in the all-cores CPU sample (BASELINE.md 2)")
     ap.add_argument("--cpu-sample-1core", type=int, default=24, help="gates in the 1-core CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core available to this job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -333,6 +334,7 @@ def main():
         }
     if rank == 0 and world == 1:
         result["ntt_roofline"] = ntt_rooflines(NttPlan, torch, dev, stream, args.ntt_count)
+        result["copy_bw"] = copy_bandwidth(torch, dev, stream, args.ntt_count)
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(main_r, args)
@@ -398,6 +400,26 @@ def ntt_rooflines(NttPlan, torch, dev, stream, count, reps=20):
     return out
 
 
+def copy_bandwidth(torch, dev, stream, count, reps=50):
+    """measured device copy bandwidth (record it next to the 8 TB/s vendor peak): torch's
+    copy of the bytes of one 4096-polynomial NTT pass (32 MiB read + 32 MiB written), on the bench stream"""
+    x = torch.empty(count * 1024, dtype=torch.int64, device=dev)
+    y = torch.empty_like(x)
+    with torch.cuda.stream(stream):
+        for _ in range(5):
+            y.copy_(x)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            y.copy_(x)
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) / reps * 1e3
+    gbs = 2 * x.numel() * 8 / (us * 1e-6) / 1e9
+    return {"bytes_per_copy": 2 * x.numel() * 8, "us": round(us, 3), "GBs": round(gbs, 1),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4), "method": "torch copy_ on the bench stream, 50 reps"}
+
+
 def host_info():
     """CPU facts of this host: the whole machine and what this job may use."""
     info = {"nproc": os.cpu_count()}
@@ -439,7 +461,7 @@ def cpu_baseline(r, args):
     a1, b1, a2, b2 = r["inputs"]
     ao, bo = r["out"]
     label = "GINX" if method == 2 else "LMKCDEY"
-    S_all = min(args.cpu_sample if method == 2 else args.cpu_sample // 2, len(b1))
+    S_all = min(args.cpu_sample, len(b1))
     S_one = min(args.cpu_sample_1core if method == 2 else max(1, args.cpu_sample_1core * 2 // 3), len(b1))
     if ref_available():
         ref = Ref(ps, method)
@@ -478,11 +500,19 @@ def cpu_baseline(r, args):
         # NTT on one core, 60-bit and STD128 moduli; config 2 CPU cost = 4096 x that
         ntt = {}
         rng = np.random.default_rng(0x5EED0001)
+        ref.L.ref_ntt_batch_bench.restype = ctypes.c_double
+        ref.L.ref_ntt_batch_bench.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.c_int]
         for nm, Q in (("q60", 1152921504606830593), ("std128", 134215681)):
             x = rng.integers(0, Q, size=1024, dtype=np.uint64)
             ns = ref.L.ref_ntt_bench(Q, 1024, x.ctypes.data, 20000)
+            xb = rng.integers(0, Q, size=(4096, 1024), dtype=np.uint64)
+            ref.L.ref_ntt_batch_bench(Q, 1024, xb.ctypes.data, 4096, threads)   # warm-up
+            nsb = min(ref.L.ref_ntt_batch_bench(Q, 1024, xb.ctypes.data, 4096, threads) for _ in range(3))
             ntt[nm] = {"Q": Q, "us_per_ntt_1core": round(ns / 1e3, 3),
-                       "config2_us_4096_1core": round(ns * 4096 / 1e3, 1)}
+                       "config2_us_4096_1core": round(ns * 4096 / 1e3, 1),
+                       "config2_us_4096_all_cores": round(nsb / 1e3, 1), "all_cores_threads": threads,
+                       "config2_GBs_all_cores": round(4096 * NTT_BYTES_PER_POLY / (nsb * 1e-9) / 1e9, 2)}
         out["ntt_config1"] = ntt
     return out
 

@@ -34,30 +34,18 @@ struct BootTables {
     uint32_t nR;     // N (Montgomery): undoes the N^-1 scaling when the accumulator is written out
 };
 
-// Digit exchange between the half-waves in the external products: 1 = ds_bpermute of the other
-// half's digits, with the key rows of half 1 stored swapped in pairs (row d at position d ^ 1) so
-// that every lane multiplies (own, other) digits in the same order; 0 = v_permlane32_swap (both
-// digit orders in every lane, plain row order).  Engine::load_bsk and the device key generator
-// write the layout this selects.
-#ifndef FHE_XCHG
-#define FHE_XCHG 1
-#endif
-constexpr bool kBskHalfSwap = FHE_XCHG != 0;
+// Digit exchange between the half-waves in the external products: ds_bpermute of the other half's
+// digits, with the key rows of half 1 stored swapped in pairs (row d at position d ^ 1) so that every
+// lane multiplies (own, other) digits in the same order.  Engine::load_bsk and the device key
+// generator write this layout.
+constexpr bool kBskHalfSwap = true;
 // GINX: the two ternary keys of an index (BSK+ / BSK-) interleaved per lane as one 16-byte
 // vector (K+[2k], K+[2k+1], K-[2k], K-[2k+1]) per digit row and slot pair: one load per digit
-#ifndef FHE_GINX_U4
-#define FHE_GINX_U4 1
-#endif
-constexpr bool kGinxU4 = FHE_GINX_U4 != 0;
+constexpr bool kGinxU4 = true;
 // op-list methods (LMKCDEY, AP/DM, automorphism keys): the 4 slots l*32 + 4kk .. +3 of a lane as
 // one 16-byte vector per row; word offset within a key of (row d, slot pair k = 0..15, lane, e)
-#ifndef FHE_ROW_U4
-#define FHE_ROW_U4 1
-#endif
-constexpr bool kRowU4 = FHE_ROW_U4 != 0;
 __host__ __device__ constexpr size_t row_off(uint32_t d, uint32_t k, uint32_t lane, uint32_t e) {
-    return kRowU4 ? (((size_t)d * 8 + (k >> 1)) * 64 + lane) * 4 + (k & 1) * 2 + e
-                  : (((size_t)d * 16 + k) * 64 + lane) * 2 + e;
+    return (((size_t)d * 8 + (k >> 1)) * 64 + lane) * 4 + (k & 1) * 2 + e;
 }
 // word offset, within index i's 2 * dG2 * 2N words, of (sign ks, row d, slot pair k, lane, e)
 __host__ __device__ constexpr size_t ginx_u4_off(uint32_t ks, uint32_t d, uint32_t k, uint32_t lane, uint32_t e) {

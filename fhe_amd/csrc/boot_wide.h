@@ -1,4 +1,6 @@
-// boot_wide.h -- the large-precision parameter family on the device (bootstrap_wide.hip):
+// boot_wide.h -- the wide accumulator (bootstrap_wide.hip): the large-precision parameter family, and
+// every parameter set outside the 32-bit register-resident kernels (A32 policy below Q < 2^30).
+// The large-precision family:
 // GenerateBinFHEContext(set, arbFunc, logQ, N, GINX, false) (binfhecontext.cpp:55-104) with a
 // 54-bit accumulator modulus Q (27-bit for logQ = 11), N = 2048 (1024), qKS = 2^35, n = 1305.
 // The accumulator works in 64-bit residues: Shoup products for the NTT twiddles, 128-bit digit x
@@ -22,6 +24,12 @@ struct WideTables {
     uint64_t Q, qinv;       // qinv = -Q^-1 mod 2^64
     uint64_t ninv, ninvS;   // N^-1 and its Shoup quotient
     uint64_t oneM;          // 2^64 mod Q
+    uint64_t r2;            // 2^128 mod Q (keys into Montgomery form)
+    // narrow = 1: the 32-bit policy (Q < 2^30, digitsG2 Q < 2^32): the same tables one word wide,
+    // Shoup quotients floor(w 2^32 / Q), Montgomery R = 2^32, and every key array in u32 words
+    uint32_t narrow;
+    const uint32_t *tab32, *tabS32, *tabI32, *tabIS32, *psiM32;
+    uint32_t Q32, qinv32, ninv32, ninvS32, oneM32, r2_32;
 };
 
 // one bootstrap launch: the blind rotation of GINX (rgsw-acc-cggi.cpp:59-151) over the monomial
@@ -43,19 +51,18 @@ struct WideArgs {
     uint32_t acc_tv;
 };
 
-hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
+// bsk: [n][2][dG2][2][N] Montgomery keys, u64 words (u32 with t.narrow)
+hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
-// LMKCDEY / DM on the 64-bit accumulator: the op lists of launch_prep_lmk / launch_prep_dm
+// LMKCDEY / DM on the wide accumulator: the op lists of launch_prep_lmk / launch_prep_dm
 // (k_blind_rotate_wide_ops); bsk = the EXT keys [keys][digitsG2][2][N], autok = [numAutoKeys +
-// 1][digitsG - 1][2][N], Montgomery form
-hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, const uint64_t* bsk,
-                                        const uint64_t* autok, const uint16_t* ops, const uint32_t* nops,
-                                        uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
-                                        bool dm, hipStream_t s);
-// ExternalProduct seam: raw RGSW words (< Q) -> the Montgomery form of the op-list kernel's keys;
-// R2 = 2^128 mod Q, qinv = -Q^-1 mod 2^64 (WideTables::qinv)
-hipError_t launch_pack_rgsw_wide(const uint64_t* raw, size_t words, uint64_t Q, uint64_t qinv, uint64_t R2, uint64_t* out,
-                                 hipStream_t s);
+// 1][digitsG - 1][2][N], Montgomery form (u64, or u32 with t.narrow)
+hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, const void* bsk, const void* autok,
+                                        const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                        uint64_t* ext_a, uint64_t* ext_b, bool dm, hipStream_t s);
+// ExternalProduct seam: raw RGSW words (< Q) -> the Montgomery form of the op-list kernel's keys
+// (u64 words, u32 with t.narrow)
+hipError_t launch_pack_rgsw_wide(const uint64_t* raw, size_t words, const WideTables& t, void* out, hipStream_t s);
 // KeySwitch (lwe-pke.cpp:348-372) mod qKS = 2^k with u64 rows A [rows][n], B [rows], then
 // ModSwitch(qKS -> q_out) (q_out = 0: none); ms_a [count][N], ms_b [count] mod qKS
 hipError_t launch_keyswitch_wide(size_t count, uint32_t n, uint32_t N, uint32_t baseKS, uint32_t digitsKS, uint64_t qKS,

@@ -25,23 +25,8 @@
 #include "arith.h"
 #include "boot.h"
 
-#ifndef FHE_BF_GROUP
-#define FHE_BF_GROUP 0   // >0: sched_barrier after every FHE_BF_GROUP butterflies (bounds live temps)
-#endif
 #ifndef FHE_KEY_PF
 #define FHE_KEY_PF 2     // key chunks (2 slots each) requested ahead of use in the CMUX loop
-#endif
-#ifndef FHE_MAC_PIPE
-#define FHE_MAC_PIPE 1   // GINX: digit exchange and monomial reads one slot pair ahead
-#endif
-#ifndef FHE_TW_PRE
-#define FHE_TW_PRE 1     // GINX: per-lane twiddles of a pass's B' stages requested together at its start
-#endif
-#ifndef FHE_FWD_FUSED
-#define FHE_FWD_FUSED 1
-#endif
-#ifndef FHE_FWD_SHARED
-#define FHE_FWD_SHARED 0
 #endif
 #ifndef FHE_WAVES_PER_EU
 #define FHE_WAVES_PER_EU 2
@@ -50,14 +35,6 @@
 namespace fhe_amd {
 
 namespace {
-
-FHE_DEV void bf_fence(int idx) {
-#if FHE_BF_GROUP > 0
-    if ((idx + 1) % FHE_BF_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
-#else
-    (void)idx;
-#endif
-}
 
 constexpr int kTile = 32 * 33;  // one half-wave transpose tile (u32 words)
 constexpr int kAccBoundLZ = 28; // GINX, Q < 2^27: |acc| < 2.8 Q between iterations (units of Q/10)
@@ -101,50 +78,17 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
     y          = s - t;
     x          = x + t;
 }
-// v_mad_i64_i32 (a * b + c, 32 x 32 -> 64 signed), emitted explicitly: written as C the compiler
-// sometimes widens a hoisted -Q into a 64-bit constant and expands the product into 5 instructions
-// 2: plain C, with -Q re-materialised inside each loop body (fresh_nq) so that instruction
-// selection sees a sign-extended 32-bit operand; inline asm makes the hazard recognizer put an
-// s_nop after every such instruction (600 per iteration)
-#ifndef FHE_ASM_MAD
-#define FHE_ASM_MAD 2
-#endif
-#ifndef FHE_MAC_NEW
-#define FHE_MAC_NEW 1   // LZ: one reduction per slot, acc folded in (signed acc)
-#endif
-#ifndef FHE_INV_S
-#define FHE_INV_S 1     // LZ: signed inverse NTT
-#endif
 #ifndef FHE_DM_WAVES
 #define FHE_DM_WAVES 3   // waves per SIMD of the AP/DM op-list kernel
-#endif
-#ifndef FHE_LMK_TWPRE
-#define FHE_LMK_TWPRE 1  // LMKCDEY: per-lane B' twiddles requested together (FHE_TW_PRE)
-#endif
-#ifndef FHE_LMK_PIPE
-#define FHE_LMK_PIPE 1   // LMKCDEY: digit exchange one 4-slot group ahead of the external product
-#endif
-#ifndef FHE_AUTO_WIDE
-#define FHE_AUTO_WIDE 1  // LMKCDEY automorphism: acc0' inverse-transformed across the whole wave
 #endif
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
-#ifndef FHE_LMK_L2PF
-#define FHE_LMK_L2PF 0   // LMKCDEY: dwords per lane of the next op's key lines touched ahead (8 KB of lines per wave each)
-#endif
-#ifndef FHE_LMK_K0EARLY
-#define FHE_LMK_K0EARLY 0  // LMKCDEY: the op's first key vectors requested before its inverse pass
-#endif
+// v_mad_i64_i32 (a * b + c, 32 x 32 -> 64 signed) in plain C, with -Q re-materialised inside each
+// loop body (fresh_nq) so that instruction selection sees a sign-extended 32-bit operand (hoisted,
+// the compiler widens -Q into a 64-bit constant and the product becomes 5 instructions)
 FHE_DEV int64_t mad_i64_i32(int32_t a, int32_t b, int64_t c) {
-#if FHE_ASM_MAD == 1
-    int64_t d;
-    uint64_t junk;
-    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(junk) : "v"(a), "v"(b), "v"(c));
-    return d;
-#else
     return (int64_t)a * b + c;
-#endif
 }
 // signed Montgomery (the Q < 2^27 path): a read as int32, bR < Q -> (a b 2^-32 mod Q) in (-Q, Q)
 // for any |a| < 2^31: |a bR - mm Q| < 2^31 Q + 2^31 Q
@@ -160,9 +104,7 @@ FHE_DEV uint32_t smont_red(int64_t t, const Mod& m) {
 }
 // -Q as a value defined inside the current loop body (an empty asm the optimizer cannot hoist)
 FHE_DEV Mod fresh_nq(Mod m) {
-#if FHE_ASM_MAD == 2
     asm volatile("" : "+s"(m.nQ));
-#endif
     return m;
 }
 // signed Cooley-Tukey: |x|, |y| < B in, < B + Q out, two adds and no offset
@@ -179,30 +121,14 @@ FHE_DEV void gs_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
     y          = mont_mul(d, wR, m);
 }
 
-// intra-wave LDS hand-off: orders the compiler's LDS accesses; the LDS
-// executes one wave's DS instructions in issue order.
-#ifndef FHE_LDS_SYNC
-#define FHE_LDS_SYNC 0
-#endif
+// intra-wave LDS hand-off: orders this wave's LDS accesses around a layout change
 FHE_DEV void wave_lds_sync() {
-#if FHE_LDS_SYNC == 0
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#else
-    // one wave's DS instructions are executed by the LDS in issue order, so a
-    // read issued after a write (or a write after a read) of the same tile by
-    // the same wave is ordered without waiting for completion; only the
-    // compiler must not move LDS accesses across this point.
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-#endif
 }
 
 FHE_DEV void transpose32(uint32_t (&v)[32], uint32_t* tile, int l) {
-#if defined(FHE_ABL) && (FHE_ABL & 4)
-    return;  // ablation: no transposes
-#endif
 #pragma unroll
     for (int r = 0; r < 32; ++r) tile[l * 33 + r] = v[r];
     wave_lds_sync();
@@ -234,7 +160,6 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             if (r & (1 << rb)) continue;
             const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
             ct_bf(v[r], v[r | (1 << rb)], w, m);
-            bf_fence(r);
         }
     }
 #pragma unroll
@@ -245,13 +170,8 @@ FHE_DEV void fwd_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << b)) continue;
-#if defined(FHE_ABL) && (FHE_ABL & 8)
-            const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;  // ablation: no per-lane twiddle reads
-#else
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
-#endif
             ct_bf(v[r], v[r | (1 << b)], w, m);
-            bf_fence(r);
         }
     }
 }
@@ -306,11 +226,7 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << b)) continue;
-#if defined(FHE_ABL) && (FHE_ABL & 8)
-            const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;
-#else
             const uint32_t w = TWB(b, r >> (b + 1));
-#endif
             if (LZ) {
                 ct_bf_s(v[r], v[r | (1 << b)], w, m);
                 ct_bf_s(u[r], u[r | (1 << b)], w, m);
@@ -359,13 +275,8 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             if (r & (1 << b)) continue;
-#if defined(FHE_ABL) && (FHE_ABL & 8)
-            const uint32_t w = (uint32_t)(b * 977 + r) ^ (uint32_t)l;
-#else
             const uint32_t w = s_twB[twb_off(b) + (r >> (b + 1)) * 32 + l];
-#endif
             gs_bf(v[r], v[r | (1 << b)], w, m);
-            bf_fence(r);
         }
     }
     transpose32(v, tile, l);
@@ -377,7 +288,6 @@ FHE_DEV void inv_pass(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t* 
             if (r & (1 << rb)) continue;
             const uint32_t w = twA[(1 << (9 - b)) + (r >> (rb + 1))];
             gs_bf(v[r], v[r | (1 << rb)], w, m);
-            bf_fence(r);
         }
     }
     // bit 9 (transformnat-impl.h:599-623); its N^-1 factor is already in the data
@@ -512,13 +422,7 @@ FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
 // the same register of the other half-wave (lane ^ 32), through the LDS crossbar (no VALU)
 FHE_DEV uint32_t other_half(uint32_t x, int xaddr) { return (uint32_t)__builtin_amdgcn_ds_bpermute(xaddr, (int)x); }
 
-// key vector load; FHE_ABL & 64 (timing ablation, wrong results): every key index folded to key 0,
-// the same instructions always hitting in cache, to measure what key cache misses cost
-#if defined(FHE_ABL) && (FHE_ABL & 64)
-#define FHE_KEY_INDEX(x) ((x) * 0)
-#else
-#define FHE_KEY_INDEX(x) (x)
-#endif
+// key vector load
 FHE_DEV uint4 kload(const uint4* p, size_t i) { return p[i]; }
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 
@@ -619,7 +523,7 @@ __global__ void k_prep_ginx(GateInputs in, GateArgs g, uint16_t* __restrict__ id
 constexpr int kWaves = 4;
 // LZ: the monomial table holds (plain, Montgomery) pairs
 constexpr size_t boot_lds(bool full, bool lz) {
-    return (size_t)(992 * 2 + (lz && FHE_MAC_NEW ? 2 : 1) * (full ? kMonoTableWords : kMonoHalfWords) + kWaves * 2 * kTile) * 4;
+    return (size_t)(992 * 2 + (lz ? 2 : 1) * (full ? kMonoTableWords : kMonoHalfWords) + kWaves * 2 * kTile) * 4;
 }
 
 // MFULL: full-resolution monomial table (ciphertext modulus 2N, any exponent); otherwise the
@@ -642,7 +546,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     constexpr int mwords = mfull ? kMonoTableWords : kMonoHalfWords;
     uint32_t* s_mono = sm + 1984;
     uint2* s_mono2   = reinterpret_cast<uint2*>(sm + 1984);  // LZ: (plain, Montgomery) pairs
-    uint32_t* s_tile = sm + 1984 + (LZ && FHE_MAC_NEW ? 2 : 1) * mwords;
+    uint32_t* s_tile = sm + 1984 + (LZ ? 2 : 1) * mwords;
     for (int i = threadIdx.x; i < 992; i += 256) {
         s_twBf[i] = T.twB_fwd[i];
         s_twBi[i] = T.twB_inv[i];
@@ -651,7 +555,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         const uint32_t* src = mfull ? T.mono_full : T.mono;
         const uint32_t* srp = mfull ? T.monoP_full : T.monoP;
         for (int i = threadIdx.x; i < mwords; i += 256) {
-            if (LZ && FHE_MAC_NEW) s_mono2[i] = make_uint2(srp[i], src[i]);
+            if (LZ) s_mono2[i] = make_uint2(srp[i], src[i]);
             else s_mono[i] = src[i];
         }
     }
@@ -698,46 +602,19 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     const int xaddr      = (lane ^ 32) << 2;
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m = fresh_nq(m0);
-        // wave-uniform base + per-lane 32-bit offset: saddr loads with immediate offsets
-        const uint2* kb = bsk + (size_t)i * (2 * 4 * 16 * 64);
-#define ki (kb + lofs)
-        uint2 kbuf[FHE_KEY_PF + 1][8];
         const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
         uint32_t dA[32], dB[32];
         // --- iNTT of a copy of acc -> canonical COEF (AddToAccCGGI :104-106)
 #pragma unroll
         for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-#if defined(FHE_ABL) && (FHE_ABL & 16)
-        if (0)  // ablation: no inverse pass
-#endif
-        if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20, true, FHE_TW_PRE != 0>(dA, tile, l, twAi, s_twBi, T.w1R, T.oneR, m);
+        if (LZ) inv_pass_s<kAccBoundLZ, true, true>(dA, tile, l, twAi, s_twBi, T.w1R, T.oneR, m);
         else inv_pass(dA, tile, l, T.twA_inv, s_twBi, T.w1R, m);
         // --- SignedDigitDecompose (rgsw-acc.cpp:54-91): drop the lowest signed digit,
         //     keep the next two.  Half h decomposes acc_h: dA = D_h, dB = D_{2+h}.
 #pragma unroll
         for (int r = 0; r < 32; ++r) decompose2<LZ>(dA[r], dec, dA[r], dB[r]);
         // --- NTT of the four digit polynomials (two per pass, one per half)
-#if defined(FHE_ABL) && (FHE_ABL & 32)
-        // ablation: no forward passes
-#elif FHE_FWD_FUSED
-        fwd_pass2<LZ ? 1 : 0, FHE_TW_PRE != 0>(dA, dB, tile, l, twAf, s_twBf, m);
-#elif FHE_FWD_SHARED
-        // one copy of the forward-pass code for both digit polynomials (instruction-cache
-        // footprint): transform dA, swap, transform (old dB), swap back
-#pragma clang loop unroll(disable)
-        for (int pass = 0; pass < 2; ++pass) {
-            fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
-#pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                const uint32_t t = dA[r];
-                dA[r]            = dB[r];
-                dB[r]            = t;
-            }
-        }
-#else
-        fwd_pass(dA, tile, l, T.twA_fwd, s_twBf, m);
-        fwd_pass(dB, tile, l, T.twA_fwd, s_twBf, m);
-#endif
+        fwd_pass2<LZ ? 1 : 0, true>(dA, dB, tile, l, twAf, s_twBf, m);
         // --- external product + CMUX, slot by slot.  Lane (h, l) owns slots
         //     l*32 + r of component h; its keys are 16-byte vectors (4 slots) laid
         //     out so that each load instruction reads 1 KiB contiguous.
@@ -751,15 +628,13 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         const uint32_t Pp = el + (el >> 5);                    // index el + 64k       -> Pp + 66k
         const uint32_t gl = eper - el;
         const uint32_t Pn = gl + (gl >> 5);                    // index eper - el - 64k -> Pn - 66k
-#if FHE_GINX_U4
         // one 16-byte vector per digit row and slot pair: (K+[2k], K+[2k+1], K-[2k], K-[2k+1])
-        const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)FHE_KEY_INDEX(i) * (4 * 16 * 64);
+        const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)i * (4 * 16 * 64);
         uint4 kq[FHE_KEY_PF + 1][4];
 #pragma unroll
         for (int k = 0; k < FHE_KEY_PF; ++k)
 #pragma unroll
             for (int d = 0; d < 4; ++d) kq[k][d] = kload(kb4, (d * 16 + k) * 64 + lofs);
-#if FHE_MAC_PIPE
         // the other half's digits (ds_bpermute) and the monomial pairs of slot pair k + 1 are
         // requested before slot pair k is consumed (LDS latency off the critical path)
         uint32_t xo[2][4];
@@ -781,73 +656,24 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
             }
         };
         issue(0, 0);
-#endif
 #pragma clang loop unroll(full)
         for (int k = 0; k < 16; ++k) {
             if (k + FHE_KEY_PF < 16) {
 #pragma unroll
                 for (int d = 0; d < 4; ++d) kq[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d] = kload(kb4, (d * 16 + k + FHE_KEY_PF) * 64 + lofs);
             }
-#if FHE_MAC_PIPE
             if (k + 1 < 16) issue(k + 1, (k + 1) & 1);
-#endif
             asm volatile("" ::: "memory");
 #define KP(d) make_uint2(kq[k % (FHE_KEY_PF + 1)][d].x, kq[k % (FHE_KEY_PF + 1)][d].y)
 #define KN(d) make_uint2(kq[k % (FHE_KEY_PF + 1)][d].z, kq[k % (FHE_KEY_PF + 1)][d].w)
-#else
-#if FHE_KEY_PF > 0
-#pragma unroll
-        for (int k = 0; k < FHE_KEY_PF; ++k)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                kbuf[k][d]     = ki[((0 * 4 + d) * 16 + k) * 64];
-                kbuf[k][4 + d] = ki[((1 * 4 + d) * 16 + k) * 64];
-            }
-#endif
-#pragma clang loop unroll(full)
-        for (int k = 0; k < 16; ++k) {
-            // software pipeline: chunk k+PF is requested while chunk k is consumed
-#if FHE_KEY_PF > 0
-            if (k + FHE_KEY_PF < 16) {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-#if defined(FHE_ABL) && (FHE_ABL & 1)
-                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d]     = make_uint2(d * 7 + k + i, lane);  // ablation: no key loads
-                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][4 + d] = make_uint2(d * 5 + k, lane + i);
-#else
-                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][d]     = ki[((0 * 4 + d) * 16 + k + FHE_KEY_PF) * 64];
-                    kbuf[(k + FHE_KEY_PF) % (FHE_KEY_PF + 1)][4 + d] = ki[((1 * 4 + d) * 16 + k + FHE_KEY_PF) * 64];
-#endif
-                }
-            }
-#else
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                kbuf[0][d]     = ki[((0 * 4 + d) * 16 + k) * 64];
-                kbuf[0][4 + d] = ki[((1 * 4 + d) * 16 + k) * 64];
-            }
-#endif
-            asm volatile("" ::: "memory");
-#define KP(d) kbuf[k % (FHE_KEY_PF + 1)][d]
-#define KN(d) kbuf[k % (FHE_KEY_PF + 1)][4 + (d)]
-#endif
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * k + e;
                 // all four digits in every lane: D0/D1 = digit A of acc0/acc1, D2/D3 = digit B
-#if FHE_MAC_PIPE && FHE_GINX_U4
                 const uint32_t D0 = dA[r], D1 = xo[k & 1][2 * e], D2 = dB[r], D3 = xo[k & 1][2 * e + 1];
-#elif FHE_XCHG
-                // (own, other) digit order; the half-1 key rows are stored swapped to match
-                const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
-#else
-                auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
-                const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
-#endif
                 // slot x = l*32 + r evaluates at psi^(2 brv(x) + 1), 2 brv(x) + 1 = 64 brv5(r) + 2 brv5(l) + 1
                 const uint32_t u  = __builtin_amdgcn_readfirstlane((as * (uint32_t)(__builtin_bitreverse32(r) >> 27)) & umask) * 66;
-                if (LZ && FHE_MAC_NEW) {
+                if (LZ) {
                     // S1, S2 = sum_d D_d K(+/-)_d unreduced (|.| < 40 Q^2 < 2^60, keys x 2^32); the monomial
                     // products S (X^m - 1) = lo(S) m + hi(S) (m 2^32) use the (plain, Montgomery) table pair,
                     // and acc is folded in as acc (2^32 mod Q): one signed Montgomery reduction per slot.
@@ -856,14 +682,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                                                            e ? KP(2).y : KP(2).x, e ? KP(3).y : KP(3).x, 0);
                     const int64_t S2 = (int64_t)mac4<true>(D0, D1, D2, D3, e ? KN(0).y : KN(0).x, e ? KN(1).y : KN(1).x,
                                                            e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, 0);
-#if defined(FHE_ABL) && (FHE_ABL & 2)
-                    const uint2 mp = make_uint2(Pp + u, Pp ^ u), mn = make_uint2(Pn - u, Pn ^ u);
-#elif FHE_MAC_PIPE && FHE_GINX_U4
                     const uint2 mp = mo[k & 1][e][0], mn = mo[k & 1][e][1];
-                    (void)u;
-#else
-                    const uint2 mp = s_mono2[Pp + u], mn = s_mono2[Pn - u];
-#endif
                     int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
                     S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
                     S += (int64_t)(int32_t)acc[r] * (int32_t)T.oneR;
@@ -874,11 +693,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
                     const uint64_t S2 = mac4<LZ>(D0, D1, D2, D3, e ? KN(0).y : KN(0).x, e ? KN(1).y : KN(1).x,
                                                  e ? KN(2).y : KN(2).x, e ? KN(3).y : KN(3).x, moff);
                     const uint32_t t1 = mont_red(S1, m), t2 = mont_red(S2, m);
-#if defined(FHE_ABL) && (FHE_ABL & 2)
-                    const uint64_t S  = (uint64_t)t1 * (Pp + u) + (uint64_t)t2 * (Pn - u);  // ablation: no monomial reads
-#else
                     const uint64_t S  = (uint64_t)t1 * s_mono[Pp + u] + (uint64_t)t2 * s_mono[Pn - u];
-#endif
                     // digits < 16Q (Q < 2^28): S1, S2 < 64 Q^2 -> t1, t2 < 5Q; S < 10Q^2 -> mont_red < 1.7Q;
                     // acc kept in [0, 2Q)
                     acc[r]            = csub(acc[r] + mont_red(S, m), m.Q2);
@@ -887,7 +702,6 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #undef KP
 #undef KN
         }
-#undef ki
     }
 
     if (ACCIO) {
@@ -897,7 +711,7 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     // --- extraction (binfhe-base-scheme.cpp:110-121): acc0 <- Transpose(acc0) (automorphism
     // 2N-1), both to COEF; ctExt = (acc0 coefficients, (Q>>3)+1 + acc1[0]); then ModSwitch to qKS.
     // In COEF, Transpose maps coefficient k to -a_(N-k) (k >= 1), a_0 to itself.
-    if (LZ && FHE_INV_S) inv_pass_s<FHE_MAC_NEW ? kAccBoundLZ : 20>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
+    if (LZ) inv_pass_s<kAccBoundLZ>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, T.oneR, m);
     else inv_pass(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m);
     wave_lds_sync();
     if (h == 0) {
@@ -1105,72 +919,30 @@ FHE_DEV void inv_wave_s(uint32_t (&v)[16], uint32_t* tile, int L, const uint32_t
         v[r | 8]         = min(d, d + m.Q);
     }
 }
-#ifndef FHE_AUTO_EXPORD
-#define FHE_AUTO_EXPORD 1  // automorphism_wide: regions in exponent order (3 VALU per gathered slot)
-#endif
 // automorphism X -> X^k of both components (as automorphism_eval: every half-wave gets its own
 // component back in layout B'), plus acc0' gathered into layout C for inv_wave_s
 FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* region, const uint32_t* region0,
                                int l, int L, uint32_t k) {
-    if (FHE_AUTO_EXPORD) {
-        // slot s = (l << 5) | r is stored at its exponent index brv10(s) = brv5(r) << 5 | brv5(l)
-        // (EVAL slot s holds the value at psi^(2 brv10(s) + 1)); the slot that reads exponent
-        // index t' gathers index ((2 t' + 1) k mod 2N) >> 1: one add, one bit-field extract, one
-        // address add per value
-        // FHE_AUTO_EXPORD 2: index t at t + 2 (t >> 6) (< kTile), which spreads the layout-C
-        // gather's lanes (t = 4 b k + c over 64 lanes b) over all banks
-        auto at = [](uint32_t t) -> uint32_t { return FHE_AUTO_EXPORD == 2 ? t + ((t >> 6) << 1) : t; };
-        static_assert(1023 + 2 * 15 < kTile, "padded region fits the tile");
-        const uint32_t bl = __builtin_bitreverse32((uint32_t)l) >> 27;
+    // slot s = (l << 5) | r is stored at its exponent index brv10(s) = brv5(r) << 5 | brv5(l)
+    // (EVAL slot s holds the value at psi^(2 brv10(s) + 1)); the slot that reads exponent
+    // index t' gathers index ((2 t' + 1) k mod 2N) >> 1: one add, one bit-field extract, one
+    // address add per value
+    const uint32_t bl = __builtin_bitreverse32((uint32_t)l) >> 27;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) region[at(((__builtin_bitreverse32((uint32_t)r) >> 27) << 5) | bl)] = v[r];
-        wave_lds_sync();
-        const uint32_t cl = (2 * bl + 1) * k;
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
-#if defined(FHE_ABL) && (FHE_ABL & 256)
-            v[r] = region[(uint32_t)r * 32 + l];   // ablation (wrong results): linear reads
-            (void)cl; (void)sr;
-#else
-            v[r]              = region[at(((cl + sr) >> 1) & 1023)];
-#endif
-        }
-        const uint32_t cL = (((__builtin_bitreverse32((uint32_t)L) >> 26) << 3) + 1) * k;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t H = (uint32_t)r >> 2, j = (uint32_t)r & 3;
-            const uint32_t su = ((((j & 1) << 1 | j >> 1) << 9) + (((H & 1) << 1 | H >> 1) << 1)) * k;  // uniform
-#if defined(FHE_ABL) && (FHE_ABL & 512)
-            a0[r] = region0[(uint32_t)r * 64 + L];   // ablation (wrong results): linear reads
-            (void)cL; (void)su;
-#else
-            a0[r]             = region0[at(((cL + su) >> 1) & 1023)];
-#endif
-        }
-        wave_lds_sync();
-        return;
-    }
-#pragma unroll
-    for (int r = 0; r < 32; ++r) region[l * 33 + r] = v[r];
+    for (int r = 0; r < 32; ++r) region[(((__builtin_bitreverse32((uint32_t)r) >> 27) << 5) | bl)] = v[r];
     wave_lds_sync();
-    const uint32_t cl = (2 * (__builtin_bitreverse32((uint32_t)l) >> 27) + 1) * k;
+    const uint32_t cl = (2 * bl + 1) * k;
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
         const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
-        const uint32_t t  = ((cl + sr) & 2047) >> 1;
-        const uint32_t sx = __builtin_bitreverse32(t) >> 22;
-        v[r]              = region[sx + (sx >> 5)];
+        v[r]              = region[(((cl + sr) >> 1) & 1023)];
     }
-    // layout C: x = (H << 8) | (L << 2) | j, 2 brv10(x) + 1 = brv2(j) << 9 | brv6(L) << 3 | brv2(H) << 1 | 1
     const uint32_t cL = (((__builtin_bitreverse32((uint32_t)L) >> 26) << 3) + 1) * k;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t H = (uint32_t)r >> 2, j = (uint32_t)r & 3;
         const uint32_t su = ((((j & 1) << 1 | j >> 1) << 9) + (((H & 1) << 1 | H >> 1) << 1)) * k;  // uniform
-        const uint32_t t  = ((cL + su) & 2047) >> 1;
-        const uint32_t sx = __builtin_bitreverse32(t) >> 22;
-        a0[r]             = region0[sx + (sx >> 5)];
+        a0[r]             = region0[(((cL + su) >> 1) & 1023)];
     }
     wave_lds_sync();
 }
@@ -1195,7 +967,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         s_twBi[i] = T.twB_inv[i];
     }
     uint32_t* s_tabI = s_tile + kWaves * 2 * kTile;  // FHE_AUTO_WIDE: TableI (1024 words)
-    if (!DM && FHE_AUTO_WIDE)
+    if (!DM)
         for (int i = threadIdx.x; i < 1024; i += 256) s_tabI[i] = T.tabI[i];
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
@@ -1250,47 +1022,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         const uint32_t* twAi = T.twA_inv;
         asm volatile("" : "+s"(twAf), "+s"(twAi));
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
-#if FHE_LMK_L2PF
-        // the next op's key rows, one dword per 128-byte line in consumption order, pulled into L2
-        // while this op's transforms run; the values are retired (not used) at the end of the op
-        uint32_t pf[FHE_LMK_L2PF];
-        {
-            const uint32_t nx = __builtin_amdgcn_readfirstlane((uint32_t)gops[it + 1 < cnt ? it + 1 : it]);
-            const bool ext    = DM || !(nx & 0x8000u);
-            const uint32_t* base = ext ? reinterpret_cast<const uint32_t*>(bsk) + (size_t)nx * (4 * 8 * 64 * 4)
-                                       : reinterpret_cast<const uint32_t*>(autok) + (size_t)(nx & 0x7fffu) * (2 * 8 * 64 * 4);
-#pragma unroll
-            for (int j = 0; j < FHE_LMK_L2PF; ++j) {
-                const uint32_t Ln  = (uint32_t)(j * 64 + lane);
-                const uint32_t off = ext ? ((((Ln >> 3) & 3) * 8 + (Ln >> 5)) << 8) + ((Ln & 7) << 5)
-                                         : (((((Ln >> 3) & 1) * 8 + ((Ln >> 4) & 7)) << 8) + ((Ln & 7) << 5));
-                pf[j] = base[off];
-            }
-        }
-#endif
         uint32_t dA[32], dB[32];
         if (DM || !(op & 0x8000u)) {
             // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
-#if FHE_ROW_U4
-            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)FHE_KEY_INDEX(op) * (4 * 8 * 64);
+            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)op * (4 * 8 * 64);
             uint4 kq[2][4];
-            if (FHE_LMK_K0EARLY)
-#pragma unroll
-                for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
-#endif
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass_s<20, LZ, !DM && FHE_LMK_TWPRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
+            inv_pass_s<20, LZ, !DM>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
-            fwd_pass2<FM, !DM && FHE_LMK_TWPRE>(dA, dB, tile, l, twAf, s_twBf, m);
-#if FHE_ROW_U4
+            fwd_pass2<FM, !DM>(dA, dB, tile, l, twAf, s_twBf, m);
             // one 16-byte vector per digit row and 4 slots (boot.h row_off)
-            if (!FHE_LMK_K0EARLY)
 #pragma unroll
-                for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
+            for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
             // LMKCDEY: the other half's digits of slots 4(kk+1).. requested before 4kk.. are consumed
-            constexpr bool PIPE = !DM && FHE_LMK_PIPE;
+            constexpr bool PIPE = !DM;
             uint32_t xq[2][8];
             auto issue = [&](int kk, int b) {
 #pragma unroll
@@ -1312,15 +1059,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 for (int e = 0; e < 4; ++e) {
                     const int r = 4 * kk + e;
 #define KC(d) (e == 0 ? kq[kk & 1][d].x : e == 1 ? kq[kk & 1][d].y : e == 2 ? kq[kk & 1][d].z : kq[kk & 1][d].w)
-#if FHE_XCHG
                     const uint32_t D0 = dA[r], D2 = dB[r];
                     const uint32_t D1 = PIPE ? xq[kk & 1][2 * e] : other_half(dA[r], xaddr);
                     const uint32_t D3 = PIPE ? xq[kk & 1][2 * e + 1] : other_half(dB[r], xaddr);
-#else
-                    auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                    auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
-                    const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
-#endif
                     // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28): |S| < 40 Q^2 or 24 Q^2, so
                     // |S| 2^-32 + Q/2 < 2Q
                     const int64_t S = (int64_t)mac4<true>(D0, D1, D2, D3, KC(0), KC(1), KC(2), KC(3), 0);
@@ -1328,38 +1069,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #undef KC
                 }
             }
-#else
-            const uint2* kb = bsk + (size_t)op * (4 * 16 * 64);
-            uint2 kk[2][4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) kk[0][d] = kb[(d * 16 + 0) * 64 + lane];
-#pragma clang loop unroll(full)
-            for (int k = 0; k < 16; ++k) {
-                if (k + 1 < 16) {  // request chunk k+1 while chunk k is consumed
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) kk[(k + 1) & 1][d] = kb[(d * 16 + k + 1) * 64 + lane];
-                }
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int r = 2 * k + e;
-#if FHE_XCHG
-                    const uint32_t D0 = dA[r], D1 = other_half(dA[r], xaddr), D2 = dB[r], D3 = other_half(dB[r], xaddr);
-#else
-                    auto p01 = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                    auto p23 = __builtin_amdgcn_permlane32_swap(dB[r], dB[r], false, false);
-                    const uint32_t D0 = p01[0], D1 = p01[1], D2 = p23[0], D3 = p23[1];
-#endif
-                    // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28): |S| < 40 Q^2 or 24 Q^2, so
-                    // |S| 2^-32 + Q/2 < 2Q
-                    const int64_t S = (int64_t)mac4<true>(D0, D1, D2, D3, e ? kk[k & 1][0].y : kk[k & 1][0].x,
-                                                          e ? kk[k & 1][1].y : kk[k & 1][1].x,
-                                                          e ? kk[k & 1][2].y : kk[k & 1][2].x,
-                                                          e ? kk[k & 1][3].y : kk[k & 1][3].x, 0);
-                    acc[r] = smont_red(S, m);
-                }
-            }
-#endif
         } else {
             // ---- Automorphism(5^t or 2N-5, autokey[t])
             const uint32_t t = op & 0x7fffu;
@@ -1369,7 +1078,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
             }
             asm volatile("" : "+s"(kexp));  // no reuse of the prologue's (2N - 5) index math (spills)
-#if FHE_AUTO_WIDE
             {
                 // acc0' across the wave: layout C -> canonical COEF layout A (16 per lane), its two
                 // digits scattered into the two tiles in A' order (digit A for half 0, B for half 1)
@@ -1389,22 +1097,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 for (int r = 0; r < 32; ++r) dA[r] = tile[l * 33 + r];
                 wave_lds_sync();
             }
-#else
-            automorphism_eval(acc, tile, l, kexp);  // both halves: acc0', acc1'
-#pragma unroll
-            for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass_s<20, LZ, FHE_LMK_TWPRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);  // half 0: COEF acc0'
-#pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                decompose2<true>(dA[r], dec, dA[r], dB[r]);
-                // (half 0's digit A, half 0's digit B) -> lower / upper half of dA
-                auto sw = __builtin_amdgcn_permlane32_swap(dA[r], dB[r], false, false);
-                dA[r]   = sw[0];
-            }
-#endif
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
-#if FHE_ROW_U4
-            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)FHE_KEY_INDEX(t) * (2 * 8 * 64);
+            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
             uint4 ka[2][2];
             ka[0][0] = kload(kb4, (0 * 8 + 0) * 64 + lane);
             ka[0][1] = kload(kb4, (1 * 8 + 0) * 64 + lane);
@@ -1413,25 +1107,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #pragma unroll
                 for (int e = 0; e < 4; ++e) xa[b][e] = other_half(dA[4 * kk + e], xaddr);
             };
-            if (FHE_LMK_PIPE) issue(0, 0);
+            issue(0, 0);
 #pragma clang loop unroll(full)
             for (int kk = 0; kk < 8; ++kk) {
                 if (kk + 1 < 8) {
                     ka[(kk + 1) & 1][0] = kload(kb4, (0 * 8 + kk + 1) * 64 + lane);
                     ka[(kk + 1) & 1][1] = kload(kb4, (1 * 8 + kk + 1) * 64 + lane);
-                    if (FHE_LMK_PIPE) issue(kk + 1, (kk + 1) & 1);
+                    issue(kk + 1, (kk + 1) & 1);
                 }
                 asm volatile("" ::: "memory");
                 const uint4 k0 = ka[kk & 1][0], k1 = ka[kk & 1][1];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int r = 4 * kk + e;
-#if FHE_XCHG
-                    const uint32_t P0 = dA[r], P1 = FHE_LMK_PIPE ? xa[kk & 1][e] : other_half(dA[r], xaddr);
-#else
-                    auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                    const uint32_t P0 = p[0], P1 = p[1];
-#endif
+                    const uint32_t P0 = dA[r], P1 = xa[kk & 1][e];
                     const uint32_t c0 = e == 0 ? k0.x : e == 1 ? k0.y : e == 2 ? k0.z : k0.w;
                     const uint32_t c1 = e == 0 ? k1.x : e == 1 ? k1.y : e == 2 ? k1.z : k1.w;
                     // |S| < 2 (6Q) Q + 2Q Q -> |acc| < 14 Q^2 2^-32 + Q/2 < 2Q
@@ -1440,41 +1129,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                     acc[r] = smont_red(S, m);
                 }
             }
-#else
-            const uint2* kb = autok + (size_t)t * (2 * 16 * 64);
-            uint2 ka[2][2];
-            ka[0][0] = kb[(0 * 16 + 0) * 64 + lane];
-            ka[0][1] = kb[(1 * 16 + 0) * 64 + lane];
-#pragma clang loop unroll(full)
-            for (int k = 0; k < 16; ++k) {
-                if (k + 1 < 16) {
-                    ka[(k + 1) & 1][0] = kb[(0 * 16 + k + 1) * 64 + lane];
-                    ka[(k + 1) & 1][1] = kb[(1 * 16 + k + 1) * 64 + lane];
-                }
-                asm volatile("" ::: "memory");
-                const uint2 k0 = ka[k & 1][0], k1 = ka[k & 1][1];
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int r = 2 * k + e;
-#if FHE_XCHG
-                    const uint32_t P0 = dA[r], P1 = other_half(dA[r], xaddr);
-#else
-                    auto p = __builtin_amdgcn_permlane32_swap(dA[r], dA[r], false, false);
-                    const uint32_t P0 = p[0], P1 = p[1];
-#endif
-                    // |S| < 2 (6Q) Q + 2Q Q -> |acc| < 14 Q^2 2^-32 + Q/2 < 2Q
-                    int64_t S = (int64_t)(int32_t)P0 * (int32_t)(e ? k0.y : k0.x) +
-                                (int64_t)(int32_t)P1 * (int32_t)(e ? k1.y : k1.x);
-                    S += (int64_t)(int32_t)acc[r] * (int32_t)oneRh;
-                    acc[r] = smont_red(S, m);
-                }
-            }
-#endif
         }
-#if FHE_LMK_L2PF
-#pragma unroll
-        for (int j = 0; j < FHE_LMK_L2PF; ++j) asm volatile("" ::"v"(pf[j]));
-#endif
     }
     if (ACCIO) {
         acc_store(acc, g, gate, h, l, T.nR, m);
@@ -1695,7 +1350,7 @@ hipError_t launch_blind_rotate_lmk(const GateArgs& g, const BootTables& t, const
                                    uint32_t* ext_a, uint32_t* ext_b, bool dm, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
     const uint32_t blocks = (g.count + kWaves - 1) / kWaves;
-    const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile + (!dm && FHE_AUTO_WIDE ? 1024 : 0)) * 4;
+    const size_t lds      = (size_t)(992 * 2 + kWaves * 2 * kTile + (!dm ? 1024 : 0)) * 4;
     const uint2* k  = reinterpret_cast<const uint2*>(bsk);
     const uint2* ak = reinterpret_cast<const uint2*>(autok);
     const bool lz   = t.Q < (1u << 27);
@@ -2032,7 +1687,7 @@ __global__ void k_repack_ginx2(const uint32_t* __restrict__ src, uint32_t n, uin
 }
 
 bool ginx2_supported(const GateArgs& g, const BootTables& t) {
-    return t.Q < (1u << 27) && g.N == 1024 && g.ctmod < 2 * g.N && g.tv == nullptr && g.acc_io == nullptr && kGinxU4;
+    return t.Q < (1u << 27) && g.N == 1024 && g.ctmod < 2 * g.N && g.tv == nullptr && g.acc_io == nullptr;
 }
 
 hipError_t launch_repack_ginx2(const void* bsk, uint32_t n, void* bsk2, hipStream_t s) {
@@ -2313,20 +1968,10 @@ __global__ void k_pack_rgsw(const uint64_t* __restrict__ raw, uint32_t count, ui
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
         // t enumerates destination words of key g: (d, k, lane, e) in row_off order
         const uint64_t g = t / (8 * N), w = t % (8 * N);
-        uint32_t d, k, lane, e;
-        if (kRowU4) {   // (((d * 8 + k/2) * 64 + lane) * 4 + (k & 1) * 2 + e
-            const uint32_t q4 = (uint32_t)(w >> 2), sub = (uint32_t)(w & 3);
-            lane = q4 & 63;
-            const uint32_t dk = q4 >> 6;
-            d = dk >> 3;
-            k = ((dk & 7) << 1) | (sub >> 1);
-            e = sub & 1;
-        } else {
-            e = (uint32_t)(w & 1);
-            lane = (uint32_t)(w >> 1) & 63;
-            k = (uint32_t)(w >> 7) & 15;
-            d = (uint32_t)(w >> 11);
-        }
+        // (((d * 8 + k/2) * 64 + lane) * 4 + (k & 1) * 2 + e
+        const uint32_t q4 = (uint32_t)(w >> 2), sub = (uint32_t)(w & 3);
+        const uint32_t lane = q4 & 63, dk = q4 >> 6;
+        const uint32_t d = dk >> 3, k = ((dk & 7) << 1) | (sub >> 1), e = sub & 1;
         const uint32_t h = lane >> 5, l = lane & 31;
         const uint32_t row = kBskHalfSwap ? d ^ h : d;
         const uint64_t src = raw[g * 8 * N + ((uint64_t)row * 2 + h) * N + l * 32 + 2 * k + e];

@@ -14,6 +14,10 @@
 //   4. acc_c += S+_c (X^m - 1) + S-_c (X^-m - 1), the monomials EVAL(X^m) = psi^((2 brv(j)+1) m)
 //      from one 2N-entry power table.
 // Keys are read straight from HBM, coalesced (consecutive threads, consecutive slots).
+// Two arithmetic policies share the code: A64 (64-bit residues, any Q < 2^62) and A32 (32-bit residues
+// for Q < 2^30 with digitsG2 Q < 2^32: the N = 2048 STD256* / STD256Q* rows, SIGNED_MOD_TEST, TOY):
+// Shoup products x w - hi(x w') Q in one 32 x 32 multiply pair, digit x key sums in 64 bits, one
+// Montgomery (R = 2^32) reduction per sum -- a third of A64's multiplies and half its LDS words.
 #include "boot_wide.h"
 
 #include <algorithm>
@@ -21,6 +25,14 @@
 // waves per SIMD the blind-rotation kernel is compiled for (VGPR budget 512 / waves)
 #ifndef FHE_WIDE_WAVES
 #define FHE_WIDE_WAVES 4
+#endif
+// the A32 instantiations: the gate kernel at 4 (124 VGPRs; at 6 it spills 40 and runs 27% slower), the
+// op-list kernel at 6 (80 VGPRs: +8% on STD256_LMKCDEY / STD256Q_3_LMKCDEY, profiles/r03_bench_sets_narrow.txt)
+#ifndef FHE_WIDE32_WAVES
+#define FHE_WIDE32_WAVES 4
+#endif
+#ifndef FHE_WIDE32_OPS_WAVES
+#define FHE_WIDE32_OPS_WAVES 6
 #endif
 
 namespace fhe_amd {
@@ -32,28 +44,6 @@ struct U128 {
     uint64_t lo, hi;
 };
 
-WD void mac(U128& s, uint64_t a, uint64_t b) {
-    const uint64_t lo = a * b, hi = __umul64hi(a, b);
-    s.lo += lo;
-    s.hi += hi + (s.lo < lo ? 1 : 0);
-}
-// t < Q 2^64  ->  t 2^-64 mod Q in [0, Q)
-WD uint64_t redc(const U128& t, uint64_t Q, uint64_t qinv) {
-    const uint64_t u = t.lo * qinv;
-    const uint64_t r = t.hi + __umul64hi(u, Q) + (t.lo != 0 ? 1 : 0);
-    return r >= Q ? r - Q : r;
-}
-// x w mod Q for w < Q, ws = floor(w 2^64 / Q), any 64-bit x
-WD uint64_t mul_shoup(uint64_t x, uint64_t w, uint64_t ws, uint64_t Q) {
-    const uint64_t r = x * w - __umul64hi(x, ws) * Q;
-    return r >= Q ? r - Q : r;
-}
-WD uint64_t add_q(uint64_t a, uint64_t b, uint64_t Q) {
-    const uint64_t s = a + b;
-    return s >= Q ? s - Q : s;
-}
-WD uint64_t sub_q(uint64_t a, uint64_t b, uint64_t Q) { return a >= b ? a - b : a + Q - b; }
-
 // RoundqQ(v, q, Q) = floor(0.5 + double(v) double(q) / double(Q)) mod q (lwe-pke.cpp:41-46), in
 // IEEE double like the reference (no contraction: the product is divided before the add)
 WD uint64_t round_qQ(uint64_t v, uint64_t q, uint64_t Q) {
@@ -62,12 +52,103 @@ WD uint64_t round_qQ(uint64_t v, uint64_t q, uint64_t Q) {
     return (uint64_t)floor(0.5 + x) % q;
 }
 
+// 64-bit residues: Shoup products, 128-bit sums, Montgomery R = 2^64 (keys K 2^64 mod Q)
+struct A64 {
+    using T = uint64_t;
+    using S = U128;
+    static constexpr int kWaves = FHE_WIDE_WAVES, kOpsWaves = FHE_WIDE_WAVES;
+    const uint64_t *tab, *tabS, *tabI, *tabIS, *psiM;
+    uint64_t Q, qinv, ninv, ninvS, oneM;
+    WD explicit A64(const WideTables& t)
+        : tab(t.tab), tabS(t.tabS), tabI(t.tabI), tabIS(t.tabIS), psiM(t.psiM), Q(t.Q), qinv(t.qinv), ninv(t.ninv),
+          ninvS(t.ninvS), oneM(t.oneM) {}
+    WD static S zero() { return U128{0, 0}; }
+    WD static void mac(S& s, T a, T b) {
+        const uint64_t lo = a * b, hi = __umul64hi(a, b);
+        s.lo += lo;
+        s.hi += hi + (s.lo < lo ? 1 : 0);
+    }
+    // t < Q 2^64  ->  t 2^-64 mod Q in [0, Q)
+    WD T redc(const S& t) const {
+        const uint64_t u = t.lo * qinv;
+        const uint64_t r = t.hi + __umul64hi(u, Q) + (t.lo != 0 ? 1 : 0);
+        return r >= Q ? r - Q : r;
+    }
+    // x w mod Q for w < Q, ws = floor(w 2^64 / Q), any 64-bit x
+    WD T mul_shoup(T x, T w, T ws) const {
+        const uint64_t r = x * w - __umul64hi(x, ws) * Q;
+        return r >= Q ? r - Q : r;
+    }
+    WD T add(T a, T b) const {
+        const T s = a + b;
+        return s >= Q ? s - Q : s;
+    }
+    WD T sub(T a, T b) const { return a >= b ? a - b : a + Q - b; }
+    // butterflies on canonical values
+    WD void ct(T& x, T& y, T w, T ws) const {
+        const T V = mul_shoup(y, w, ws);
+        y = sub(x, V);
+        x = add(x, V);
+    }
+    WD void gs(T& x, T& y, T w, T ws) const {
+        const T U = x;
+        x = add(U, y);
+        y = mul_shoup(sub(U, y), w, ws);
+    }
+    WD T fwd_out(T x) const { return x; }
+};
+// 32-bit residues for Q < 2^30: the same operations one word wide (keys K 2^32 mod Q); the unreduced
+// digit x key sums stay below digitsG2 Q^2 < Q 2^32 (Engine checks digitsG2 Q < 2^32), so one
+// reduction lands in [0, 2Q)
+struct A32 {
+    using T = uint32_t;
+    using S = uint64_t;
+    static constexpr int kWaves = FHE_WIDE32_WAVES, kOpsWaves = FHE_WIDE32_OPS_WAVES;
+    const uint32_t *tab, *tabS, *tabI, *tabIS, *psiM;
+    uint32_t Q, qinv, ninv, ninvS, oneM;
+    WD explicit A32(const WideTables& t)
+        : tab(t.tab32), tabS(t.tabS32), tabI(t.tabI32), tabIS(t.tabIS32), psiM(t.psiM32), Q(t.Q32), qinv(t.qinv32),
+          ninv(t.ninv32), ninvS(t.ninvS32), oneM(t.oneM32) {}
+    WD static S zero() { return 0; }
+    WD static void mac(S& s, T a, T b) { s += (uint64_t)a * b; }
+    WD T redc(S t) const {
+        const uint32_t u = (uint32_t)t * qinv;
+        const uint32_t r = (uint32_t)((t + (uint64_t)u * Q) >> 32);
+        return r >= Q ? r - Q : r;
+    }
+    // x w mod Q for w < Q, ws = floor(w 2^32 / Q), any 32-bit x: x w - hi(x ws) Q in [0, 2Q)
+    WD T mul_shoup(T x, T w, T ws) const {
+        const uint32_t r = x * w - __umulhi(x, ws) * Q;
+        return r >= Q ? r - Q : r;
+    }
+    WD T add(T a, T b) const {
+        const T s = a + b;
+        return s >= Q ? s - Q : s;
+    }
+    WD T sub(T a, T b) const { return a >= b ? a - b : a + Q - b; }
+    // Harvey-lazy butterflies (4Q < 2^32): the forward transform keeps values in [0, 4Q) and ends
+    // canonical (fwd_out), the inverse keeps [0, 2Q) (its readers reduce through mul_shoup)
+    WD static T csub(T x, T m) { return x >= m ? x - m : x; }
+    WD T lazy_mul(T x, T w, T ws) const { return x * w - __umulhi(x, ws) * Q; }  // [0, 2Q)
+    WD void ct(T& x, T& y, T w, T ws) const {
+        const T X = csub(x, 2 * Q);
+        const T t = lazy_mul(y, w, ws);
+        y = X + 2 * Q - t;
+        x = X + t;
+    }
+    WD void gs(T& x, T& y, T w, T ws) const {
+        const T U = x;
+        x = csub(U + y, 2 * Q);
+        y = lazy_mul(U + 2 * Q - y, w, ws);
+    }
+    WD T fwd_out(T x) const { return csub(csub(x, 2 * Q), Q); }
+};
+
 // Merged Cooley-Tukey forward transform in place on NB polynomials at buf + p N (bit-reversed
 // output, ForwardTransformToBitReverseInPlace transformnat-impl.h:302-373); all threads, synced.
-template <int LOGN, int NB>
-WD void ntt_fwd(uint64_t* buf, const WideTables& tb) {
+template <int LOGN, int NB, class A>
+WD void ntt_fwd(typename A::T* buf, const A& a) {
     constexpr int N = 1 << LOGN, T = N / 4;
-    const uint64_t Q = tb.Q;
 #pragma unroll 1
     for (int s = 0; s < LOGN; ++s) {
         const int logt = LOGN - 1 - s, t = 1 << logt;
@@ -76,13 +157,17 @@ WD void ntt_fwd(uint64_t* buf, const WideTables& tb) {
             const int b = (int)threadIdx.x + T * k;
             const int i = b >> logt;
             const int j = (i << (logt + 1)) | (b & (t - 1));
-            const uint64_t w = tb.tab[(1 << s) + i], ws = tb.tabS[(1 << s) + i];
+            const auto w = a.tab[(1 << s) + i], ws = a.tabS[(1 << s) + i];
 #pragma unroll
             for (int p = 0; p < NB; ++p) {
-                const uint64_t U = buf[p * N + j];
-                const uint64_t V = mul_shoup(buf[p * N + j + t], w, ws, Q);
-                buf[p * N + j]     = add_q(U, V, Q);
-                buf[p * N + j + t] = sub_q(U, V, Q);
+                auto x = buf[p * N + j], y = buf[p * N + j + t];
+                a.ct(x, y, w, ws);
+                if (s == LOGN - 1) {
+                    x = a.fwd_out(x);
+                    y = a.fwd_out(y);
+                }
+                buf[p * N + j]     = x;
+                buf[p * N + j + t] = y;
             }
         }
         __syncthreads();
@@ -90,10 +175,9 @@ WD void ntt_fwd(uint64_t* buf, const WideTables& tb) {
 }
 // Gentleman-Sande inverse (InverseTransformFromBitReverseInPlace :511-624) WITHOUT the final
 // N^-1 scaling (the readers apply it)
-template <int LOGN, int NB>
-WD void ntt_inv(uint64_t* buf, const WideTables& tb) {
+template <int LOGN, int NB, class A>
+WD void ntt_inv(typename A::T* buf, const A& a) {
     constexpr int N = 1 << LOGN, T = N / 4;
-    const uint64_t Q = tb.Q;
 #pragma unroll 1
     for (int s = 0; s < LOGN; ++s) {
         const int logt = s, t = 1 << logt, m = N >> (s + 1);
@@ -102,12 +186,13 @@ WD void ntt_inv(uint64_t* buf, const WideTables& tb) {
             const int b = (int)threadIdx.x + T * k;
             const int i = b >> logt;
             const int j = (i << (logt + 1)) | (b & (t - 1));
-            const uint64_t w = tb.tabI[m + i], ws = tb.tabIS[m + i];
+            const auto w = a.tabI[m + i], ws = a.tabIS[m + i];
 #pragma unroll
             for (int p = 0; p < NB; ++p) {
-                const uint64_t U = buf[p * N + j], V = buf[p * N + j + t];
-                buf[p * N + j]     = add_q(U, V, Q);
-                buf[p * N + j + t] = mul_shoup(sub_q(U, V, Q), w, ws, Q);
+                auto x = buf[p * N + j], y = buf[p * N + j + t];
+                a.gs(x, y, w, ws);
+                buf[p * N + j]     = x;
+                buf[p * N + j + t] = y;
             }
         }
         __syncthreads();
@@ -116,35 +201,34 @@ WD void ntt_inv(uint64_t* buf, const WideTables& tb) {
 
 // Radix-4 passes of the same transforms: each thread takes whole 4-element units through two
 // stages between barriers (LOGN / 2 barriers instead of LOGN), an odd last stage radix-2.
-template <int LOGN, int NB>
-WD void ntt_fwd4(uint64_t* buf, const WideTables& tb) {
+template <int LOGN, int NB, class A>
+WD void ntt_fwd4(typename A::T* buf, const A& a) {
     constexpr int N = 1 << LOGN, T = N / 4;
-    const uint64_t Q = tb.Q;
     const int u = (int)threadIdx.x;  // one unit per thread per polynomial
 #pragma unroll 1
     for (int s = 0; s + 1 < LOGN; s += 2) {
         const int logt = LOGN - 1 - s, t = 1 << logt, th = t >> 1, m = 1 << s;
         const int i = u >> (logt - 1), k = u & (th - 1);
         const int j0 = (i << (logt + 1)) + k;
-        const uint64_t w = tb.tab[m + i], ws = tb.tabS[m + i];
-        const uint64_t w1 = tb.tab[2 * m + 2 * i], w1s = tb.tabS[2 * m + 2 * i];
-        const uint64_t w2 = tb.tab[2 * m + 2 * i + 1], w2s = tb.tabS[2 * m + 2 * i + 1];
+        const auto w = a.tab[m + i], ws = a.tabS[m + i];
+        const auto w1 = a.tab[2 * m + 2 * i], w1s = a.tabS[2 * m + 2 * i];
+        const auto w2 = a.tab[2 * m + 2 * i + 1], w2s = a.tabS[2 * m + 2 * i + 1];
+        const bool last = !(LOGN & 1) && s + 2 == LOGN;
 #pragma unroll
         for (int p = 0; p < NB; ++p) {
-            uint64_t* b = buf + p * N + j0;
-            uint64_t x0 = b[0], x1 = b[th], x2 = b[t], x3 = b[t + th];
-            uint64_t V = mul_shoup(x2, w, ws, Q);
-            x2 = sub_q(x0, V, Q);
-            x0 = add_q(x0, V, Q);
-            V = mul_shoup(x3, w, ws, Q);
-            x3 = sub_q(x1, V, Q);
-            x1 = add_q(x1, V, Q);
-            V = mul_shoup(x1, w1, w1s, Q);
-            b[0] = add_q(x0, V, Q);
-            b[th] = sub_q(x0, V, Q);
-            V = mul_shoup(x3, w2, w2s, Q);
-            b[t] = add_q(x2, V, Q);
-            b[t + th] = sub_q(x2, V, Q);
+            auto* b = buf + p * N + j0;
+            auto x0 = b[0], x1 = b[th], x2 = b[t], x3 = b[t + th];
+            a.ct(x0, x2, w, ws);
+            a.ct(x1, x3, w, ws);
+            a.ct(x0, x1, w1, w1s);
+            a.ct(x2, x3, w2, w2s);
+            if (last) {
+                x0 = a.fwd_out(x0); x1 = a.fwd_out(x1); x2 = a.fwd_out(x2); x3 = a.fwd_out(x3);
+            }
+            b[0] = x0;
+            b[th] = x1;
+            b[t] = x2;
+            b[t + th] = x3;
         }
         __syncthreads();
     }
@@ -152,55 +236,58 @@ WD void ntt_fwd4(uint64_t* buf, const WideTables& tb) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int bf = u + T * k;
-            const uint64_t w = tb.tab[N / 2 + bf], ws = tb.tabS[N / 2 + bf];
+            const auto w = a.tab[N / 2 + bf], ws = a.tabS[N / 2 + bf];
 #pragma unroll
             for (int p = 0; p < NB; ++p) {
-                uint64_t* b = buf + p * N + 2 * bf;
-                const uint64_t U = b[0], V = mul_shoup(b[1], w, ws, Q);
-                b[0] = add_q(U, V, Q);
-                b[1] = sub_q(U, V, Q);
+                auto* b = buf + p * N + 2 * bf;
+                auto x = b[0], y = b[1];
+                a.ct(x, y, w, ws);
+                b[0] = a.fwd_out(x);
+                b[1] = a.fwd_out(y);
             }
         }
         __syncthreads();
     }
 }
-template <int LOGN, int NB>
-WD void ntt_inv4(uint64_t* buf, const WideTables& tb) {
+template <int LOGN, int NB, class A>
+WD void ntt_inv4(typename A::T* buf, const A& a) {
     constexpr int N = 1 << LOGN, T = N / 4;
-    const uint64_t Q = tb.Q;
     const int u = (int)threadIdx.x;
 #pragma unroll 1
     for (int s = 0; s + 1 < LOGN; s += 2) {
         const int t = 1 << s, m = N >> (s + 1);
         const int i = u >> s, k = u & (t - 1);
         const int e0 = (i << (s + 2)) + k;
-        const uint64_t wa = tb.tabI[m + 2 * i], was = tb.tabIS[m + 2 * i];
-        const uint64_t wb = tb.tabI[m + 2 * i + 1], wbs = tb.tabIS[m + 2 * i + 1];
-        const uint64_t w2 = tb.tabI[(m >> 1) + i], w2s = tb.tabIS[(m >> 1) + i];
+        const auto wa = a.tabI[m + 2 * i], was = a.tabIS[m + 2 * i];
+        const auto wb = a.tabI[m + 2 * i + 1], wbs = a.tabIS[m + 2 * i + 1];
+        const auto w2 = a.tabI[(m >> 1) + i], w2s = a.tabIS[(m >> 1) + i];
 #pragma unroll
         for (int p = 0; p < NB; ++p) {
-            uint64_t* b = buf + p * N + e0;
-            const uint64_t x0 = b[0], x1 = b[t], x2 = b[2 * t], x3 = b[3 * t];
-            const uint64_t y0 = add_q(x0, x1, Q), y1 = mul_shoup(sub_q(x0, x1, Q), wa, was, Q);
-            const uint64_t y2 = add_q(x2, x3, Q), y3 = mul_shoup(sub_q(x2, x3, Q), wb, wbs, Q);
-            b[0] = add_q(y0, y2, Q);
-            b[2 * t] = mul_shoup(sub_q(y0, y2, Q), w2, w2s, Q);
-            b[t] = add_q(y1, y3, Q);
-            b[3 * t] = mul_shoup(sub_q(y1, y3, Q), w2, w2s, Q);
+            auto* b = buf + p * N + e0;
+            auto x0 = b[0], x1 = b[t], x2 = b[2 * t], x3 = b[3 * t];
+            a.gs(x0, x1, wa, was);
+            a.gs(x2, x3, wb, wbs);
+            a.gs(x0, x2, w2, w2s);
+            a.gs(x1, x3, w2, w2s);
+            b[0] = x0;
+            b[t] = x1;
+            b[2 * t] = x2;
+            b[3 * t] = x3;
         }
         __syncthreads();
     }
     if (LOGN & 1) {  // last stage: t = N / 2, m = 1
-        const uint64_t w = tb.tabI[1], ws = tb.tabIS[1];
+        const auto w = a.tabI[1], ws = a.tabIS[1];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int j = u + T * k;
 #pragma unroll
             for (int p = 0; p < NB; ++p) {
-                uint64_t* b = buf + p * N + j;
-                const uint64_t U = b[0], V = b[N / 2];
-                b[0] = add_q(U, V, Q);
-                b[N / 2] = mul_shoup(sub_q(U, V, Q), w, ws, Q);
+                auto* b = buf + p * N + j;
+                auto x = b[0], y = b[N / 2];
+                a.gs(x, y, w, ws);
+                b[0] = x;
+                b[N / 2] = y;
             }
         }
         __syncthreads();
@@ -210,56 +297,60 @@ WD void ntt_inv4(uint64_t* buf, const WideTables& tb) {
 #ifndef FHE_WIDE_R4
 #define FHE_WIDE_R4 1
 #endif
-template <int LOGN, int NB>
-WD void fwd(uint64_t* buf, const WideTables& tb) {
-    if (FHE_WIDE_R4) ntt_fwd4<LOGN, NB>(buf, tb);
-    else ntt_fwd<LOGN, NB>(buf, tb);
+template <int LOGN, int NB, class A>
+WD void fwd(typename A::T* buf, const A& a) {
+    if (FHE_WIDE_R4) ntt_fwd4<LOGN, NB>(buf, a);
+    else ntt_fwd<LOGN, NB>(buf, a);
 }
-template <int LOGN, int NB>
-WD void inv(uint64_t* buf, const WideTables& tb) {
-    if (FHE_WIDE_R4) ntt_inv4<LOGN, NB>(buf, tb);
-    else ntt_inv<LOGN, NB>(buf, tb);
+template <int LOGN, int NB, class A>
+WD void inv(typename A::T* buf, const A& a) {
+    if (FHE_WIDE_R4) ntt_inv4<LOGN, NB>(buf, a);
+    else ntt_inv<LOGN, NB>(buf, a);
 }
 }  // namespace
 
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
-    k_blind_rotate_wide(WideArgs g, WideTables tb, const uint64_t* __restrict__ bsk, const uint16_t* __restrict__ idx,
-                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b) {
-    constexpr int N = 1 << LOGN, T = N / 4, S = 4;
-    __shared__ uint64_t buf[2 * N];
+template <int LOGN, class A>
+__global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
+    k_blind_rotate_wide(WideArgs g, WideTables tb, const typename A::T* __restrict__ bsk,
+                        const uint16_t* __restrict__ idx, const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a,
+                        uint64_t* __restrict__ ext_b) {
+    using T = typename A::T;
+    using Sum = typename A::S;
+    constexpr int N = 1 << LOGN, TH = N / 4, S = 4;
+    __shared__ T buf[2 * N];
+    const A a(tb);
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
-    const uint64_t Q = tb.Q, QHalf = Q >> 1;
+    const T Q = a.Q, QHalf = Q >> 1;
     const uint32_t dG2 = (g.digitsG - 1) * 2, gb = g.gbits, sh = 64 - gb;
 
     // test vector (BootstrapGateCore binfhe-base-scheme.cpp:556-575 / BootstrapFuncCore :596-608):
     // acc1 = NTT(m), acc0 = 0
-    uint64_t acc0[S], acc1[S];
+    T acc0[S], acc1[S];
     if (g.acc_io && !g.acc_tv) {  // the seam's accumulator (EvalAcc on a given acc)
         const uint64_t* src = g.acc_io + (size_t)gate * 2 * N;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            acc0[r] = src[t + T * r];
-            acc1[r] = src[N + t + T * r];
+            acc0[r] = (T)src[t + TH * r];
+            acc1[r] = (T)src[N + t + TH * r];
         }
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            const uint32_t x = t + T * r;
+            const uint32_t x = t + TH * r;
             uint64_t v = 0;
             if (x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
                 v = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
-            buf[x] = v;
+            buf[x] = (T)v;
         }
         __syncthreads();
-        fwd<LOGN, 1>(buf, tb);
+        fwd<LOGN, 1>(buf, a);
 #pragma unroll
         for (int r = 0; r < S; ++r) {
             acc0[r] = 0;
-            acc1[r] = buf[t + T * r];
+            acc1[r] = buf[t + TH * r];
         }
     }
 
@@ -272,30 +363,30 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            buf[t + T * r]     = acc0[r];
-            buf[N + t + T * r] = acc1[r];
+            buf[t + TH * r]     = acc0[r];
+            buf[N + t + TH * r] = acc1[r];
         }
         __syncthreads();
-        inv<LOGN, 2>(buf, tb);
+        inv<LOGN, 2>(buf, a);
         // SignedDigitDecompose state: centred value, lowest digit dropped
         int64_t d[2][S];
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                const uint64_t v = mul_shoup(buf[p * N + t + T * r], tb.ninv, tb.ninvS, Q);
+                const T v = a.mul_shoup(buf[p * N + t + TH * r], a.ninv, a.ninvS);
                 int64_t x = v < QHalf ? (int64_t)v : (int64_t)v - (int64_t)Q;
                 const int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
                 d[p][r] = (x - r0) >> gb;
             }
-        U128 acc[2][2][S];  // [sign][component][slot]
+        Sum acc[2][2][S];  // [sign][component][slot]
 #pragma unroll
         for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
-                for (int r = 0; r < S; ++r) acc[sg][c][r] = U128{0, 0};
-        const uint64_t* key = bsk + (size_t)i * key_stride;
+                for (int r = 0; r < S; ++r) acc[sg][c][r] = A::zero();
+        const T* key = bsk + (size_t)i * key_stride;
 #pragma unroll 1
         for (uint32_t L = 0; 2 * L < dG2; ++L) {
             __syncthreads();  // previous readers of buf are done
@@ -307,21 +398,21 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
                     int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
                     d[p][r] = (x - r0) >> gb;
                     if (r0 < 0) r0 += (int64_t)Q;
-                    buf[p * N + t + T * r] = (uint64_t)r0;
+                    buf[p * N + t + TH * r] = (T)r0;
                 }
             __syncthreads();
-            fwd<LOGN, 2>(buf, tb);
+            fwd<LOGN, 2>(buf, a);
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                const uint32_t j = t + T * r;
-                const uint64_t x0 = buf[j], x1 = buf[N + j];
+                const uint32_t j = t + TH * r;
+                const T x0 = buf[j], x1 = buf[N + j];
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const uint64_t* k0 = key + ((size_t)(sg * dG2 + 2 * L) * 2 + c) * N;
-                        mac(acc[sg][c][r], x0, k0[j]);
-                        mac(acc[sg][c][r], x1, k0[2 * N + j]);  // row 2L + 1
+                        const T* k0 = key + ((size_t)(sg * dG2 + 2 * L) * 2 + c) * N;
+                        A::mac(acc[sg][c][r], x0, k0[j]);
+                        A::mac(acc[sg][c][r], x1, k0[2 * N + j]);  // row 2L + 1
                     }
             }
         }
@@ -329,18 +420,18 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
         const uint32_t mneg = 2 * N - m, emask = 2 * N - 1;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            const uint32_t j = t + T * r;
+            const uint32_t j = t + TH * r;
             const uint32_t e = 2 * (__brev(j) >> (32 - LOGN)) + 1;
-            const uint64_t mp = sub_q(tb.psiM[(e * m) & emask], tb.oneM, Q);
-            const uint64_t mn = sub_q(tb.psiM[(e * mneg) & emask], tb.oneM, Q);
+            const T mp = a.sub(a.psiM[(e * m) & emask], a.oneM);
+            const T mn = a.sub(a.psiM[(e * mneg) & emask], a.oneM);
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                U128 z{0, 0};
-                mac(z, redc(acc[0][c][r], Q, tb.qinv), mp);
-                mac(z, redc(acc[1][c][r], Q, tb.qinv), mn);
-                const uint64_t add = redc(z, Q, tb.qinv);
-                if (c == 0) acc0[r] = add_q(acc0[r], add, Q);
-                else acc1[r] = add_q(acc1[r], add, Q);
+                Sum z = A::zero();
+                A::mac(z, a.redc(acc[0][c][r]), mp);
+                A::mac(z, a.redc(acc[1][c][r]), mn);
+                const T add = a.redc(z);
+                if (c == 0) acc0[r] = a.add(acc0[r], add);
+                else acc1[r] = a.add(acc1[r], add);
             }
         }
     }
@@ -349,8 +440,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
         uint64_t* dst = g.acc_io + (size_t)gate * 2 * N;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            dst[t + T * r]     = acc0[r];
-            dst[N + t + T * r] = acc1[r];
+            dst[t + TH * r]     = acc0[r];
+            dst[N + t + TH * r] = acc1[r];
         }
         return;
     }
@@ -359,35 +450,35 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        buf[t + T * r]     = acc0[r];
-        buf[N + t + T * r] = acc1[r];
+        buf[t + TH * r]     = acc0[r];
+        buf[N + t + TH * r] = acc1[r];
     }
     __syncthreads();
-    inv<LOGN, 2>(buf, tb);
+    inv<LOGN, 2>(buf, a);
     uint64_t* oa = ext_a + (size_t)gate * N;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        const uint32_t x = t + T * r;
-        const uint64_t c = mul_shoup(buf[x == 0 ? 0 : N - x], tb.ninv, tb.ninvS, Q);
+        const uint32_t x = t + TH * r;
+        const T c = a.mul_shoup(buf[x == 0 ? 0 : N - x], a.ninv, a.ninvS);
         const uint64_t v = (x == 0 || c == 0) ? c : Q - c;
         oa[x] = g.msb_out ? round_qQ(v, g.qKS, Q) : v;
     }
     if (t == 0) {
-        const uint64_t bb = add_q(g.b_const % Q, mul_shoup(buf[N], tb.ninv, tb.ninvS, Q), Q);
+        const uint64_t bb = a.add((T)(g.b_const % Q), a.mul_shoup(buf[N], a.ninv, a.ninvS));
         ext_b[gate] = g.msb_out ? round_qQ(bb, g.qKS, Q) : bb;
     }
 }
 
 // ---------------------------------------------------------------------------
-// LMKCDEY (rgsw-acc-lmkcdey.cpp:70-287) and DM (rgsw-acc-dm.cpp:62-145) on the 64-bit accumulator:
+// LMKCDEY (rgsw-acc-lmkcdey.cpp:70-287) and DM (rgsw-acc-dm.cpp:62-145) on the wide accumulator:
 // the per-gate op list of k_prep_lmk_w / k_prep_dm_w, in the work split of k_blind_rotate_wide.
 //   EXT(i)  (AddToAccLMKCDEY / AddToAccDM): both accumulators to COEF, digitsG - 1 gadget levels of
 //           both (rows 2L / 2L + 1 of ek[i]), acc_c <- sum_rows D x ek[i][row][c]  (acc replaced);
 //   AUTO(t) (Automorphism, k = 5^t, or 2N - 5 for t = 0): acc <- sigma_k(acc) in EVAL (a slot
 //           permutation), acc0' alone to COEF and decomposed, acc0 <- sum_L D_L x ak[t][L][0],
 //           acc1 <- acc1' + sum_L D_L x ak[t][L][1].
-// LMKCDEY starts with acc1 <- sigma_(2N-5)(acc1) (:99).  Keys in Montgomery form, 128-bit sums, one
-// reduction per slot and component.
+// LMKCDEY starts with acc1 <- sigma_(2N-5)(acc1) (:99).  Keys in Montgomery form, one reduction per
+// slot and component.
 // ---------------------------------------------------------------------------
 namespace {
 // EVAL slot j holds the value at psi^(2 brv(j) + 1); sigma_k's slot j reads slot brv((e_j k mod 2N - 1) / 2)
@@ -399,109 +490,112 @@ WD uint32_t auto_src(uint32_t j, uint32_t k) {
 }
 }  // namespace
 
-template <int LOGN, bool DM>
-__global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
-    k_blind_rotate_wide_ops(WideArgs g, WideTables tb, const uint64_t* __restrict__ bsk,
-                            const uint64_t* __restrict__ autok, const uint16_t* __restrict__ ops,
+template <int LOGN, bool DM, class A>
+__global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
+    k_blind_rotate_wide_ops(WideArgs g, WideTables tb, const typename A::T* __restrict__ bsk,
+                            const typename A::T* __restrict__ autok, const uint16_t* __restrict__ ops,
                             const uint32_t* __restrict__ nops, uint32_t maxops, const uint32_t* __restrict__ tvb,
                             uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b) {
-    constexpr int N = 1 << LOGN, T = N / 4, S = 4;
-    __shared__ uint64_t buf[2 * N];
+    using T = typename A::T;
+    using Sum = typename A::S;
+    constexpr int N = 1 << LOGN, TH = N / 4, S = 4;
+    __shared__ T buf[2 * N];
+    const A a(tb);
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
-    const uint64_t Q = tb.Q, QHalf = Q >> 1;
+    const T Q = a.Q, QHalf = Q >> 1;
     const uint32_t dA = g.digitsG - 1, dG2 = 2 * dA, gb = g.gbits, sh = 64 - gb;
 
-    uint64_t acc0[S], acc1[S];
+    T acc0[S], acc1[S];
     if (g.acc_io && !g.acc_tv) {  // the seam's accumulator; LMKCDEY's acc1 <- sigma_(2N-5)(acc1) (:99)
         const uint64_t* src = g.acc_io + (size_t)gate * 2 * N;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            acc0[r] = src[t + T * r];
-            acc1[r] = src[N + (DM ? t + T * r : auto_src<LOGN>(t + T * r, 2 * N - 5))];
+            acc0[r] = (T)src[t + TH * r];
+            acc1[r] = (T)src[N + (DM ? t + TH * r : auto_src<LOGN>(t + TH * r, 2 * N - 5))];
         }
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            const uint32_t x = t + T * r;
+            const uint32_t x = t + TH * r;
             uint64_t v = 0;
             if (x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
                 v = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
-            buf[x] = v;
+            buf[x] = (T)v;
         }
         __syncthreads();
-        fwd<LOGN, 1>(buf, tb);
+        fwd<LOGN, 1>(buf, a);
 #pragma unroll
         for (int r = 0; r < S; ++r) {
             acc0[r] = 0;
-            acc1[r] = buf[DM ? t + T * r : auto_src<LOGN>(t + T * r, 2 * N - 5)];
+            acc1[r] = buf[DM ? t + TH * r : auto_src<LOGN>(t + TH * r, 2 * N - 5)];
         }
     }
     // the decomposition of rgsw-acc.cpp:54-91 from the canonical COEF value at buf[p N + j]:
     // centred, the lowest digit dropped, one level per call of digit()
     auto start = [&](int p, uint32_t j) -> int64_t {
-        const uint64_t v = mul_shoup(buf[p * N + j], tb.ninv, tb.ninvS, Q);
+        const T v = a.mul_shoup(buf[p * N + j], a.ninv, a.ninvS);
         const int64_t x = v < QHalf ? (int64_t)v : (int64_t)v - (int64_t)Q;
         const int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
         return (x - r0) >> gb;
     };
-    auto digit = [&](int64_t& d) -> uint64_t {
+    auto digit = [&](int64_t& d) -> T {
         int64_t r0 = (int64_t)((uint64_t)d << sh) >> sh;
         d = (d - r0) >> gb;
         if (r0 < 0) r0 += (int64_t)Q;
-        return (uint64_t)r0;
+        return (T)r0;
     };
     const uint16_t* gops = ops + (size_t)gate * maxops;
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(nops[gate]);
 #pragma unroll 1
     for (uint32_t it = 0; it < cnt; ++it) {
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
-        U128 U[2][S];
+        Sum U[2][S];
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int r = 0; r < S; ++r) U[c][r] = U128{0, 0};
+            for (int r = 0; r < S; ++r) U[c][r] = A::zero();
         __syncthreads();
         if (DM || !(op & 0x8000u)) {
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                buf[t + T * r]     = acc0[r];
-                buf[N + t + T * r] = acc1[r];
+                buf[t + TH * r]     = acc0[r];
+                buf[N + t + TH * r] = acc1[r];
             }
             __syncthreads();
-            inv<LOGN, 2>(buf, tb);
+            inv<LOGN, 2>(buf, a);
             int64_t d[2][S];
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
-                for (int r = 0; r < S; ++r) d[p][r] = start(p, t + T * r);
-            const uint64_t* key = bsk + (size_t)op * dG2 * 2 * N;
+                for (int r = 0; r < S; ++r) d[p][r] = start(p, t + TH * r);
+            const T* key = bsk + (size_t)op * dG2 * 2 * N;
 #pragma unroll 1
             for (uint32_t L = 0; L < dA; ++L) {
                 __syncthreads();
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
-                    for (int r = 0; r < S; ++r) buf[p * N + t + T * r] = digit(d[p][r]);
+                    for (int r = 0; r < S; ++r) buf[p * N + t + TH * r] = digit(d[p][r]);
                 __syncthreads();
-                fwd<LOGN, 2>(buf, tb);
+                fwd<LOGN, 2>(buf, a);
 #pragma unroll
                 for (int r = 0; r < S; ++r) {
-                    const uint32_t j = t + T * r;
-                    const uint64_t x0 = buf[j], x1 = buf[N + j];
+                    const uint32_t j = t + TH * r;
+                    const T x0 = buf[j], x1 = buf[N + j];
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        mac(U[c][r], x0, key[((size_t)(2 * L) * 2 + c) * N + j]);
-                        mac(U[c][r], x1, key[((size_t)(2 * L + 1) * 2 + c) * N + j]);
+                        A::mac(U[c][r], x0, key[((size_t)(2 * L) * 2 + c) * N + j]);
+                        A::mac(U[c][r], x1, key[((size_t)(2 * L + 1) * 2 + c) * N + j]);
                     }
                 }
             }
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                acc0[r] = redc(U[0][r], Q, tb.qinv);
-                acc1[r] = redc(U[1][r], Q, tb.qinv);
+                acc0[r] = a.redc(U[0][r]);
+                acc1[r] = a.redc(U[1][r]);
             }
         } else {
             const uint32_t ta = op & 0x7fffu;
@@ -512,45 +606,45 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
             }
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                buf[t + T * r]     = acc0[r];
-                buf[N + t + T * r] = acc1[r];
+                buf[t + TH * r]     = acc0[r];
+                buf[N + t + TH * r] = acc1[r];
             }
             __syncthreads();
-            uint64_t a0[S];
+            T a0[S];
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                const uint32_t src = auto_src<LOGN>(t + T * r, k);
+                const uint32_t src = auto_src<LOGN>(t + TH * r, k);
                 a0[r]   = buf[src];
                 acc1[r] = buf[N + src];
             }
             __syncthreads();
 #pragma unroll
-            for (int r = 0; r < S; ++r) buf[t + T * r] = a0[r];
+            for (int r = 0; r < S; ++r) buf[t + TH * r] = a0[r];
             __syncthreads();
-            inv<LOGN, 1>(buf, tb);
+            inv<LOGN, 1>(buf, a);
             int64_t d[S];
 #pragma unroll
-            for (int r = 0; r < S; ++r) d[r] = start(0, t + T * r);
-            const uint64_t* key = autok + (size_t)ta * dA * 2 * N;
+            for (int r = 0; r < S; ++r) d[r] = start(0, t + TH * r);
+            const T* key = autok + (size_t)ta * dA * 2 * N;
 #pragma unroll 1
             for (uint32_t L = 0; L < dA; ++L) {
                 __syncthreads();
 #pragma unroll
-                for (int r = 0; r < S; ++r) buf[t + T * r] = digit(d[r]);
+                for (int r = 0; r < S; ++r) buf[t + TH * r] = digit(d[r]);
                 __syncthreads();
-                fwd<LOGN, 1>(buf, tb);
+                fwd<LOGN, 1>(buf, a);
 #pragma unroll
                 for (int r = 0; r < S; ++r) {
-                    const uint32_t j = t + T * r;
-                    const uint64_t x = buf[j];
+                    const uint32_t j = t + TH * r;
+                    const T x = buf[j];
 #pragma unroll
-                    for (int c = 0; c < 2; ++c) mac(U[c][r], x, key[((size_t)L * 2 + c) * N + j]);
+                    for (int c = 0; c < 2; ++c) A::mac(U[c][r], x, key[((size_t)L * 2 + c) * N + j]);
                 }
             }
 #pragma unroll
             for (int r = 0; r < S; ++r) {
-                acc0[r] = redc(U[0][r], Q, tb.qinv);
-                acc1[r] = add_q(acc1[r], redc(U[1][r], Q, tb.qinv), Q);
+                acc0[r] = a.redc(U[0][r]);
+                acc1[r] = a.add(acc1[r], a.redc(U[1][r]));
             }
         }
     }
@@ -559,8 +653,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
         uint64_t* dst = g.acc_io + (size_t)gate * 2 * N;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            dst[t + T * r]     = acc0[r];
-            dst[N + t + T * r] = acc1[r];
+            dst[t + TH * r]     = acc0[r];
+            dst[N + t + TH * r] = acc1[r];
         }
         return;
     }
@@ -568,36 +662,40 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, FHE_WIDE_WAVES)
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        buf[t + T * r]     = acc0[r];
-        buf[N + t + T * r] = acc1[r];
+        buf[t + TH * r]     = acc0[r];
+        buf[N + t + TH * r] = acc1[r];
     }
     __syncthreads();
-    inv<LOGN, 2>(buf, tb);
+    inv<LOGN, 2>(buf, a);
     uint64_t* oa = ext_a + (size_t)gate * N;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        const uint32_t x = t + T * r;
-        const uint64_t c = mul_shoup(buf[x == 0 ? 0 : N - x], tb.ninv, tb.ninvS, Q);
+        const uint32_t x = t + TH * r;
+        const T c = a.mul_shoup(buf[x == 0 ? 0 : N - x], a.ninv, a.ninvS);
         const uint64_t v = (x == 0 || c == 0) ? c : Q - c;
         oa[x] = g.msb_out ? round_qQ(v, g.qKS, Q) : v;
     }
     if (t == 0) {
-        const uint64_t bb = add_q(g.b_const % Q, mul_shoup(buf[N], tb.ninv, tb.ninvS, Q), Q);
+        const uint64_t bb = a.add((T)(g.b_const % Q), a.mul_shoup(buf[N], a.ninv, a.ninvS));
         ext_b[gate] = g.msb_out ? round_qQ(bb, g.qKS, Q) : bb;
     }
 }
 
-hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, const uint64_t* bsk,
-                                        const uint64_t* autok, const uint16_t* ops, const uint32_t* nops,
-                                        uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
-                                        bool dm, hipStream_t s) {
-    if (g.count == 0) return hipSuccess;
-    if ((g.N != 512 && g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 ||
-        g.factor == 0 || g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
-        return hipErrorInvalidValue;
-#define FHE_WIDE_OPS(LG, DM_)                                                                                  \
-    hipLaunchKernelGGL((k_blind_rotate_wide_ops<LG, DM_>), dim3(g.count), dim3((1 << LG) / 4), 0, s, g, t, bsk, \
-                       autok, ops, nops, maxops, tvb, ext_a, ext_b)
+static bool wide_args_ok(const WideArgs& g) {
+    return (g.N == 512 || g.N == 1024 || g.N == 2048) && g.digitsG >= 2 && g.gbits >= 1 && g.gbits <= 62 &&
+           g.factor != 0 && g.ctmod <= 2 * g.N && !(g.ctmod & (g.ctmod - 1));
+}
+
+template <class A>
+static void launch_ops(const WideArgs& g, const WideTables& t, const void* bsk, const void* autok, const uint16_t* ops,
+                       const uint32_t* nops, uint32_t maxops, const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b,
+                       bool dm, hipStream_t s) {
+    using T = typename A::T;
+    const T* kb = static_cast<const T*>(bsk);
+    const T* ka = static_cast<const T*>(autok);
+#define FHE_WIDE_OPS(LG, DM_)                                                                                     \
+    hipLaunchKernelGGL((k_blind_rotate_wide_ops<LG, DM_, A>), dim3(g.count), dim3((1 << LG) / 4), 0, s, g, t, kb, \
+                       ka, ops, nops, maxops, tvb, ext_a, ext_b)
     if (g.N == 2048) {
         if (dm) FHE_WIDE_OPS(11, true);
         else FHE_WIDE_OPS(11, false);
@@ -609,39 +707,69 @@ hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, 
         else FHE_WIDE_OPS(9, false);
     }
 #undef FHE_WIDE_OPS
+}
+
+hipError_t launch_blind_rotate_wide_ops(const WideArgs& g, const WideTables& t, const void* bsk, const void* autok,
+                                        const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                        uint64_t* ext_a, uint64_t* ext_b, bool dm, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!wide_args_ok(g)) return hipErrorInvalidValue;
+    if (t.narrow) launch_ops<A32>(g, t, bsk, autok, ops, nops, maxops, tvb, ext_a, ext_b, dm, s);
+    else launch_ops<A64>(g, t, bsk, autok, ops, nops, maxops, tvb, ext_a, ext_b, dm, s);
     return hipGetLastError();
 }
 
-// ExternalProduct seam: raw RGSW rows (canonical mod Q) -> Montgomery form x 2^64 mod Q, the form
-// k_blind_rotate_wide_ops reads its keys in: redc(x R2) with R2 = 2^128 mod Q (x R2 < Q^2 < Q 2^64)
+// ExternalProduct seam: raw RGSW rows (canonical mod Q) -> Montgomery form x R mod Q, the form
+// k_blind_rotate_wide_ops reads its keys in: redc(x R2) with R2 = R^2 mod Q (x R2 < Q^2 < Q R)
 __global__ void k_pack_rgsw_wide(const uint64_t* __restrict__ raw, size_t words, uint64_t Q, uint64_t qinv, uint64_t R2,
                                  uint64_t* __restrict__ out) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
         const uint64_t x = raw[i];
-        out[i] = redc(U128{x * R2, __umul64hi(x, R2)}, Q, qinv);
+        const uint64_t lo = x * R2, u = lo * qinv;
+        const uint64_t r = __umul64hi(x, R2) + __umul64hi(u, Q) + (lo != 0 ? 1 : 0);
+        out[i] = r >= Q ? r - Q : r;
+    }
+}
+__global__ void k_pack_rgsw_narrow(const uint64_t* __restrict__ raw, size_t words, uint32_t Q, uint32_t qinv,
+                                   uint32_t R2, uint32_t* __restrict__ out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t t = (uint64_t)(uint32_t)raw[i] * R2;
+        const uint32_t u = (uint32_t)t * qinv;
+        const uint32_t r = (uint32_t)((t + (uint64_t)u * Q) >> 32);
+        out[i] = r >= Q ? r - Q : r;
     }
 }
 
-hipError_t launch_pack_rgsw_wide(const uint64_t* raw, size_t words, uint64_t Q, uint64_t qinv, uint64_t R2, uint64_t* out,
-                                 hipStream_t s) {
+hipError_t launch_pack_rgsw_wide(const uint64_t* raw, size_t words, const WideTables& t, void* out, hipStream_t s) {
     if (words == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)std::min<size_t>((words + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_pack_rgsw_wide, dim3(blocks), dim3(256), 0, s, raw, words, Q, qinv, R2, out);
+    if (t.narrow)
+        hipLaunchKernelGGL(k_pack_rgsw_narrow, dim3(blocks), dim3(256), 0, s, raw, words, t.Q32, t.qinv32, t.r2_32,
+                           static_cast<uint32_t*>(out));
+    else
+        hipLaunchKernelGGL(k_pack_rgsw_wide, dim3(blocks), dim3(256), 0, s, raw, words, t.Q, t.qinv, t.r2,
+                           static_cast<uint64_t*>(out));
     return hipGetLastError();
 }
 
-hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const uint64_t* bsk, const uint16_t* idx,
+template <class A>
+static void launch_gate(const WideArgs& g, const WideTables& t, const void* bsk, const uint16_t* idx,
+                        const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+    const auto* kb = static_cast<const typename A::T*>(bsk);
+    if (g.N == 2048)
+        hipLaunchKernelGGL((k_blind_rotate_wide<11, A>), dim3(g.count), dim3(512), 0, s, g, t, kb, idx, tvb, ext_a, ext_b);
+    else if (g.N == 1024)
+        hipLaunchKernelGGL((k_blind_rotate_wide<10, A>), dim3(g.count), dim3(256), 0, s, g, t, kb, idx, tvb, ext_a, ext_b);
+    else  // TOY
+        hipLaunchKernelGGL((k_blind_rotate_wide<9, A>), dim3(g.count), dim3(128), 0, s, g, t, kb, idx, tvb, ext_a, ext_b);
+}
+
+hipError_t launch_blind_rotate_wide(const WideArgs& g, const WideTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if ((g.N != 512 && g.N != 1024 && g.N != 2048) || g.digitsG < 2 || g.gbits < 1 || g.gbits > 62 ||
-        g.factor == 0 || g.ctmod > 2 * g.N || (g.ctmod & (g.ctmod - 1)))
-        return hipErrorInvalidValue;
-    if (g.N == 2048)
-        hipLaunchKernelGGL(k_blind_rotate_wide<11>, dim3(g.count), dim3(512), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
-    else if (g.N == 1024)
-        hipLaunchKernelGGL(k_blind_rotate_wide<10>, dim3(g.count), dim3(256), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
-    else  // TOY
-        hipLaunchKernelGGL(k_blind_rotate_wide<9>, dim3(g.count), dim3(128), 0, s, g, t, bsk, idx, tvb, ext_a, ext_b);
+    if (!wide_args_ok(g)) return hipErrorInvalidValue;
+    if (t.narrow) launch_gate<A32>(g, t, bsk, idx, tvb, ext_a, ext_b, s);
+    else launch_gate<A64>(g, t, bsk, idx, tvb, ext_a, ext_b, s);
     return hipGetLastError();
 }
 

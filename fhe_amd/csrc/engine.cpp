@@ -104,6 +104,9 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         if (p_.n > 2048) throw std::invalid_argument("device path supports n <= 2048");
         FHE_HIP_CHECK(hipSetDevice(device_));
         FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        const char* nw = std::getenv("FHE_HIP_NARROW");  // "0": keep 64-bit residues (A/B, tests)
+        narrow_ = !(nw && std::string(nw) == "0") && p_.Q < (1ull << 30) &&
+                  (uint64_t)p_.digitsG2 * p_.Q < (1ull << 32);
         build_tables_wide();
         set_base(p_.baseG);
         if (g3_set(p_)) {
@@ -286,9 +289,44 @@ void Engine::build_tables_wide() {
         t[4 * N + e] = mulmod(x, R, Q);
         x = mulmod(x, p_.psi, Q);
     }
+    // the 32-bit policy's copies (A32): Shoup quotients floor(w 2^32 / Q), psi^e 2^32 mod Q
+    const size_t w32 = narrow_ ? 6 * (size_t)N : 0;  // tab, tabS, tabI, tabIS (N each), psiM (2N)
+    std::vector<uint64_t> t32((w32 + 1) / 2, 0);
+    uint32_t* n32 = reinterpret_cast<uint32_t*>(t32.data());
+    if (narrow_) {
+        auto shoup32 = [&](uint64_t w) { return (uint32_t)(((u128)w << 32) / Q); };
+        for (uint32_t i = 0; i < N; ++i) {
+            n32[i] = (uint32_t)h.tab[i];
+            n32[N + i] = shoup32(h.tab[i]);
+            n32[2 * N + i] = (uint32_t)h.tabI[i];
+            n32[3 * N + i] = shoup32(h.tabI[i]);
+        }
+        const uint64_t R32 = (1ull << 32) % Q;
+        uint64_t y = 1;
+        for (uint32_t e = 0; e < 2 * N; ++e) {
+            n32[4 * N + e] = (uint32_t)mulmod(y, R32, Q);
+            y = mulmod(y, p_.psi, Q);
+        }
+        wtabs_.narrow = 1;
+        wtabs_.Q32 = (uint32_t)Q;
+        wtabs_.qinv32 = neg_inv32((uint32_t)Q);
+        wtabs_.ninv32 = (uint32_t)h.ninv;
+        wtabs_.ninvS32 = shoup32(h.ninv);
+        wtabs_.oneM32 = (uint32_t)R32;
+        wtabs_.r2_32 = (uint32_t)mulmod(R32, R32, Q);
+    }
+    t.insert(t.end(), t32.begin(), t32.end());
     FHE_HIP_CHECK(hipMalloc(&d_wtables_, t.size() * 8));
     FHE_HIP_CHECK(hipMemcpy(d_wtables_, t.data(), t.size() * 8, hipMemcpyHostToDevice));
     const uint64_t* d = static_cast<const uint64_t*>(d_wtables_);
+    if (narrow_) {
+        const uint32_t* d32 = reinterpret_cast<const uint32_t*>(d + 6 * (size_t)N);
+        wtabs_.tab32 = d32;
+        wtabs_.tabS32 = d32 + N;
+        wtabs_.tabI32 = d32 + 2 * N;
+        wtabs_.tabIS32 = d32 + 3 * N;
+        wtabs_.psiM32 = d32 + 4 * N;
+    }
     wtabs_.tab = d;
     wtabs_.tabS = d + N;
     wtabs_.tabI = d + 2 * N;
@@ -301,26 +339,33 @@ void Engine::build_tables_wide() {
     wtabs_.ninv = h.ninv;
     wtabs_.ninvS = shoup64(h.ninv, Q);
     wtabs_.oneM = R;
+    wtabs_.r2 = mulmod(R, R, Q);
 }
 
 void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     if (!bsk) throw std::invalid_argument("bsk is null");
     if (words != p_.bsk_words()) throw std::invalid_argument("bsk has wrong length");
-    if (wide_) {  // raw layout [n][2][dG2][2][N], Montgomery form K 2^64 mod Q (bootstrap_wide.hip)
+    if (wide_) {  // raw layout [n][2][dG2][2][N], Montgomery form K R mod Q (bootstrap_wide.hip), R = 2^64
+                  // (u64 words) or 2^32 (u32 words, narrow_)
         const uint64_t Q = p_.Q;
-        std::vector<uint64_t> dev(words);
+        const unsigned sh = narrow_ ? 32 : 64;
+        const size_t wb = narrow_ ? 4 : 8;
+        std::vector<uint64_t> dev((words * wb + 7) / 8);
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(dev.data());
         bool bad = false;
 #pragma omp parallel for schedule(static) reduction(|| : bad)
         for (int64_t i = 0; i < (int64_t)words; ++i) {
             bad = bad || bsk[i] >= Q;
-            dev[i] = (uint64_t)(((u128)(bsk[i] % Q) << 64) % Q);
+            const uint64_t v = (uint64_t)(((u128)(bsk[i] % Q) << sh) % Q);
+            if (narrow_) d32[i] = (uint32_t)v;
+            else dev[i] = v;
         }
         if (bad) throw std::invalid_argument("bsk coefficient not reduced mod Q");
         FHE_HIP_CHECK(hipSetDevice(device_));
         if (d_bsk_) FHE_HIP_CHECK(hipFree(d_bsk_));
         d_bsk_ = nullptr;
-        FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * 8));
-        FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), words * 8, hipMemcpyHostToDevice));
+        FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * wb));
+        FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), words * wb, hipMemcpyHostToDevice));
         if (g3_) pack_ginx3(bsk);
         return;
     }
@@ -346,7 +391,7 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
             for (uint32_t k = 0; k < 16; ++k)
                 for (uint32_t lane = 0; lane < 64; ++lane) {
                     const uint32_t h = lane >> 5, l = lane & 31;
-                    const uint32_t row = kBskHalfSwap ? d ^ h : d;  // boot.h FHE_XCHG
+                    const uint32_t row = kBskHalfSwap ? d ^ h : d;  // boot.h kBskHalfSwap
                     const size_t src = ((size_t)row * 2 + h) * N + l * 32 + 2 * k;
                     const size_t dst = row_off(d, k, lane, 0);  // boot.h
                     dst_key[dst] = to_mont(mulmod(src_key[src] % Q, ninv, Q), Q);
@@ -620,9 +665,8 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
             return;
         }
         if (p_.method == M_LMKCDEY || p_.method == M_AP) {
-            const uint64_t* bsk = static_cast<const uint64_t*>(d_bsk_);
             const bool dm = p_.method == M_AP;
-            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, bsk, dm ? bsk : bsk + (size_t)p_.n * p_.digitsG2 * 2 * p_.N,
+            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, wkey(0), wkey(dm ? 0 : (size_t)p_.n * p_.digitsG2 * 2 * p_.N),
                                                        d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, dm, s));
             return;
         }
@@ -630,8 +674,7 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
             FHE_HIP_CHECK(launch_blind_rotate_ginx3(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_wext_a_, d_wext_b_, s));
             return;
         }
-        FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, static_cast<const uint64_t*>(d_bsk_) + cur_off_, d_idx_, d_tvb_,
-                                               d_wext_a_, d_wext_b_, s));
+        FHE_HIP_CHECK(launch_blind_rotate_wide(w, wtabs_, wkey(cur_off_), d_idx_, d_tvb_, d_wext_a_, d_wext_b_, s));
         return;
     }
     // the kernels' digit decomposition (bootstrap.hip decompose2) works on d + C in 32 bits
@@ -719,7 +762,7 @@ void Engine::external_product_device(size_t count, const uint64_t* rgsw, const u
     FHE_HIP_CHECK(hipSetDevice(device_));
     constexpr size_t kChunk = 0x8000;   // op codes hold key indices < 0x8000
     const size_t keyw = (size_t)p_.digitsG2 * 2 * p_.N;
-    const size_t wpk = wide_ ? 2 : 1;   // u32 words per packed key word (u64 Montgomery on the 64-bit path)
+    const size_t wpk = wide_ && !narrow_ ? 2 : 1;   // u32 words per packed key word (u64 Montgomery on the 64-bit path)
     const size_t cap = std::min(count, kChunk);
     if (cap > epcap_) {
         sync_streams();
@@ -732,7 +775,6 @@ void Engine::external_product_device(size_t count, const uint64_t* rgsw, const u
         epcap_ = cap;
     }
     const uint32_t ninv_mont = wide_ ? 0u : to_mont(invmod(p_.N, p_.Q), p_.Q);
-    const uint64_t R = (uint64_t)(((u128)1 << 64) % p_.Q), R2 = mulmod(R, R, p_.Q);
     for (size_t off = 0; off < count; off += kChunk) {
         const size_t c = std::min(kChunk, count - off);
         if (result + off * 2 * p_.N != rlwe + off * 2 * p_.N)
@@ -740,9 +782,8 @@ void Engine::external_product_device(size_t count, const uint64_t* rgsw, const u
                                          hipMemcpyDeviceToDevice, s));
         FHE_HIP_CHECK(launch_single_ops(d_epops_, d_epn_, (uint32_t)c, 1, s));
         if (wide_) {
-            // the 64-bit DM op loop (k_blind_rotate_wide_ops): one EXT op per item with its own key
-            uint64_t* k64 = reinterpret_cast<uint64_t*>(d_epk_);
-            FHE_HIP_CHECK(launch_pack_rgsw_wide(rgsw + off * keyw, c * keyw, p_.Q, wtabs_.qinv, R2, k64, s));
+            // the wide DM op loop (k_blind_rotate_wide_ops): one EXT op per item with its own key
+            FHE_HIP_CHECK(launch_pack_rgsw_wide(rgsw + off * keyw, c * keyw, wtabs_, d_epk_, s));
             WideArgs w{};
             w.count = (uint32_t)c;
             w.n = p_.n;
@@ -753,7 +794,7 @@ void Engine::external_product_device(size_t count, const uint64_t* rgsw, const u
             w.gbits = p_.gBits;
             w.qKS = p_.qKS;
             w.acc_io = result + off * 2 * p_.N;
-            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, k64, k64, d_epops_, d_epn_, 1, nullptr, nullptr,
+            FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, d_epk_, d_epk_, d_epops_, d_epn_, 1, nullptr, nullptr,
                                                        nullptr, true, s));
             continue;
         }

@@ -219,7 +219,15 @@ private:
     uint64_t* d_io_ = nullptr;
     // large-precision family: u64 keys (Montgomery BSK, raw KSK A ++ B), tables, u64 ctExt
     bool wide_ = false;
+    // the wide accumulator in 32-bit residues (bootstrap_wide.hip A32): Q < 2^30 and digitsG2 Q < 2^32;
+    // d_bsk_ then holds u32 Montgomery words
+    bool narrow_ = false;
     WideTables wtabs_{};
+    // word w of the resident wide keys (u64, or u32 when narrow_)
+    const void* wkey(size_t w) const {
+        return narrow_ ? (const void*)(static_cast<const uint32_t*>(d_bsk_) + w)
+                       : (const void*)(static_cast<const uint64_t*>(d_bsk_) + w);
+    }
     void* d_wtables_ = nullptr;
     uint64_t* d_wksk_ = nullptr;
     uint64_t* d_wext_a_ = nullptr;

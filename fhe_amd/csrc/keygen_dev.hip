@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) k_kg_finish(const KgDesc* __restrict__ D,
         // ((kk * 64 + h * 32 + l) * 2 + e), values x * N^-1 in Montgomery form (* 2^32 mod Q)
         const uint32_t l = j >> 5, kk = (j & 31) >> 1, el = j & 1;
         const uint32_t v0 = (uint32_t)((((r0 * ninv) % Q) << 32) % Q), v1 = (uint32_t)((((r1 * ninv) % Q) << 32) % Q);
-        // component 1 of row rp sits at position rp ^ 1 with kBskHalfSwap (boot.h FHE_XCHG)
+        // component 1 of row rp sits at position rp ^ 1 with kBskHalfSwap (boot.h)
         const uint32_t rp1 = kBskHalfSwap ? k.rp ^ 1 : k.rp;
         if (ginx_u4) {
             // rp = (2 i + ks) dG2 + row with dG2 = 4 (boot.h ginx_u4_off)

@@ -8,19 +8,10 @@
 // i.e. NativePoly::SwitchFormat (src/core/include/lattice/hal/default/poly-impl.h:420-440):
 // forward output j (bit-reversed order) is a(psi^(2*brv(j)+1)); inverse is its exact inverse.
 //
-// Work decomposition (one polynomial per half-wave of 32 lanes, 32 coefficients
-// per lane, 4 waves = 8 polynomials per workgroup iteration, persistent grid):
-//   index x = (h << 6) | (l << 1) | b0           ("layout A": lane l = x bits 5..1,
-//                                                  register r = (h << 1) | b0)
-//   "layout B" swaps register and lane:   lane = (h << 1) | b0, register = x bits 5..1.
-// Forward: load A (16-byte loads: coefficient pairs) -> stages on bits 9..6 in
-// registers (twiddles uniform across lanes: scalar loads) -> LDS transpose to B
-// -> stages on bits 5..1 in registers (per-lane twiddles from the LDS-staged
-// table) -> LDS transpose to A -> stage on bit 0 -> 16-byte stores.
-// Inverse: the same in reverse order; the final stage folds N^-1 as the
-// reference does (transformnat-impl.h:599-623).
-// Global traffic = 8 B read + 8 B written per coefficient (u64 words, as the
-// reference stores them); all arithmetic exact mod Q.
+// One polynomial per wave64 (16 coefficients per lane) in three register layouts, two LDS
+// transposes per transform: k_ntt1024w (32-bit residues, Q < 2^30) and k_ntt1024w64 (64-bit, Q < 2^62;
+// the Sol60 policy for the poly-benchmark prime 2^60 - 2^14 + 1).  Global traffic = 8 B read + 8 B
+// written per coefficient (u64 words, as the reference stores them); all arithmetic exact mod Q.
 #include "arith.h"
 #include "ntt.h"
 
@@ -29,12 +20,6 @@ namespace fhe_amd {
 template <typename T>
 struct ModT;
 
-#ifndef FHE_NTT_COPY
-#define FHE_NTT_COPY 0      // experiment: skip the arithmetic (memory-only timing)
-#endif
-#ifndef FHE_NTT_WAVESYNC
-#define FHE_NTT_WAVESYNC 1  // transposes synchronise the wave only (tiles are half-wave private)
-#endif
 
 // 32-bit path (Q < 2^30): Harvey-style lazy butterflies.  Forward values live in
 // [0, 4Q), inverse values in [0, 2Q); one correction at the end gives [0, Q).
@@ -46,7 +31,6 @@ struct ModT<uint32_t> {
     FHE_DEV uint32_t lazy_mul(uint32_t x, TW w) const { return mul_shoup_lazy(x, w.x, w.y, Q); }
     // CT: (x, y) in [0,4Q)^2 -> (x + wy, x - wy) in [0,4Q)^2
     FHE_DEV void ct(uint32_t& x, uint32_t& y, TW w) const {
-        if (FHE_NTT_COPY) return;
         x = csub(x, Q2);
         const uint32_t t = lazy_mul(y, w);
         y = x + Q2 - t;
@@ -54,209 +38,18 @@ struct ModT<uint32_t> {
     }
     // GS: (x, y) in [0,2Q)^2 -> (x + y, (x - y) w) in [0,2Q)^2
     FHE_DEV void gs(uint32_t& x, uint32_t& y, TW w) const {
-        if (FHE_NTT_COPY) return;
         const uint32_t d = x + Q2 - y;
         x = csub(x + y, Q2);
         y = lazy_mul(d, w);
     }
     // last inverse stage with N^-1 folded: ((x + y) n^-1, (x - y) w1 n^-1) in [0,Q)
     FHE_DEV void gs_last(uint32_t& x, uint32_t& y, TW lo, TW hi) const {
-        if (FHE_NTT_COPY) return;
         const uint32_t d = x + Q2 - y;
         x = csub(lazy_mul(x + y, lo), Q);
         y = csub(lazy_mul(d, hi), Q);
     }
     FHE_DEV uint32_t fwd_out(uint32_t x) const { return csub(csub(x, Q2), Q); }
 };
-
-// 64-bit path (Q < 2^62): fully reduced butterflies.
-template <>
-struct ModT<uint64_t> {
-    using TW = ulonglong2;  // (w, w' = floor(w 2^64 / Q))
-    uint64_t Q, Q2;
-    FHE_DEV void ct(uint64_t& x, uint64_t& y, TW w) const {
-        if (FHE_NTT_COPY) return;
-        const uint64_t t = mul_shoup64(y, w.x, w.y, Q);
-        y = sub_mod64(x, t, Q);
-        x = add_mod64(x, t, Q);
-    }
-    FHE_DEV void gs(uint64_t& x, uint64_t& y, TW w) const {
-        if (FHE_NTT_COPY) return;
-        const uint64_t t = sub_mod64(x, y, Q);
-        x = add_mod64(x, y, Q);
-        y = mul_shoup64(t, w.x, w.y, Q);
-    }
-    FHE_DEV void gs_last(uint64_t& x, uint64_t& y, TW lo, TW hi) const {
-        if (FHE_NTT_COPY) return;
-        const uint64_t s = add_mod64(x, y, Q), d = sub_mod64(x, y, Q);
-        x = mul_shoup64(s, lo.x, lo.y, Q);
-        y = mul_shoup64(d, hi.x, hi.y, Q);
-    }
-    FHE_DEV uint64_t fwd_out(uint64_t x) const { return x; }
-};
-
-// 32x32 transpose of one half-wave's registers through its private LDS tile
-// (row stride 33 words: conflict-free on both sides).
-template <typename T>
-FHE_DEV void half_transpose(T (&v)[32], T* tile, int l) {
-#pragma unroll
-    for (int r = 0; r < 32; ++r) tile[l * 33 + r] = v[r];
-    if (FHE_NTT_WAVESYNC) { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); }
-    else __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = tile[r * 33 + l];
-    if (FHE_NTT_WAVESYNC) { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); }
-    else __syncthreads();
-}
-
-// Raw 16-byte coefficient-pair loads of one polynomial row for this lane (layout A).
-FHE_DEV void load_raw(ulonglong2 (&pre)[16], const uint64_t* src, int l) {
-#pragma unroll
-    for (int h = 0; h < 16; ++h) pre[h] = *reinterpret_cast<const ulonglong2*>(src + (h << 6) + (l << 1));
-}
-
-// Forward (CT, Table) or inverse (GS, TableI, N^-1 folded into the last stage) transform of
-// the 32 coefficients a half-wave lane holds in layout A; returns them in layout A.
-template <typename T, bool INV>
-FHE_DEV void transform(T (&v)[32], const typename ModT<T>::TW* __restrict__ tab, const typename ModT<T>::TW* s_tw,
-                       T* tile, int l, const ModT<T>& m, typename ModT<T>::TW last_lo, typename ModT<T>::TW last_hi) {
-    using TW    = typename ModT<T>::TW;
-    const int hl = l >> 1;
-    if (!INV) {
-        // stages on bits 9..6 (layout A): twiddle index depends on h only (scalar loads)
-#pragma unroll
-        for (int b = 9; b >= 6; --b) {
-            const int hb = b - 6;
-#pragma unroll
-            for (int h = 0; h < 16; ++h) {
-                if (h & (1 << hb)) continue;
-                const TW w = tab[(1 << (9 - b)) + (h >> (hb + 1))];
-                m.ct(v[(h << 1) | 0], v[((h | (1 << hb)) << 1) | 0], w);
-                m.ct(v[(h << 1) | 1], v[((h | (1 << hb)) << 1) | 1], w);
-            }
-        }
-        half_transpose(v, tile, l);
-        // layout B: lane = (h << 1) | b0, register r = x bits 5..1
-#pragma unroll
-        for (int b = 5; b >= 1; --b) {
-            const int rb = b - 1;
-#pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                if (r & (1 << rb)) continue;
-                const TW w = s_tw[(1 << (9 - b)) + ((hl << (5 - b)) | (r >> b))];
-                m.ct(v[r], v[r | (1 << rb)], w);
-            }
-        }
-        half_transpose(v, tile, l);
-        // stage on bit 0 (layout A)
-#pragma unroll
-        for (int h = 0; h < 16; ++h) m.ct(v[2 * h], v[2 * h + 1], s_tw[512 + (h << 5) + l]);
-    } else {
-#pragma unroll
-        for (int h = 0; h < 16; ++h) m.gs(v[2 * h], v[2 * h + 1], s_tw[512 + (h << 5) + l]);
-        half_transpose(v, tile, l);
-#pragma unroll
-        for (int b = 1; b <= 5; ++b) {
-            const int rb = b - 1;
-#pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                if (r & (1 << rb)) continue;
-                const TW w = s_tw[(1 << (9 - b)) + ((hl << (5 - b)) | (r >> b))];
-                m.gs(v[r], v[r | (1 << rb)], w);
-            }
-        }
-        half_transpose(v, tile, l);
-#pragma unroll
-        for (int b = 6; b <= 8; ++b) {
-            const int hb = b - 6;
-#pragma unroll
-            for (int h = 0; h < 16; ++h) {
-                if (h & (1 << hb)) continue;
-                const TW w = tab[(1 << (9 - b)) + (h >> (hb + 1))];
-                m.gs(v[(h << 1) | 0], v[((h | (1 << hb)) << 1) | 0], w);
-                m.gs(v[(h << 1) | 1], v[((h | (1 << hb)) << 1) | 1], w);
-            }
-        }
-        // bit 9: lo' = (lo + hi) N^-1, hi' = (lo - hi) w1 N^-1
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            m.gs_last(v[(h << 1) | 0], v[((h | 8) << 1) | 0], last_lo, last_hi);
-            m.gs_last(v[(h << 1) | 1], v[((h | 8) << 1) | 1], last_lo, last_hi);
-        }
-    }
-}
-
-// Persistent, software-pipelined batch kernel.  A wave transforms a pair of
-// polynomials per iteration (one per half-wave) and walks pairs wave_id,
-// wave_id + W, ... (W = waves in the grid); the raw loads of its next pair are
-// issued before the current pair's arithmetic and stores, so HBM reads, the
-// butterflies and HBM writes of consecutive pairs overlap.  The LDS twiddle
-// table is filled once per workgroup; the transposes use half-wave-private LDS
-// tiles and need only wave-level ordering.
-template <typename T, bool INV>
-__global__ void __launch_bounds__(256)
-    k_ntt1024(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
-              const typename ModT<T>::TW* __restrict__ tab, T Q, typename ModT<T>::TW last_lo,
-              typename ModT<T>::TW last_hi) {
-    using M  = ModT<T>;
-    using TW = typename M::TW;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    TW* s_tw = reinterpret_cast<TW*>(smem);                      // 1024 entries
-    T* tiles = reinterpret_cast<T*>(smem + 1024 * sizeof(TW));   // 8 x 32 x 33
-    const M m{Q, (T)(2 * Q)};
-
-    for (int i = threadIdx.x; i < 1024; i += 256) s_tw[i] = tab[i];
-
-    const int l  = threadIdx.x & 31;
-    const int hp = threadIdx.x >> 5;                 // half-wave within the workgroup
-    T* tile      = tiles + hp * (32 * 33);
-    const uint32_t npairs = (count + 1) >> 1;
-    const uint32_t W      = gridDim.x * 4;
-    uint32_t pair         = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t half   = (threadIdx.x >> 5) & 1;
-
-    // Rows are clamped to count - 1, so every load and store is unconditional (the
-    // waitcnt before each unpack then covers just the prefetch, not the previous
-    // pair's stores).  The second half-wave of an odd tail pair transforms row
-    // count - 1 as well and rewrites the same values; prefetches past the last
-    // pair load row count - 1 and are never used.
-    auto row = [&](uint32_t pr) -> uint32_t {
-        const uint32_t ply = 2 * pr + half;
-        return ply < count ? ply : count - 1;
-    };
-    // one pair: unpack the raw words, transform, store (the register buffer is then free)
-    auto step = [&](ulonglong2 (&buf)[16], uint32_t pr) {
-        T v[32];
-#pragma unroll
-        for (int h = 0; h < 16; ++h) {
-            v[2 * h]     = (T)buf[h].x;
-            v[2 * h + 1] = (T)buf[h].y;
-        }
-        transform<T, INV>(v, tab, s_tw, tile, l, m, last_lo, last_hi);
-        uint64_t* dst = out + (size_t)row(pr) * 1024;
-#pragma unroll
-        for (int h = 0; h < 16; ++h) {
-            ulonglong2 t;
-            t.x = (uint64_t)(INV ? v[2 * h] : m.fwd_out(v[2 * h]));
-            t.y = (uint64_t)(INV ? v[2 * h + 1] : m.fwd_out(v[2 * h + 1]));
-            *reinterpret_cast<ulonglong2*>(dst + (h << 6) + (l << 1)) = t;
-        }
-    };
-    // two register buffers, alternated by a 2x unrolled loop: the next pair's loads are
-    // in flight while the current pair is transformed and stored, with no copies
-    ulonglong2 bufA[16], bufB[16];
-    if (pair < npairs) load_raw(bufA, in + (size_t)row(pair) * 1024, l);
-    __syncthreads();  // s_tw ready
-    for (; pair < npairs; pair += 2 * W) {
-        load_raw(bufB, in + (size_t)row(pair + W) * 1024, l);
-        __builtin_amdgcn_sched_barrier(0);
-        step(bufA, pair);
-        if (pair + W >= npairs) break;
-        load_raw(bufA, in + (size_t)row(pair + 2 * W) * 1024, l);
-        __builtin_amdgcn_sched_barrier(0);
-        step(bufB, pair + W);
-    }
-}
 
 // ---------------------------------------------------------------------------------------------
 // One polynomial per wave64 (32-bit path, Q < 2^30): 16 coefficients per lane, so a 4096-poly
@@ -270,9 +63,6 @@ __global__ void __launch_bounds__(256)
 // LDS word address of x in both transposes: x + 4 (x >> 6) (conflict-free for the dword accesses
 // of A and B; C reads/writes 16-byte runs).
 // ---------------------------------------------------------------------------------------------
-#ifndef FHE_NTT_T3
-#define FHE_NTT_T3 1   // k_ntt1024w: global rows in layout A both ways (third LDS transpose)
-#endif
 namespace {
 constexpr int kWTile = 1024 + 64;  // words per wave
 FHE_DEV int wt(int x) { return x + ((x >> 6) << 2); }
@@ -398,24 +188,15 @@ __global__ void __launch_bounds__(512)
     uint32_t poly    = blockIdx.x * (blockDim.x >> 6) + wv;
     auto rowp        = [&](uint32_t p) -> uint32_t { return p < count ? p : count - 1; };
 
-    // raw loads: forward reads layout A (one dword -- the low word -- of 16 u64 rows of 512 B),
-    // inverse reads layout C (the (lo, hi) words of 4 consecutive u64 per x9x8: 16-byte loads)
+    // raw loads, both directions in layout A: the low word of 16 u64 rows of 512 B (the values are
+    // below 2^32)
     using Raw = uint4[8];
     auto load = [&](Raw& buf, uint32_t p) {
-        const uint64_t* src = in + (size_t)rowp(p) * 1024;
-        if (!INV || FHE_NTT_T3) {
-            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(in + (size_t)rowp(p) * 1024);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                buf[r].x = s32[2 * ((2 * r) * 64 + L)];
-                buf[r].y = s32[2 * ((2 * r + 1) * 64 + L)];
-            }
-        } else {
-#pragma unroll
-            for (int hh = 0; hh < 4; ++hh) {
-                buf[2 * hh]     = *reinterpret_cast<const uint4*>(src + (hh << 8) + (L << 2));
-                buf[2 * hh + 1] = *reinterpret_cast<const uint4*>(src + (hh << 8) + (L << 2) + 2);
-            }
+        for (int r = 0; r < 8; ++r) {
+            buf[r].x = s32[2 * ((2 * r) * 64 + L)];
+            buf[r].y = s32[2 * ((2 * r + 1) * 64 + L)];
         }
     };
     auto step = [&](Raw& buf, uint32_t p) {
@@ -482,7 +263,6 @@ __global__ void __launch_bounds__(512)
                 m.ct(v[4 * hh + 2], v[4 * hh + 3], w0b);
             }
             uint64_t* dst = out + (size_t)rowp(p) * 1024;
-#if FHE_NTT_T3
             // T3: C -> A, then coalesced 512-byte rows
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -496,15 +276,7 @@ __global__ void __launch_bounds__(512)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
             for (int r = 0; r < 16; ++r) dst[(r << 6) + L] = (uint64_t)tile[wt((r << 6) | L)];
-#else
-#pragma unroll
-            for (int hh = 0; hh < 4; ++hh) {
-                *reinterpret_cast<uint4*>(dst + (hh << 8) + (L << 2)) = make_uint4(m.fwd_out(v[4 * hh]), 0, m.fwd_out(v[4 * hh + 1]), 0);
-                *reinterpret_cast<uint4*>(dst + (hh << 8) + (L << 2) + 2) = make_uint4(m.fwd_out(v[4 * hh + 2]), 0, m.fwd_out(v[4 * hh + 3]), 0);
-            }
-#endif
         } else {
-#if FHE_NTT_T3
             // T3^-1: A (coalesced rows) -> C
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
@@ -522,15 +294,6 @@ __global__ void __launch_bounds__(512)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#else
-#pragma unroll
-            for (int hh = 0; hh < 4; ++hh) {
-                v[4 * hh]     = buf[2 * hh].x;
-                v[4 * hh + 1] = buf[2 * hh].z;
-                v[4 * hh + 2] = buf[2 * hh + 1].x;
-                v[4 * hh + 3] = buf[2 * hh + 1].z;
-            }
-#endif
             // C: stage 0 then stage 1 (GS); signed: planned reductions (InvPlanW)
             auto redp = [&](int st) {
                 if (A::kSigned) {
@@ -641,7 +404,6 @@ struct Lazy64 {
     ulonglong2 lo, hi;  // (N^-1, pre), (w1 N^-1, pre)
     FHE_DEV static uint64_t csub(uint64_t x, uint64_t m) { return x >= m ? x - m : x; }
     FHE_DEV uint64_t lazy_mul(uint64_t x, ulonglong2 w) const {
-        if (FHE_NTT_COPY) return x;
         return x * w.x - __umul64hi(x, w.y) * Q;
     }
     FHE_DEV void ct(uint64_t& x, uint64_t& y, ulonglong2 w) const {
@@ -671,7 +433,6 @@ struct Sol60 {
     ulonglong2 lo, hi;  // (N^-1, pre), (w1 N^-1, pre)
     // y w mod Q in [0, 4Q) for any y < 2^64 (w < Q, w.y = floor(w 2^64 / Q))
     FHE_DEV uint64_t mul(uint64_t y, ulonglong2 w) const {
-        if (FHE_NTT_COPY) return y;
         const uint32_t yl = (uint32_t)y, yh = (uint32_t)(y >> 32);
         const uint32_t pl = (uint32_t)w.y, ph = (uint32_t)(w.y >> 32);
         // y w' / 2^64 = yh ph + (yl ph + yh pl) / 2^32 + yl pl / 2^64: the high words of the middle
@@ -679,9 +440,21 @@ struct Sol60 {
         const uint64_t q = (uint64_t)yh * ph + __umulhi(yl, ph) + __umulhi(yh, pl);  // floor(y w' / 2^64) - {0, 1, 2}
         const uint32_t wl = (uint32_t)w.x, wh = (uint32_t)(w.x >> 32);
         const uint64_t p  = (uint64_t)yl * wl;
-        // y w - q Q = y w - (q << 60) + (q << S) - q  (mod 2^64; the true value is in [0, 4Q))
-        const uint32_t rh = (uint32_t)(p >> 32) + yl * wh + yh * wl - ((uint32_t)q << 28);
-        return ((((uint64_t)rh) << 32) | (uint32_t)p) + (q << S) - q;
+        // y w - q Q = P + (q << S) - D (mod 2^64; the true value is in [0, 4Q)), with P = y w mod 2^64
+        // (one 32 x 32 -> 64 product, two low products into its high word) and D = q + (q << 60)
+        // (high word (q << 28) + (q >> 32)): three adds, one 64-bit shift, one 64-bit subtract
+        const uint32_t ph32 = (uint32_t)(p >> 32) + yl * wh + yh * wl;
+        const uint64_t E = ((((uint64_t)ph32) << 32) | (uint32_t)p) + (q << S);
+        // E - D as one subtract with borrow (the compiler splits D into its words and folds the high
+        // one into the product's addend: a move and a negation more per product)
+        uint32_t rl, rh;
+        asm("v_sub_co_u32 %0, vcc, %4, %2\n\t"
+            "v_lshl_add_u32 %1, %2, 28, %3\n\t"
+            "v_subb_co_u32 %1, vcc, %5, %1, vcc"
+            : "=&v"(rl), "=&v"(rh)
+            : "v"((uint32_t)q), "v"((uint32_t)(q >> 32)), "v"((uint32_t)E), "v"((uint32_t)(E >> 32))
+            : "vcc");
+        return ((uint64_t)rh << 32) | rl;
     }
     // any x < 2^64 -> x mod 2^60 + (x >> 60) c < Q + 16 c < 2Q (bound 2 in the plan)
     FHE_DEV uint64_t fold(uint64_t x) const {
@@ -692,15 +465,28 @@ struct Sol60 {
         const uint64_t f = fold(x);
         return f >= Q ? f - Q : f;
     }
+    // (x, a) -> (x + t, a - t): the borrow chain of the subtract with the add between its halves
+    // (no wait state; the compiler puts an s_nop between adjacent halves)
+    FHE_DEV static void add_sub(uint64_t& x, uint64_t a, uint64_t t, uint64_t& d) {
+        uint32_t dl, dh;
+        uint64_t s;
+        asm("v_sub_co_u32 %0, vcc, %3, %5\n\t"
+            "v_lshl_add_u64 %2, %7, 0, %8\n\t"
+            "v_subb_co_u32 %1, vcc, %4, %6, vcc"
+            : "=&v"(dl), "=&v"(dh), "=&v"(s)
+            : "v"((uint32_t)a), "v"((uint32_t)(a >> 32)), "v"((uint32_t)t), "v"((uint32_t)(t >> 32)), "v"(x), "v"(t)
+            : "vcc");
+        x = s;
+        d = ((uint64_t)dh << 32) | dl;
+    }
     FHE_DEV void ct(uint64_t& x, uint64_t& y, ulonglong2 w) const {
         const uint64_t t = mul(y, w);
-        y = x + 4 * Q - t;
-        x = x + t;
+        add_sub(x, x + 4 * Q, t, y);
     }
     // k: the plan's bound of y (y < k Q), so x - y + k Q >= 0
     FHE_DEV void gs(uint64_t& x, uint64_t& y, ulonglong2 w, int k) const {
-        const uint64_t d = x + (uint64_t)k * Q - y;
-        x = x + y;
+        uint64_t d;
+        add_sub(x, x + (uint64_t)k * Q, y, d);
         y = mul(d, w);
     }
     FHE_DEV void gs_last(uint64_t& x, uint64_t& y, int k) const {
@@ -1005,51 +791,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
 }
 }  // namespace
 
-#ifndef FHE_NTT_WAVE
-#define FHE_NTT_WAVE 1   // 32-bit path: one polynomial per wave (k_ntt1024w)
-#endif
-#ifndef FHE_NTT_SIGNED
-#define FHE_NTT_SIGNED 1 // k_ntt1024w: signed Montgomery arithmetic for Q < 2^27
-#endif
 #ifndef FHE_NTT_WWPS
 #define FHE_NTT_WWPS 5   // k_ntt1024w: resident waves per SIMD the grid is sized for
 #endif
 
-#ifndef FHE_NTT_WPS
-#define FHE_NTT_WPS 2   // resident waves per SIMD the grid is sized for
-#endif
-
-template <typename T>
-static hipError_t launch(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
-                         hipStream_t s) {
-    using TW        = typename ModT<T>::TW;
-    const size_t sm = 1024 * sizeof(TW) + (size_t)8 * 32 * 33 * sizeof(T);
-    if (count == 0) return hipSuccess;
-    // one workgroup = 4 waves = 8 polynomials per iteration; cap the grid at the
-    // resident capacity so that every wave iterates (pipelining) on large batches
-    const uint32_t groups = (count + 7) / 8;
-    const uint32_t cap    = (uint32_t)p.cus * FHE_NTT_WPS;  // 4 waves/group, 4 SIMDs/CU
-    dim3 grid(groups < cap ? groups : cap), block(256);
-    const TW* tab = reinterpret_cast<const TW*>(inverse ? p.d_tab_inv : p.d_tab_fwd);
-    TW lo, hi;
-    if constexpr (sizeof(T) == 4) {
-        lo = TW{(uint32_t)p.ninv, (uint32_t)p.ninv_pre};
-        hi = TW{(uint32_t)p.w1ninv, (uint32_t)p.w1ninv_pre};
-    } else {
-        lo = TW{p.ninv, p.ninv_pre};
-        hi = TW{p.w1ninv, p.w1ninv_pre};
-    }
-    if (inverse)
-        hipLaunchKernelGGL((k_ntt1024<T, true>), grid, block, sm, s, in, out, count, tab, (T)p.Q, lo, hi);
-    else
-        hipLaunchKernelGGL((k_ntt1024<T, false>), grid, block, sm, s, in, out, count, tab, (T)p.Q, lo, hi);
-    return hipGetLastError();
-}
-
 static hipError_t launch_wave(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                               hipStream_t s) {
     if (count == 0) return hipSuccess;
-    const bool sg = FHE_NTT_SIGNED && p.d_tabm_fwd != nullptr;  // Q < 2^27
+    const bool sg = p.d_tabm_fwd != nullptr;  // Q < 2^27: signed Montgomery
     // 8 waves (polynomials) per workgroup; twiddles (8 or 4 KB) + 8 tiles of 4.25 KB
     const size_t sm       = 1024 * (sg ? 4 : 8) + (size_t)8 * kWTile * 4;
     const uint32_t groups = (count + 7) / 8;
@@ -1072,12 +821,6 @@ static hipError_t launch_wave(const NttPlan& p, const uint64_t* in, uint64_t* ou
     return hipGetLastError();
 }
 
-#ifndef FHE_NTT64_WAVE
-#define FHE_NTT64_WAVE 1   // 64-bit path: one polynomial per wave (k_ntt1024w64)
-#endif
-#ifndef FHE_NTT64_SOL
-#define FHE_NTT64_SOL 1    // k_ntt1024w64: the Sol60 policy for Q = 2^60 - (2^S - 1)
-#endif
 static hipError_t launch_wave64(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                                 hipStream_t s) {
     if (count == 0) return hipSuccess;
@@ -1092,7 +835,7 @@ static hipError_t launch_wave64(const NttPlan& p, const uint64_t* in, uint64_t* 
 #define FHE_NTT64_LAUNCH(MT, PF_)                                                                              \
     if (inverse) hipLaunchKernelGGL((k_ntt1024w64<true, MT, PF_>), grid, block, sm, s, in, out, count, tab, m); \
     else hipLaunchKernelGGL((k_ntt1024w64<false, MT, PF_>), grid, block, sm, s, in, out, count, tab, m)
-    if (FHE_NTT64_SOL && p.sol_shift) {
+    if (p.sol_shift) {  // Q = 2^60 - (2^S - 1): Sol60
         const Sol60 m{p.Q, p.sol_shift, lo, hi};
         if (pf) { FHE_NTT64_LAUNCH(Sol60, true); } else { FHE_NTT64_LAUNCH(Sol60, false); }
     } else {
@@ -1105,10 +848,8 @@ static hipError_t launch_wave64(const NttPlan& p, const uint64_t* in, uint64_t* 
 
 hipError_t ntt1024_launch(const NttPlan& p, const uint64_t* in, uint64_t* out, uint32_t count, bool inverse,
                           hipStream_t s) {
-    if (p.wide) return FHE_NTT64_WAVE ? launch_wave64(p, in, out, count, inverse, s)
-                                      : launch<uint64_t>(p, in, out, count, inverse, s);
-    if (FHE_NTT_WAVE) return launch_wave(p, in, out, count, inverse, s);
-    return launch<uint32_t>(p, in, out, count, inverse, s);
+    if (p.wide) return launch_wave64(p, in, out, count, inverse, s);
+    return launch_wave(p, in, out, count, inverse, s);
 }
 
 }  // namespace fhe_amd

@@ -208,7 +208,9 @@ def make_fb(names=("std128", "lmkcdey")):
         out = {"paramset": ps, "method": m, "key_seed": np.uint64(key_seed), "ms": ms, "xs": xs,
                "in_sha": np.array(sha(sa) + sha(sb) + sha(la) + sha(lb))}
         for lname, lut in fb_luts(q, p, ref.N).items():
-            ao, bo = ref.eval_func(sa, sb, q, lut)
+            # one thread: the reference's LMKCDEY EvalFunc crashes under its own OpenMP parallel loop
+            # (reproduced with 16 ciphertexts; fine ciphertext by ciphertext)
+            ao, bo = ref.eval_func(sa, sb, q, lut, nthreads=1)
             out[f"func_{lname}_a"], out[f"func_{lname}_b"] = ao.astype(np.uint16), bo.astype(np.uint16)
         for rb in (0, 1):
             ao, bo = ref.eval_floor(sa, sb, q, rb)
@@ -311,14 +313,33 @@ def full_inputs(name, count=FULL_GATES):
     return ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2
 
 
+def _full_slice(args):
+    """one process's share of a full batch, single-threaded (the reference's LMKCDEY EvalAcc crashes
+    under its OpenMP gate loop with these keys; separate processes share nothing)"""
+    name, lo, hi = args
+    ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2 = full_inputs(name)
+    ref = Ref(ps, m)
+    ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    return ref.eval_gate(GATES["AND"], a1[lo:hi], b1[lo:hi], a2[lo:hi], b2[lo:hi], nthreads=1)
+
+
 def make_full(names=("std128", "lmkcdey"), nthreads=8):
     import time
     for name in names:
         ps, m, key_seed, keys, bits1, bits2, a1, b1, a2, b2 = full_inputs(name)
-        ref = Ref(ps, m)
-        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
         t0 = time.time()
-        ao, bo = ref.eval_gate(GATES["AND"], a1, b1, a2, b2, nthreads=nthreads)
+        if GATE_SETS[name][1] == LMKCDEY:
+            import multiprocessing as mp
+            step = FULL_GATES // nthreads
+            with mp.get_context("spawn").Pool(nthreads) as pool:
+                parts = pool.map(_full_slice, [(name, s, s + step) for s in range(0, FULL_GATES, step)])
+            ao = np.concatenate([p[0] for p in parts])
+            bo = np.concatenate([p[1] for p in parts])
+            ref = Ref(ps, m)
+        else:
+            ref = Ref(ps, m)
+            ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+            ao, bo = ref.eval_gate(GATES["AND"], a1, b1, a2, b2, nthreads=nthreads)
         dt = time.time() - t0
         dec = np.array([ref.decrypt(keys.sk, ao[i], bo[i], ref.q) for i in range(0, FULL_GATES, 97)])
         assert np.array_equal(dec, (bits1 & bits2)[::97]), "reference AND outputs do not decrypt"

@@ -20,6 +20,7 @@ for g in $groups; do
     large)  for s in $(python -c "import sys; sys.path.insert(0,'tests/golden'); sys.path.insert(0,'tests'); from make_golden import LARGE_SETS; print(' '.join(LARGE_SETS))"); do python $G large $s; done ;;
     config3) python $G config3 ;;
     full)   python $G full std128; python $G full lmkcdey ;;
+    fulllmk) python $G full lmkcdey ;;
   esac
   echo "== $g done $(date +%T)"
 done

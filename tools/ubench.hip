@@ -163,6 +163,48 @@ __global__ void k_lshladd64(unsigned long long* out, unsigned seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
 
+__global__ void k_lshl64(unsigned long long* out, unsigned seed) {
+    unsigned long long a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    unsigned long long a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    unsigned b = (seed & 7) | 1;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_lshlrev_b64 %0, %8, %0\n\t v_lshlrev_b64 %1, %8, %1\n\t"
+            "v_lshlrev_b64 %2, %8, %2\n\t v_lshlrev_b64 %3, %8, %3\n\t"
+            "v_lshlrev_b64 %4, %8, %4\n\t v_lshlrev_b64 %5, %8, %5\n\t"
+            "v_lshlrev_b64 %6, %8, %6\n\t v_lshlrev_b64 %7, %8, %7"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(b));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_lshladd64b(unsigned long long* out, unsigned seed) {
+    unsigned long long a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    unsigned long long a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    unsigned long long b = seed | 1;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_lshl_add_u64 %0, %0, 0, %8\n\t v_lshl_add_u64 %1, %1, 0, %8\n\t"
+            "v_lshl_add_u64 %2, %2, 0, %8\n\t v_lshl_add_u64 %3, %3, 0, %8\n\t"
+            "v_lshl_add_u64 %4, %4, 0, %8\n\t v_lshl_add_u64 %5, %5, 0, %8\n\t"
+            "v_lshl_add_u64 %6, %6, 0, %8\n\t v_lshl_add_u64 %7, %7, 0, %8"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(b));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_mov64(unsigned long long* out, unsigned seed) {
+    unsigned long long a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    unsigned long long a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_mov_b64 %0, %1\n\t v_mov_b64 %1, %2\n\t v_mov_b64 %2, %3\n\t v_mov_b64 %3, %4\n\t"
+            "v_mov_b64 %4, %5\n\t v_mov_b64 %5, %6\n\t v_mov_b64 %6, %7\n\t v_mov_b64 %7, %0"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 template <typename K, typename T>
 static void run(const char* name, K kern, T* buf, int blocks, int threads) {
     hipEvent_t e0, e1;
@@ -196,6 +238,9 @@ int main() {
     run("v_fma_f64", k_fma64, (double*)buf, blocks, threads);
     run("v_mad_i64_i32", k_madi64, (unsigned long long*)buf, blocks, threads);
     run("v_lshl_add_u64", k_lshladd64, (unsigned long long*)buf, blocks, threads);
+    run("v_lshl_add_u64(0)", k_lshladd64b, (unsigned long long*)buf, blocks, threads);
+    run("v_lshlrev_b64", k_lshl64, (unsigned long long*)buf, blocks, threads);
+    run("v_mov_b64", k_mov64, (unsigned long long*)buf, blocks, threads);
     run("v_mul_hi_i32", k_mul_hi_i, (unsigned*)buf, blocks, threads);
     run("v_sub_u32", k_bfe, (unsigned*)buf, blocks, threads);
     run("v_min_u32", k_min, (unsigned*)buf, blocks, threads);
