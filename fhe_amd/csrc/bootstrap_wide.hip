@@ -26,7 +26,8 @@
 #ifndef FHE_WIDE_WAVES
 #define FHE_WIDE_WAVES 4
 #endif
-// the A32 instantiations: the gate kernel at 4 (124 VGPRs; at 6 it spills 40 and runs 27% slower), the
+// the A32 instantiations: the gate kernel at 4 (113 VGPRs, 64 KB of LDS with its tables; with the
+// monomial table through the caches and 6 waves it spills 14 VGPRs and runs 21-29% slower), the
 // op-list kernel at 6 (80 VGPRs: +8% on STD256_LMKCDEY / STD256Q_3_LMKCDEY, profiles/r03_bench_sets_narrow.txt)
 #ifndef FHE_WIDE32_WAVES
 #define FHE_WIDE32_WAVES 4
@@ -56,7 +57,10 @@ WD uint64_t round_qQ(uint64_t v, uint64_t q, uint64_t Q) {
 struct A64 {
     using T = uint64_t;
     using S = U128;
+    using D = int64_t;   // SignedDigitDecompose state
+    using UD = uint64_t;
     static constexpr int kWaves = FHE_WIDE_WAVES, kOpsWaves = FHE_WIDE_WAVES;
+    static constexpr bool kLds = false;  // tables read through the caches (32 KB of LDS per gate already)
     const uint64_t *tab, *tabS, *tabI, *tabIS, *psiM;
     uint64_t Q, qinv, ninv, ninvS, oneM;
     WD explicit A64(const WideTables& t)
@@ -103,7 +107,12 @@ struct A64 {
 struct A32 {
     using T = uint32_t;
     using S = uint64_t;
+    using D = int32_t;   // |centred value| < Q/2 < 2^29: the decomposition in 32-bit words
+    using UD = uint32_t;
     static constexpr int kWaves = FHE_WIDE32_WAVES, kOpsWaves = FHE_WIDE32_OPS_WAVES;
+    // the twiddle (and monomial) tables staged in LDS once per gate: every transform pass reads its
+    // twiddles right before use, so cached global reads left their latency exposed
+    static constexpr bool kLds = true;
     const uint32_t *tab, *tabS, *tabI, *tabIS, *psiM;
     uint32_t Q, qinv, ninv, ninvS, oneM;
     WD explicit A32(const WideTables& t)
@@ -143,6 +152,30 @@ struct A32 {
     }
     WD T fwd_out(T x) const { return csub(csub(x, 2 * Q), Q); }
 };
+
+// A32 gate kernel: copy the tables into LDS and point the policy at them (+2.6% at STD256).
+// Engine::build_tables_wide stores them contiguously (tab, tabS, tabI, tabIS: N words each, then
+// psiM: 2N words); mono = false would leave the monomial table out
+template <class A>
+WD void stage_tables(A& a, typename A::T* st, int N, bool mono) {
+    if constexpr (A::kLds) {
+        const int words = (mono ? 6 : 4) * N;
+        for (int i = threadIdx.x; i < words; i += blockDim.x) st[i] = a.tab[i];
+        __syncthreads();
+        a.tab = st;
+        a.tabS = st + N;
+        a.tabI = st + 2 * N;
+        a.tabIS = st + 3 * N;
+        if (mono) a.psiM = st + 4 * N;
+    }
+}
+
+// Orders one wave's LDS accesses (the next pass reads only what this wave wrote)
+WD void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Merged Cooley-Tukey forward transform in place on NB polynomials at buf + p N (bit-reversed
 // output, ForwardTransformToBitReverseInPlace transformnat-impl.h:302-373); all threads, synced.
@@ -200,7 +233,11 @@ WD void ntt_inv(typename A::T* buf, const A& a) {
 }
 
 // Radix-4 passes of the same transforms: each thread takes whole 4-element units through two
-// stages between barriers (LOGN / 2 barriers instead of LOGN), an odd last stage radix-2.
+// stages between syncs, an odd last stage radix-2.  Wave w's 64 units of a pass whose butterfly
+// blocks hold at most 64 units (forward distance t <= 128, inverse t <= 64; the last forward radix-2
+// stage remapped) lie in elements [256 w, 256 w + 256) of each polynomial, so consecutive such
+// passes synchronise the wave only; a workgroup barrier follows the passes that cross chunks and the
+// last pass (N = 2048: 3 barriers per transform instead of 6).
 template <int LOGN, int NB, class A>
 WD void ntt_fwd4(typename A::T* buf, const A& a) {
     constexpr int N = 1 << LOGN, T = N / 4;
@@ -230,12 +267,16 @@ WD void ntt_fwd4(typename A::T* buf, const A& a) {
             b[t] = x2;
             b[t + th] = x3;
         }
-        __syncthreads();
+        // this pass stayed in the wave's chunk (logt <= 7) and so does what follows: another radix-4
+        // pass or the remapped radix-2 stage (not the end of the transform)
+        const bool more4 = s + 3 < LOGN, r2next = (LOGN & 1) && s + 3 == LOGN;
+        if (logt <= 7 && (more4 || r2next)) wave_sync();
+        else __syncthreads();
     }
-    if (LOGN & 1) {  // last stage: t = 1, m = N / 2
+    if (LOGN & 1) {  // last stage: t = 1, m = N / 2; wave w takes butterflies [128 w, 128 w + 128)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            const int bf = u + T * k;
+            const int bf = ((u >> 6) << 7) + (u & 63) + 64 * k;
             const auto w = a.tab[N / 2 + bf], ws = a.tabS[N / 2 + bf];
 #pragma unroll
             for (int p = 0; p < NB; ++p) {
@@ -274,7 +315,9 @@ WD void ntt_inv4(typename A::T* buf, const A& a) {
             b[2 * t] = x2;
             b[3 * t] = x3;
         }
-        __syncthreads();
+        // within this wave's chunk while this pass and the next have t <= 64 (s + 2 <= 6)
+        if (s + 2 <= 6 && s + 3 < LOGN) wave_sync();
+        else __syncthreads();
     }
     if (LOGN & 1) {  // last stage: t = N / 2, m = 1
         const auto w = a.tabI[1], ws = a.tabIS[1];
@@ -318,10 +361,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
     using Sum = typename A::S;
     constexpr int N = 1 << LOGN, TH = N / 4, S = 4;
     __shared__ T buf[2 * N];
-    const A a(tb);
+    __shared__ T stab[A::kLds ? 6 * N : 1];
+    A a(tb);
+    stage_tables(a, stab, N, true);
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
     const T Q = a.Q, QHalf = Q >> 1;
-    const uint32_t dG2 = (g.digitsG - 1) * 2, gb = g.gbits, sh = 64 - gb;
+    using D = typename A::D;
+    using UD = typename A::UD;
+    const uint32_t dG2 = (g.digitsG - 1) * 2, gb = g.gbits, sh = 8 * sizeof(D) - gb;
 
     // test vector (BootstrapGateCore binfhe-base-scheme.cpp:556-575 / BootstrapFuncCore :596-608):
     // acc1 = NTT(m), acc0 = 0
@@ -369,14 +416,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
         __syncthreads();
         inv<LOGN, 2>(buf, a);
         // SignedDigitDecompose state: centred value, lowest digit dropped
-        int64_t d[2][S];
+        D d[2][S];
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int r = 0; r < S; ++r) {
                 const T v = a.mul_shoup(buf[p * N + t + TH * r], a.ninv, a.ninvS);
-                int64_t x = v < QHalf ? (int64_t)v : (int64_t)v - (int64_t)Q;
-                const int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
+                D x = v < QHalf ? (D)v : (D)v - (D)Q;
+                const D r0 = (D)((UD)x << sh) >> sh;
                 d[p][r] = (x - r0) >> gb;
             }
         Sum acc[2][2][S];  // [sign][component][slot]
@@ -394,10 +441,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
             for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int r = 0; r < S; ++r) {
-                    const int64_t x = d[p][r];
-                    int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
+                    const D x = d[p][r];
+                    D r0 = (D)((UD)x << sh) >> sh;
                     d[p][r] = (x - r0) >> gb;
-                    if (r0 < 0) r0 += (int64_t)Q;
+                    if (r0 < 0) r0 += (D)Q;
                     buf[p * N + t + TH * r] = (T)r0;
                 }
             __syncthreads();
@@ -500,10 +547,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
     using Sum = typename A::S;
     constexpr int N = 1 << LOGN, TH = N / 4, S = 4;
     __shared__ T buf[2 * N];
-    const A a(tb);
+    const A a(tb);  // tables through the caches: staged in LDS (48 KB per gate) this kernel ran 8% slower
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
     const T Q = a.Q, QHalf = Q >> 1;
-    const uint32_t dA = g.digitsG - 1, dG2 = 2 * dA, gb = g.gbits, sh = 64 - gb;
+    using D = typename A::D;
+    using UD = typename A::UD;
+    const uint32_t dA = g.digitsG - 1, dG2 = 2 * dA, gb = g.gbits, sh = 8 * sizeof(D) - gb;
 
     T acc0[S], acc1[S];
     if (g.acc_io && !g.acc_tv) {  // the seam's accumulator; LMKCDEY's acc1 <- sigma_(2N-5)(acc1) (:99)
@@ -535,16 +584,16 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
     }
     // the decomposition of rgsw-acc.cpp:54-91 from the canonical COEF value at buf[p N + j]:
     // centred, the lowest digit dropped, one level per call of digit()
-    auto start = [&](int p, uint32_t j) -> int64_t {
+    auto start = [&](int p, uint32_t j) -> D {
         const T v = a.mul_shoup(buf[p * N + j], a.ninv, a.ninvS);
-        const int64_t x = v < QHalf ? (int64_t)v : (int64_t)v - (int64_t)Q;
-        const int64_t r0 = (int64_t)((uint64_t)x << sh) >> sh;
+        const D x = v < QHalf ? (D)v : (D)v - (D)Q;
+        const D r0 = (D)((UD)x << sh) >> sh;
         return (x - r0) >> gb;
     };
-    auto digit = [&](int64_t& d) -> T {
-        int64_t r0 = (int64_t)((uint64_t)d << sh) >> sh;
+    auto digit = [&](D& d) -> T {
+        D r0 = (D)((UD)d << sh) >> sh;
         d = (d - r0) >> gb;
-        if (r0 < 0) r0 += (int64_t)Q;
+        if (r0 < 0) r0 += (D)Q;
         return (T)r0;
     };
     const uint16_t* gops = ops + (size_t)gate * maxops;
@@ -566,7 +615,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
             }
             __syncthreads();
             inv<LOGN, 2>(buf, a);
-            int64_t d[2][S];
+            D d[2][S];
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -622,7 +671,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
             for (int r = 0; r < S; ++r) buf[t + TH * r] = a0[r];
             __syncthreads();
             inv<LOGN, 1>(buf, a);
-            int64_t d[S];
+            D d[S];
 #pragma unroll
             for (int r = 0; r < S; ++r) d[r] = start(0, t + TH * r);
             const T* key = autok + (size_t)ta * dA * 2 * N;
