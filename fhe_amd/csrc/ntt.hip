@@ -168,7 +168,9 @@ constexpr InvPlanW make_inv_plan_w() {
     return p;
 }
 
-template <bool INV, class A>
+// PF: a persistent wave's next polynomial is loaded during the current one (batches larger than the
+// resident grid); without it every wave transforms at most one polynomial and loads nothing more
+template <bool INV, class A, bool PF>
 __global__ void __launch_bounds__(512)
     k_ntt1024w(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count,
                const typename A::TW* __restrict__ tab, NttK K) {
@@ -374,6 +376,10 @@ __global__ void __launch_bounds__(512)
     Raw bufA, bufB;
     if (poly < count) load(bufA, poly);
     __syncthreads();  // s_tw ready
+    if (!PF) {  // one polynomial per wave: no clamped prefetch of a row nobody transforms
+        if (poly < count) step(bufA, poly);
+        return;
+    }
     for (; poly < count; poly += 2 * W) {
         load(bufB, poly + W);
         __builtin_amdgcn_sched_barrier(0);
@@ -676,20 +682,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
             }
         }
     };
-    auto step = [&](Raw& v, uint32_t p) {
+    // forward layout A: stages 9..6, uniform twiddles from the global table (no LDS)
+    auto stage_a = [&](Raw& v) {
+#pragma unroll
+        for (int b = 9; b >= 6; --b) {
+            const int rb = b - 6;
+            plan(v, 9 - b);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                if (r & (1 << rb)) continue;
+                m.ct(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
+            }
+        }
+    };
+    // pre: the A stages already ran (the first polynomial, ahead of the LDS table's barrier)
+    auto step = [&](Raw& v, uint32_t p, bool pre) {
         uint64_t* dst = out + (size_t)p * 1024;
         if (!INV) {
-            // A: stages 9..6 (uniform twiddles)
-#pragma unroll
-            for (int b = 9; b >= 6; --b) {
-                const int rb = b - 6;
-                plan(v, 9 - b);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    if (r & (1 << rb)) continue;
-                    m.ct(v[r], v[r | (1 << rb)], tab[(1 << (9 - b)) + (r >> (rb + 1))]);
-                }
-            }
+            if (!pre) stage_a(v);
             a_to_b(v);
 #pragma unroll
             for (int b = 5; b >= 2; --b) {
@@ -765,14 +775,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
             for (int r = 0; r < 16; ++r) dst[(r << 6) + L] = v[r];
         }
     };
-    // the first polynomial's rows are requested before the twiddle table is staged
+    // the first polynomial's rows, then the twiddle table; the forward transform runs its layout-A
+    // stages (uniform twiddles, no LDS) on the rows as they land, before the table's barrier
     Raw bufA;
     if (poly < count) load(bufA, poly);
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) s_tw[i] = tab[i];
+    const ulonglong2 tw0 = tab[threadIdx.x], tw1 = tab[threadIdx.x + 512];  // 512 threads (launch_wave64)
+    const bool pre = !INV && poly < count;
+    if (pre) stage_a(bufA);
+    s_tw[threadIdx.x]       = tw0;
+    s_tw[threadIdx.x + 512] = tw1;
     __syncthreads();  // s_tw ready
     if (!PF) {
-        for (; poly < count; poly += W) {
-            step(bufA, poly);
+        for (bool first = true; poly < count; poly += W, first = false) {
+            step(bufA, poly, first && pre);
             if (poly + W < count) load(bufA, poly + W);
         }
         return;
@@ -782,11 +797,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
         const bool more = poly + W < count;   // wave-uniform
         if (more) load(bufB, poly + W);
         __builtin_amdgcn_sched_barrier(0);
-        step(bufA, poly);
+        step(bufA, poly, pre && poly < 2 * W);
         if (!more) break;
         if (poly + 2 * W < count) load(bufA, poly + 2 * W);
         __builtin_amdgcn_sched_barrier(0);
-        step(bufB, poly + W);
+        step(bufB, poly + W, false);
     }
 }
 }  // namespace
@@ -809,15 +824,21 @@ static hipError_t launch_wave(const NttPlan& p, const uint64_t* in, uint64_t* ou
     k.lo = uint2{(uint32_t)p.ninv, (uint32_t)p.ninv_pre};
     k.hi = uint2{(uint32_t)p.w1ninv, (uint32_t)p.w1ninv_pre};
     k.qinvp = p.qinvp; k.oneR = p.oneR; k.ninvR = p.ninvR; k.w1ninvR = p.w1ninvR;
-    if (sg) {
-        const uint32_t* tab = static_cast<const uint32_t*>(inverse ? p.d_tabm_inv : p.d_tabm_fwd);
-        if (inverse) hipLaunchKernelGGL((k_ntt1024w<true, SignedA>), grid, block, sm, s, in, out, count, tab, k);
-        else hipLaunchKernelGGL((k_ntt1024w<false, SignedA>), grid, block, sm, s, in, out, count, tab, k);
-    } else {
-        const uint2* tab = reinterpret_cast<const uint2*>(inverse ? p.d_tab_inv : p.d_tab_fwd);
-        if (inverse) hipLaunchKernelGGL((k_ntt1024w<true, ShoupA>), grid, block, sm, s, in, out, count, tab, k);
-        else hipLaunchKernelGGL((k_ntt1024w<false, ShoupA>), grid, block, sm, s, in, out, count, tab, k);
+    const bool pf = count > grid.x * 8u;   // more polynomials than resident waves
+#define FHE_NTT32_LAUNCH(AT, TT, TAB)                                                                           \
+    {                                                                                                          \
+        const TT* tab = reinterpret_cast<const TT*>(TAB);                                                      \
+        if (pf) {                                                                                              \
+            if (inverse) hipLaunchKernelGGL((k_ntt1024w<true, AT, true>), grid, block, sm, s, in, out, count, tab, k); \
+            else hipLaunchKernelGGL((k_ntt1024w<false, AT, true>), grid, block, sm, s, in, out, count, tab, k); \
+        } else {                                                                                               \
+            if (inverse) hipLaunchKernelGGL((k_ntt1024w<true, AT, false>), grid, block, sm, s, in, out, count, tab, k); \
+            else hipLaunchKernelGGL((k_ntt1024w<false, AT, false>), grid, block, sm, s, in, out, count, tab, k); \
+        }                                                                                                      \
     }
+    if (sg) FHE_NTT32_LAUNCH(SignedA, uint32_t, inverse ? p.d_tabm_inv : p.d_tabm_fwd)
+    else FHE_NTT32_LAUNCH(ShoupA, uint2, inverse ? p.d_tab_inv : p.d_tab_fwd)
+#undef FHE_NTT32_LAUNCH
     return hipGetLastError();
 }
 
