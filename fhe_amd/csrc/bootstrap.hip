@@ -31,9 +31,6 @@
 #ifndef FHE_WAVES_PER_EU
 #define FHE_WAVES_PER_EU 2
 #endif
-#ifndef FHE_GINX_L2PF
-#define FHE_GINX_L2PF 0  // A/B: touch index i+1's keys (one dword per 128-byte line) at the top of index i
-#endif
 
 namespace fhe_amd {
 
@@ -606,15 +603,6 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m = fresh_nq(m0);
         const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]);
-#if FHE_GINX_L2PF
-        uint32_t pf0 = 0, pf1 = 0;
-        if (i + 1 < g.n) {  // this wave's quarter (16 KB) of index i+1's 64 KB of keys
-            const uint32_t* nb = reinterpret_cast<const uint32_t*>(bsk) + (size_t)(i + 1) * 16384 + wave * 4096 + lane * 32;
-            pf0 = nb[0];
-            pf1 = nb[2048];
-        }
-        asm volatile("" ::: "memory");
-#endif
         uint32_t dA[32], dB[32];
         // --- iNTT of a copy of acc -> canonical COEF (AddToAccCGGI :104-106)
 #pragma unroll
@@ -714,9 +702,6 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
 #undef KP
 #undef KN
         }
-#if FHE_GINX_L2PF
-        asm volatile("" ::"v"(pf0), "v"(pf1));
-#endif
     }
 
     if (ACCIO) {
