@@ -196,6 +196,11 @@ def rooflines(method_name, B, br_ms, ks_ms):
     valu = {
         "kernel": k1, "bound": "valu-int-mul", "achieved": round(mm_rate, 3),
         "peak": round(VALU_MODMUL_PEAK_T, 4), "unit": "T modmul/s", "frac": round(mm_rate / VALU_MODMUL_PEAK_T, 4),
+        "valu_busy_pmc": pmc_valu_busy(k1),
+        "valu_busy_basis": "fraction of the kernel's cycles each SIMD issues VALU instructions (rocprofv3 PMC "
+                           "SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs over GRBM_GUI_ACTIVE / 8 XCDs, committed summary "
+                           "profiles/*pmc_traffic.json): the kernel is issue-bound at its instruction mix when this "
+                           "is near 1",
         "basis": "SURVEY 8(a) modular multiplies per gate x gates / launch time; peak = 256 CUs x 4 SIMDs x "
                  "16 lanes/clk (half-rate 32-bit multiplies) x 2.4 GHz / 3 multiplies per modmul; the measured "
                  "multiply issue rate (profiles/r01_ubench_valu_rates.txt, 35.1 T lane-op/s) is 11.7 T modmul/s",
@@ -355,21 +360,33 @@ def env_rank():
     return env()
 
 
-def pmc_traffic(kernel, batch):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc_traffic.json,
-    written by tools/pmc_traffic.py), scaled to this batch; None if not measured.  The newest
-    summary (by file name: r02 after r01) wins."""
+def pmc_summary(kernel, field):
+    """`field` of `kernel` in the newest committed rocprofv3 PMC summary that has it
+    (profiles/*pmc_traffic.json, written by tools/pmc_traffic.py; r03 after r02), with that
+    summary's batch; (None, None) if not measured."""
     import glob
-    best = None
+    best = (None, None)
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
         k = d.get("kernels", {}).get(kernel)
-        if k and k.get("batch"):
-            best = k["hbm_bytes_per_launch"] / k["batch"] * batch
-    return None if best is None else round(best)
+        if k and k.get("batch") and k.get(field) is not None:
+            best = (k[field], k["batch"])
+    return best
+
+
+def pmc_traffic(kernel, batch):
+    """HBM bytes per launch from the committed PMC summary, scaled to this batch; None if not measured"""
+    v, b = pmc_summary(kernel, "hbm_bytes_per_launch")
+    return None if v is None else round(v / b * batch)
+
+
+def pmc_valu_busy(kernel):
+    """the kernel's VALU issue fraction from the committed PMC summary (SQ_ACTIVE_INST_VALU x 4 per SIMD
+    over GRBM_GUI_ACTIVE per XCD, tools/pmc_traffic.py); None if not measured"""
+    return pmc_summary(kernel, "valu_busy")[0]
 
 
 def ntt_rooflines(NttPlan, torch, dev, stream, count, reps=20):
@@ -394,7 +411,8 @@ def ntt_rooflines(NttPlan, torch, dev, stream, count, reps=20):
             name = kname.format("inv" if inv else "fwd")
             out.append({"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "traffic": pmc_traffic(name, count), "launch_us": round(ms * 1e3, 3), "polys": count,
+                        "traffic": pmc_traffic(name, count), "valu_busy_pmc": pmc_valu_busy(name),
+                        "launch_us": round(ms * 1e3, 3), "polys": count,
                         "Q": Q, "alg_bytes_per_launch": count * NTT_BYTES_PER_POLY})
         plan.close()
     return out

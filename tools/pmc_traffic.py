@@ -5,6 +5,8 @@ FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section), re-measured here by bu
 streaming 512 MiB with 4-, 8- and 16-byte lanes reports 262,1xx KiB each; WRITE_SIZE reports the
 bytes exactly.  FETCH_SIZE counts L2 -> fabric requests, so Infinity-Cache hits are included:
 the figure is an upper bound on DRAM traffic.
+valu_busy (pass p1) = SQ_ACTIVE_INST_VALU x 4 (the counter's quad-cycles) / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8
+XCDs): the fraction of the kernel's cycles each SIMD spends issuing VALU instructions.
 usage: python tools/pmc_traffic.py <round tag> <batch> [pmc dir]"""
 import collections
 import csv
@@ -63,6 +65,13 @@ for k in fetch:
         "kernel": key, "batch": NTT_POLYS if "ntt" in key else batch, "launches": len(fetch[k]),
         "fetch_kib": round(f, 1), "write_kib": round(w, 1),
         "hbm_bytes_per_launch": round(2 * f * 1024 + w * 1024)}
+valu, gui, insts = per_kernel("p1", "SQ_ACTIVE_INST_VALU"), per_kernel("p1", "GRBM_GUI_ACTIVE"), per_kernel("p1", "SQ_INSTS_VALU")
+for k in valu:
+    key = short(k)
+    if key in out["kernels"] and gui.get(k):
+        v, gcy = sum(valu[k]) / len(valu[k]), sum(gui[k]) / len(gui[k])
+        out["kernels"][key]["valu_busy"] = round(v * 4 / 1024 / (gcy / 8), 4)
+        out["kernels"][key]["valu_insts_per_launch"] = round(sum(insts[k]) / len(insts[k]))
 path = os.path.join("profiles", f"{tag}_pmc_traffic.json")
 json.dump(out, open(path, "w"), indent=1)
 print(json.dumps(out["kernels"], indent=1))
