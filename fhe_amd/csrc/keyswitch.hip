@@ -104,19 +104,26 @@ constexpr int kKsCols  = FHE_KS_COLS;           // columns per workgroup (packed
 constexpr int kKsRowB  = kKsCols * 2 + (FHE_KS_B64 ? 8 : 16);
 constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
 constexpr int kKsDigits = 3;                    // digitsKS
-#ifndef FHE_KS_IPR
-#define FHE_KS_IPR 4
+// Tile shapes (G gates per workgroup, IPR values of i per round at baseKS = 32), by batch size
+// (round 3, profiles/r03_ab_keyswitch.txt, per launch at 65,536 / 8192 / 1024 gates):
+//   G 256, IPR 4 (104 KB of LDS, one workgroup per CU):       6.64 ms / 0.82 ms / 125 + 11 us
+//   G 512, IPR 4:                                              4.58 ms / 0.95 ms /  79 + 11 us
+//   G 512, IPR 2 (52 KB: several workgroups per CU):           3.27 ms / 1.12 ms /  73 + 20 us
+// and at 16,384 gates 1.70 ms (G 256, IPR 4) vs 1.23 ms (G 512, IPR 2); so the row split (below 4096
+// gates) runs G 512 / IPR 4, kKsWideBatch gates and more G 512 / IPR 2, and the batches between them
+// G 256 / IPR 4 (enough workgroups to fill the chip).
+constexpr int kKsIPR = 4;                 // values of i per round (4: one uint4 of a_i) at baseKS = 32
+#ifndef FHE_KS_WIDE_BATCH
+#define FHE_KS_WIDE_BATCH 16384
 #endif
-#ifndef FHE_KS_G
-#define FHE_KS_G 256
-#endif
-constexpr int kKsIPR   = FHE_KS_IPR;            // values of i per round (4: one uint4 of a_i) at baseKS = 32
+constexpr uint32_t kKsWideBatch = FHE_KS_WIDE_BATCH;  // from here: G 512, IPR 2
+constexpr int kKsSplitG = 512;            // the row split's gate tile
 // LOGB = log2(baseKS): 5 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 6 (STD128_3/4,
 // LPF_STD128Q: 64 slices, 2 values of i per round so that the double buffer keeps the same 104 KB;
 // slices d and d + 32 share a bank slot, a 2-way conflict)
-template <int LOGB> struct KsShape {
+template <int LOGB, int IPR> struct KsShape {
     static constexpr int base  = 1 << LOGB;
-    static constexpr int ipr   = LOGB == 5 ? kKsIPR : 2;
+    static constexpr int ipr   = LOGB == 5 ? IPR : 2;
     static constexpr int step  = ipr * kKsDigits;                 // (i, j) steps per round / LDS buffer / barrier
     static constexpr int parts = base * kKsCols * 2 / 16;         // 16-byte parts staged per step
 };
@@ -126,12 +133,12 @@ template <int LOGB> struct KsShape {
 // (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
 // 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
-template <int G, bool SPLIT, int LOGB>
+template <int G, bool SPLIT, int LOGB, int IPR>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                       uint64_t* __restrict__ b_out, uint32_t* __restrict__ part) {
-    using S_ = KsShape<LOGB>;
+    using S_ = KsShape<LOGB, IPR>;
     constexpr int kKsParts = S_::parts, kKsStep = S_::step, kIPR = S_::ipr, kBase = S_::base;
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
@@ -285,12 +292,16 @@ __global__ void __launch_bounds__(512)
 
 // row-split factor of the tiled kernel for `count` gates: enough workgroups for 4 per CU, at
 // least 8 rounds each, within the scratch the caller holds (part_words u32)
-uint32_t keyswitch_split(size_t count, uint32_t n, uint32_t N, size_t part_words) {
-    const size_t tiles = ((count + FHE_KS_G - 1) / FHE_KS_G) * (ksk_width(n) / kKsCols);
+static uint32_t split_factor(size_t count, uint32_t n, uint32_t N, size_t part_words, uint32_t G) {
+    const size_t tiles = ((count + G - 1) / G) * (ksk_width(n) / kKsCols);
     uint32_t S = 1;
     while (tiles * S < 1024 && N / kKsIPR / (2 * S) >= 8 && (size_t)2 * S * count * (ksk_width(n) / 2) <= part_words)
         S *= 2;
     return S;
+}
+// (the baseKS = 32 row split's gate tile)
+uint32_t keyswitch_split(size_t count, uint32_t n, uint32_t N, size_t part_words) {
+    return split_factor(count, n, N, part_words, kKsSplitG);
 }
 
 hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint16_t* ksk,
@@ -309,13 +320,21 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     if (tile == 0) tile = g.count >= 4096 || part ? 256 : 1;
     if (tile > 1 && ((logBase != 5 && logBase != 6) || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
     if (tile > 1) {
-        const uint32_t S = part ? keyswitch_split(g.count, g.n, g.N, part_words) : 1;
-        const dim3 grid((g.count + FHE_KS_G - 1) / FHE_KS_G, W / kKsCols, S);
-#define FHE_KS_LAUNCH(SP, LB)                                                                                   \
-    hipLaunchKernelGGL((k_keyswitch_tiled<FHE_KS_G, SP, LB>), grid, dim3(FHE_KS_G), 0, s, g, ksk, ms_a, ms_b, q_out, \
+        // baseKS = 32: the tile shape by batch size (kKsIPR above); baseKS = 64: G 256
+        const uint32_t Gs = logBase == 5 ? (uint32_t)kKsSplitG : 256u;
+        const uint32_t S = part ? split_factor(g.count, g.n, g.N, part_words, Gs) : 1;
+        const uint32_t G = S > 1 ? Gs : logBase == 5 && g.count >= kKsWideBatch ? 512u : 256u;
+        const dim3 grid((g.count + G - 1) / G, W / kKsCols, S);
+#define FHE_KS_LAUNCH(G_, SP, LB, IPR_)                                                                           \
+    hipLaunchKernelGGL((k_keyswitch_tiled<G_, SP, LB, IPR_>), grid, dim3(G_), 0, s, g, ksk, ms_a, ms_b, q_out,      \
                        a_out, b_out, SP ? part : nullptr)
-        if (logBase == 5) { if (S > 1) FHE_KS_LAUNCH(true, 5); else FHE_KS_LAUNCH(false, 5); }
-        else { if (S > 1) FHE_KS_LAUNCH(true, 6); else FHE_KS_LAUNCH(false, 6); }
+        if (logBase == 5) {
+            if (S > 1) FHE_KS_LAUNCH(kKsSplitG, true, 5, 4);
+            else if (G == 512) FHE_KS_LAUNCH(512, false, 5, 2);
+            else FHE_KS_LAUNCH(256, false, 5, 4);
+        } else {
+            if (S > 1) FHE_KS_LAUNCH(256, true, 6, 2); else FHE_KS_LAUNCH(256, false, 6, 2);
+        }
 #undef FHE_KS_LAUNCH
         if (S > 1) {
             hipError_t e = hipGetLastError();

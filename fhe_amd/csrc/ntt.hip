@@ -67,6 +67,16 @@ namespace {
 constexpr int kWTile = 1024 + 64;  // words per wave
 FHE_DEV int wt(int x) { return x + ((x >> 6) << 2); }
 
+// k_ntt1024w64: staggered wave priorities.  With equal priority the waves sharing a SIMD interleave,
+// finish together and leave all their stores for the end of the pass; ranked (waves 4..7 of a
+// workgroup above 0..3, two per SIMD each), the high pair finishes first and its stores overlap the
+// low pair's arithmetic.  Round 3, interleaved A/B (profiles/r03_ab_ntt_prio.txt): 20.8 / 20.6 ->
+// 20.0 / 20.2 us per 60-bit forward / inverse pass; four levels (by grid half too) and the 32-bit
+// kernel gain nothing.
+FHE_DEV void ntt_stagger(int wv) {
+    if (__builtin_amdgcn_readfirstlane(wv >> 2)) __builtin_amdgcn_s_setprio(1);
+}
+
 // arithmetic policies of k_ntt1024w: Shoup lazy (any Q < 2^30) or signed Montgomery (Q < 2^27:
 // five VALU instructions per butterfly, no reductions in the forward transform)
 struct NttK {
@@ -779,6 +789,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
     // stages (uniform twiddles, no LDS) on the rows as they land, before the table's barrier
     Raw bufA;
     if (poly < count) load(bufA, poly);
+    ntt_stagger(wv);
     const ulonglong2 tw0 = tab[threadIdx.x], tw1 = tab[threadIdx.x + 512];  // 512 threads (launch_wave64)
     const bool pre = !INV && poly < count;
     if (pre) stage_a(bufA);
