@@ -151,13 +151,15 @@ def params(paramset, method):
 
 def kernel_path(paramset, method):
     """the accumulator kernels (paramset, method) runs on, as the engine chooses them
-    (fhe_hip_params.kernel): 1 = 32-bit one-wave, 2 = 32-bit split (digitsG = 4), 0 = 64-bit"""
+    (fhe_hip_params.kernel): 1 = 32-bit one-wave, 2 = 32-bit split (digitsG = 4), 3 = one gate per
+    workgroup in 32-bit residues, 0 = one gate per workgroup in 64-bit residues"""
     return params(paramset, method).kernel
 
 
 def uses_fast_kernels(paramset, method):
-    """True when (paramset, method) runs on one of the 32-bit accumulator kernels"""
-    return kernel_path(paramset, method) != 0
+    """True when (paramset, method) runs on one of the register-resident 32-bit accumulator kernels
+    (one wave or two waves per gate)"""
+    return kernel_path(paramset, method) in (1, 2)
 
 
 def _u64(a):

@@ -240,7 +240,7 @@ WD void ntt_inv(typename A::T* buf, const A& a) {
 // last pass (N = 2048: 3 barriers per transform instead of 6).
 template <int LOGN, int NB, class A>
 WD void ntt_fwd4(typename A::T* buf, const A& a) {
-    constexpr int N = 1 << LOGN, T = N / 4;
+    constexpr int N = 1 << LOGN;
     const int u = (int)threadIdx.x;  // one unit per thread per polynomial
 #pragma unroll 1
     for (int s = 0; s + 1 < LOGN; s += 2) {

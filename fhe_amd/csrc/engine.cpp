@@ -25,6 +25,12 @@ bool Engine::fast_path(const Params& p) {
            p.qKS <= 65536 && p.n < 1024;
 }
 
+bool Engine::narrow_set(const Params& p) {
+    // the 64-bit accumulator's 32-bit policy (bootstrap_wide.hip A32): residues and digit x key sums
+    // (< digitsG2 Q^2 < Q 2^32) in 32-bit words
+    return p.Q < (1ull << 30) && (uint64_t)p.digitsG2 * p.Q < (1ull << 32);
+}
+
 bool Engine::g3_set(const Params& p) {
     // digit fields of d + C in 32 bits (bootstrap.hip decompose_n): 4 g <= 32 and C + Q < 2^32
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
@@ -105,8 +111,7 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         FHE_HIP_CHECK(hipSetDevice(device_));
         FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         const char* nw = std::getenv("FHE_HIP_NARROW");  // "0": keep 64-bit residues (A/B, tests)
-        narrow_ = !(nw && std::string(nw) == "0") && p_.Q < (1ull << 30) &&
-                  (uint64_t)p_.digitsG2 * p_.Q < (1ull << 32);
+        narrow_ = !(nw && std::string(nw) == "0") && narrow_set(p_);
         build_tables_wide();
         set_base(p_.baseG);
         if (g3_set(p_)) {

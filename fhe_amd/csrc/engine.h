@@ -55,6 +55,7 @@ public:
     bool wide() const { return wide_; }
     // the 32-bit kernels' range: N = 1024, Q < 2^28, digitsG = 3, power-of-two q, qKS <= 2^16, n < 1024
     static bool fast_path(const Params& p);
+    static bool narrow_set(const Params& p);  // the 64-bit accumulator runs its 32-bit policy (A32)
     // the digitsG = 4 sets at N = 1024, Q < 2^27 the split kernels take (K1s / K1m)
     static bool g3_set(const Params& p);
 

@@ -89,7 +89,10 @@ typedef struct {
     uint32_t paramset, method, n, N, q, baseKS, digitsKS, baseG, digitsG, numAutoKeys, keyDist;
     uint32_t kernel;  /* the accumulator kernels the set runs on: 1 = 32-bit, one wave per gate (N = 1024,
                          Q < 2^28, digitsG = 3); 2 = 32-bit split, two waves per gate (digitsG = 4, N = 1024,
-                         Q < 2^27); 0 = 64-bit accumulator (every other set, the large-precision family) */
+                         Q < 2^27); 3 = the one-gate-per-workgroup accumulator with 32-bit residues
+                         (Q < 2^30, digitsG2 Q < 2^32: the N = 2048 STD256 / STD256Q rows, TOY, ...);
+                         0 = the same accumulator with 64-bit residues (every other set, the
+                         large-precision family) */
     uint64_t Q, psi, qKS, bsk_words, ksk_rows;  /* ksk_rows: of the raw layout (timeOptimization: 3 keys) */
 } fhe_hip_params;
 /* The large-precision family GenerateBinFHEContext(set, arbFunc, logQ, N, GINX, false)

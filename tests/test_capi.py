@@ -33,3 +33,16 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
                 txt = open(os.path.join(d, f), errors="ignore").read()
                 assert "tfhe_oracle" not in txt and "libfhe_ref" not in txt and "oracle_lib" not in txt, f
+
+
+def test_kernel_path_per_parameter_set():
+    """fhe_hip_params.kernel names the accumulator the engine picks (Engine::fast_path / g3_set /
+    narrow_set): no GPU needed, the parameter table is host data"""
+    from fhe_amd import binfhe as bf
+    STD128_3, STD192, STD256 = 4, 9, 15   # binfhe-constants.h:49-89
+    assert bf.kernel_path(bf.STD128, bf.GINX) == 1
+    assert bf.kernel_path(bf.STD128_LMKCDEY, bf.LMKCDEY) == 1
+    assert bf.kernel_path(STD128_3, bf.GINX) == 2
+    assert bf.kernel_path(STD256, bf.GINX) == 3       # N = 2048, 29-bit Q: 32-bit residues
+    assert bf.kernel_path(STD192, bf.GINX) == 0       # 37-bit Q: 64-bit residues
+    assert bf.uses_fast_kernels(bf.STD128, bf.GINX) and not bf.uses_fast_kernels(STD256, bf.GINX)

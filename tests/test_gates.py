@@ -194,20 +194,24 @@ def test_gpu_lmkcdey_on_std128_vs_oracle(restatement):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", SETS)
 def test_gpu_keyswitch_kernels_vs_oracle(name, restatement):
-    """both key-switch kernels (per-gate below 4096 ciphertexts, gate-tiled at and above,
-    keyswitch.hip) on uniform inputs mod qKS, incl. a ragged last tile, vs the oracle."""
+    """every tile shape of the gate-tiled key switch (keyswitch.hip launch_keyswitch: the row split
+    with 512-gate tiles below 4096 ciphertexts, 256-gate tiles from 4096, 512-gate tiles with two
+    values of i per round from 16,384) on uniform inputs mod qKS, incl. a ragged last tile, vs the
+    oracle.  Ciphertexts are switched independently, so at 16,384 + 259 the oracle checks the first
+    tile, a middle one and the ragged end."""
     from oracle_lib import Restatement
     g, keys, _ = fixture(name)
     O = Restatement(int(g["paramset"]), int(g["method"]))
     e = engine(name)
     P = e.params
     rng = np.random.default_rng(77)
-    for count in (300, 4096 + 259):
+    for count in (300, 4096 + 259, 16384 + 259):
         a = rng.integers(0, P.qKS, (count, P.N), dtype=np.uint64)
         b = rng.integers(0, P.qKS, count, dtype=np.uint64)
         ga, gb = e.keyswitch(a, b)
-        oa, ob = O.keyswitch(keys.kskA, keys.kskB, a, b)
-        assert np.array_equal(ga, oa) and np.array_equal(gb, ob), count
+        rows = np.arange(count) if count < 16384 else np.r_[0:512, 8000:8512, count - 771:count]
+        oa, ob = O.keyswitch(keys.kskA, keys.kskB, a[rows], b[rows])
+        assert np.array_equal(ga[rows], oa) and np.array_equal(gb[rows], ob), count
 
 
 @pytest.mark.gpu
