@@ -153,6 +153,15 @@ struct A32 {
     WD T fwd_out(T x) const { return csub(csub(x, 2 * Q), Q); }
 };
 
+// Workgroup barrier for the accumulator kernels, whose threads share data through LDS only: a
+// workgroup-scope fence on LDS ("local") waits for LDS accesses alone, so global loads issued before
+// it (the A32 gate kernel's next-level keys) stay in flight across it; __syncthreads would drain them
+WD void wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // A32 gate kernel: copy the tables into LDS and point the policy at them (+2.6% at STD256).
 // Engine::build_tables_wide stores them contiguously (tab, tabS, tabI, tabIS: N words each, then
 // psiM: 2N words); mono = false would leave the monomial table out
@@ -161,7 +170,7 @@ WD void stage_tables(A& a, typename A::T* st, int N, bool mono) {
     if constexpr (A::kLds) {
         const int words = (mono ? 6 : 4) * N;
         for (int i = threadIdx.x; i < words; i += blockDim.x) st[i] = a.tab[i];
-        __syncthreads();
+        wg_sync();
         a.tab = st;
         a.tabS = st + N;
         a.tabI = st + 2 * N;
@@ -203,7 +212,7 @@ WD void ntt_fwd(typename A::T* buf, const A& a) {
                 buf[p * N + j + t] = y;
             }
         }
-        __syncthreads();
+        wg_sync();
     }
 }
 // Gentleman-Sande inverse (InverseTransformFromBitReverseInPlace :511-624) WITHOUT the final
@@ -228,7 +237,7 @@ WD void ntt_inv(typename A::T* buf, const A& a) {
                 buf[p * N + j + t] = y;
             }
         }
-        __syncthreads();
+        wg_sync();
     }
 }
 
@@ -271,7 +280,7 @@ WD void ntt_fwd4(typename A::T* buf, const A& a) {
         // pass or the remapped radix-2 stage (not the end of the transform)
         const bool more4 = s + 3 < LOGN, r2next = (LOGN & 1) && s + 3 == LOGN;
         if (logt <= 7 && (more4 || r2next)) wave_sync();
-        else __syncthreads();
+        else wg_sync();
     }
     if (LOGN & 1) {  // last stage: t = 1, m = N / 2; wave w takes butterflies [128 w, 128 w + 128)
 #pragma unroll
@@ -287,7 +296,7 @@ WD void ntt_fwd4(typename A::T* buf, const A& a) {
                 b[1] = a.fwd_out(y);
             }
         }
-        __syncthreads();
+        wg_sync();
     }
 }
 template <int LOGN, int NB, class A>
@@ -317,7 +326,7 @@ WD void ntt_inv4(typename A::T* buf, const A& a) {
         }
         // within this wave's chunk while this pass and the next have t <= 64 (s + 2 <= 6)
         if (s + 2 <= 6 && s + 3 < LOGN) wave_sync();
-        else __syncthreads();
+        else wg_sync();
     }
     if (LOGN & 1) {  // last stage: t = N / 2, m = 1
         const auto w = a.tabI[1], ws = a.tabIS[1];
@@ -333,7 +342,7 @@ WD void ntt_inv4(typename A::T* buf, const A& a) {
                 b[N / 2] = y;
             }
         }
-        __syncthreads();
+        wg_sync();
     }
 }
 
@@ -392,7 +401,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
             }
             buf[x] = (T)v;
         }
-        __syncthreads();
+        wg_sync();
         fwd<LOGN, 1>(buf, a);
 #pragma unroll
         for (int r = 0; r < S; ++r) {
@@ -407,13 +416,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
     for (uint32_t i = 0; i < g.n; ++i) {
         const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)gi[i]);
         if (m == 0) continue;  // AddToAccCGGI with X^0 - 1 = 0 leaves acc unchanged
-        __syncthreads();
+        wg_sync();
 #pragma unroll
         for (int r = 0; r < S; ++r) {
             buf[t + TH * r]     = acc0[r];
             buf[N + t + TH * r] = acc1[r];
         }
-        __syncthreads();
+        wg_sync();
         inv<LOGN, 2>(buf, a);
         // SignedDigitDecompose state: centred value, lowest digit dropped
         D d[2][S];
@@ -436,7 +445,24 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
         const T* key = bsk + (size_t)i * key_stride;
 #pragma unroll 1
         for (uint32_t L = 0; 2 * L < dG2; ++L) {
-            __syncthreads();  // previous readers of buf are done
+            // A32: this level's 32 key words per thread requested before its digit transform, so they
+            // land during it (wg_sync's LDS-only barriers do not drain them): +1.2% on the N = 2048
+            // GINX rows, 121 VGPRs (profiles/r03_ab_wide.txt; the op-list kernel's EXT keys the same
+            // way lose 1% at 6 waves per SIMD with spills, 7% at 5)
+            constexpr bool kpf = sizeof(T) == 4;
+            T kr[kpf ? 2 : 1][2][2][kpf ? S : 1];
+            if (kpf) {
+#pragma unroll
+                for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int w = 0; w < 2; ++w)
+#pragma unroll
+                            for (int r = 0; r < S; ++r)
+                                kr[sg][c][w][r] = key[((size_t)(sg * dG2 + 2 * L + w) * 2 + c) * N + t + TH * r];
+            }
+            wg_sync();  // previous readers of buf are done
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -447,7 +473,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
                     if (r0 < 0) r0 += (D)Q;
                     buf[p * N + t + TH * r] = (T)r0;
                 }
-            __syncthreads();
+            wg_sync();
             fwd<LOGN, 2>(buf, a);
 #pragma unroll
             for (int r = 0; r < S; ++r) {
@@ -458,8 +484,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
                         const T* k0 = key + ((size_t)(sg * dG2 + 2 * L) * 2 + c) * N;
-                        A::mac(acc[sg][c][r], x0, k0[j]);
-                        A::mac(acc[sg][c][r], x1, k0[2 * N + j]);  // row 2L + 1
+                        A::mac(acc[sg][c][r], x0, kpf ? kr[sg][c][0][kpf ? r : 0] : k0[j]);
+                        A::mac(acc[sg][c][r], x1, kpf ? kr[sg][c][1][kpf ? r : 0] : k0[2 * N + j]);  // row 2L + 1
                     }
             }
         }
@@ -494,13 +520,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
     }
     // extraction (binfhe-base-scheme.cpp:110-121, :616-626): Transpose(acc0) then COEF: coefficient
     // k of acc0(X^-1) is -a_(N-k) (k >= 1), a_0 for k = 0; b = b_const + acc1[0]
-    __syncthreads();
+    wg_sync();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         buf[t + TH * r]     = acc0[r];
         buf[N + t + TH * r] = acc1[r];
     }
-    __syncthreads();
+    wg_sync();
     inv<LOGN, 2>(buf, a);
     uint64_t* oa = ext_a + (size_t)gate * N;
 #pragma unroll
@@ -574,7 +600,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
             }
             buf[x] = (T)v;
         }
-        __syncthreads();
+        wg_sync();
         fwd<LOGN, 1>(buf, a);
 #pragma unroll
         for (int r = 0; r < S; ++r) {
@@ -606,14 +632,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
         for (int c = 0; c < 2; ++c)
 #pragma unroll
             for (int r = 0; r < S; ++r) U[c][r] = A::zero();
-        __syncthreads();
+        wg_sync();
         if (DM || !(op & 0x8000u)) {
 #pragma unroll
             for (int r = 0; r < S; ++r) {
                 buf[t + TH * r]     = acc0[r];
                 buf[N + t + TH * r] = acc1[r];
             }
-            __syncthreads();
+            wg_sync();
             inv<LOGN, 2>(buf, a);
             D d[2][S];
 #pragma unroll
@@ -623,12 +649,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
             const T* key = bsk + (size_t)op * dG2 * 2 * N;
 #pragma unroll 1
             for (uint32_t L = 0; L < dA; ++L) {
-                __syncthreads();
+                wg_sync();
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
                     for (int r = 0; r < S; ++r) buf[p * N + t + TH * r] = digit(d[p][r]);
-                __syncthreads();
+                wg_sync();
                 fwd<LOGN, 2>(buf, a);
 #pragma unroll
                 for (int r = 0; r < S; ++r) {
@@ -658,7 +684,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
                 buf[t + TH * r]     = acc0[r];
                 buf[N + t + TH * r] = acc1[r];
             }
-            __syncthreads();
+            wg_sync();
             T a0[S];
 #pragma unroll
             for (int r = 0; r < S; ++r) {
@@ -666,10 +692,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
                 a0[r]   = buf[src];
                 acc1[r] = buf[N + src];
             }
-            __syncthreads();
+            wg_sync();
 #pragma unroll
             for (int r = 0; r < S; ++r) buf[t + TH * r] = a0[r];
-            __syncthreads();
+            wg_sync();
             inv<LOGN, 1>(buf, a);
             D d[S];
 #pragma unroll
@@ -677,10 +703,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
             const T* key = autok + (size_t)ta * dA * 2 * N;
 #pragma unroll 1
             for (uint32_t L = 0; L < dA; ++L) {
-                __syncthreads();
+                wg_sync();
 #pragma unroll
                 for (int r = 0; r < S; ++r) buf[t + TH * r] = digit(d[r]);
-                __syncthreads();
+                wg_sync();
                 fwd<LOGN, 1>(buf, a);
 #pragma unroll
                 for (int r = 0; r < S; ++r) {
@@ -708,13 +734,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
         return;
     }
     // extraction as k_blind_rotate_wide
-    __syncthreads();
+    wg_sync();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         buf[t + TH * r]     = acc0[r];
         buf[N + t + TH * r] = acc1[r];
     }
-    __syncthreads();
+    wg_sync();
     inv<LOGN, 2>(buf, a);
     uint64_t* oa = ext_a + (size_t)gate * N;
 #pragma unroll
