@@ -236,6 +236,46 @@ def test_gpu_large_batch_truth_and_determinism(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["std128", "lmkcdey"])
+def test_gpu_pipelined_host_batch_matches_device(name):
+    """host-buffer batches of more than one 8192-gate chunk run the copy/compute pipeline
+    (Engine::eval_gate_host): a ragged 4-chunk batch == one device-resident launch, bit-exact,
+    and every gate decrypts to its truth value"""
+    import ctypes
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import check, lib, ptr, vp
+    g, keys, _ = fixture(name)
+    ps, m = int(g["paramset"]), int(g["method"])
+    e = engine(name)
+    count = 3 * 8192 + 123
+    rng = np.random.default_rng(11)
+    x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+    a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 41)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 42)
+    ao, bo = e.eval_gate(bf.NAND, a1, b1, a2, b2)
+
+    def dalloc(nbytes):
+        d = vp()
+        check(lib().fhe_hip_alloc(0, nbytes, ctypes.byref(d)))
+        return d.value
+    bufs = [dalloc(x.nbytes) for x in (a1, b1, a2, b2)]
+    dao, dbo = dalloc(ao.nbytes), dalloc(bo.nbytes)
+    try:
+        for d, x in zip(bufs, (a1, b1, a2, b2)):
+            check(lib().fhe_hip_copy_to_device(vp(d), ptr(x), x.nbytes))
+        e.eval_gate_device(bf.NAND, count, *bufs, dao, dbo)
+        check(lib().fhe_hip_synchronize(0))
+        ao_d, bo_d = np.zeros_like(ao), np.zeros_like(bo)
+        check(lib().fhe_hip_copy_to_host(ptr(ao_d), vp(dao), ao_d.nbytes))
+        check(lib().fhe_hip_copy_to_host(ptr(bo_d), vp(dbo), bo_d.nbytes))
+    finally:
+        for d in bufs + [dao, dbo]:
+            check(lib().fhe_hip_free(vp(d)))
+    assert np.array_equal(ao, ao_d) and np.array_equal(bo, bo_d)
+    assert np.array_equal(bf.decrypt(ps, m, keys.sk, ao, bo), TRUTH[3](x1, x2).astype(np.int64))
+
+
+@pytest.mark.gpu
 def test_gpu_binfhecontext_api_truth_tables():
     """the reference-shaped API (UnitTestFHEW.cpp:175-239 truth tables)."""
     from fhe_amd import binfhe as bf
