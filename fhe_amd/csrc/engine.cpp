@@ -3,7 +3,6 @@
 
 #include <algorithm>
 #include <cstdlib>
-#include <cstring>
 #include <string>
 
 #include "keygen.h"
@@ -150,9 +149,6 @@ Engine::~Engine() {
                       (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_})
         if (ptr) (void)hipFree(ptr);
     if (order_ev_) (void)hipEventDestroy(order_ev_);
-    if (h2d_stream_) (void)hipStreamDestroy(h2d_stream_);
-    if (d2h_stream_) (void)hipStreamDestroy(d2h_stream_);
-    if (pin_) (void)hipHostFree(pin_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -953,28 +949,6 @@ void Engine::eval_gate_device(int gate, size_t count, const uint64_t* a1, const 
     keyswitch_workspace_device(count, a_out, b_out, s);
 }
 
-// Host-buffer gate batches of more than one chunk run as a copy/compute pipeline through two pinned
-// staging slots: while chunk k bootstraps on the compute stream, the host copies chunk k + 1's
-// inputs into a pinned slot (SDMA H2D on one copy stream) and chunk k - 1's outputs out of the
-// other (D2H on a second copy stream), so the ~12 KB per gate of PCIe traffic hides behind the
-// blind rotation.  One-shot pageable copies around one launch cost 16.6% at 65,536 gates, and
-// pageable copies on a side stream still 12.2% (tools/seam_time.py, profiles/r03_seam_*.txt).
-// 8192 gates is four full waves-per-SIMD rounds of K1; each chunk is an independent
-// eval_gate_device call, so the outputs are the one-launch outputs bit for bit.
-constexpr size_t kHostChunk = 8192;
-
-namespace {
-void par_copy(uint64_t* dst, const uint64_t* src, size_t words) {
-    constexpr size_t kBlk = (size_t)1 << 16;  // 512 KiB per task
-    const long nb = (long)((words + kBlk - 1) / kBlk);
-#pragma omp parallel for schedule(static)
-    for (long b = 0; b < nb; ++b) {
-        const size_t o = (size_t)b * kBlk;
-        std::memcpy(dst + o, src + o, std::min(kBlk, words - o) * sizeof(uint64_t));
-    }
-}
-}  // namespace
-
 void Engine::eval_gate_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
                             const uint64_t* b2, uint64_t* a_out, uint64_t* b_out) {
     if (count == 0) return;
@@ -987,90 +961,14 @@ void Engine::eval_gate_host(int gate, size_t count, const uint64_t* a1, const ui
     uint64_t* dao = db2 + count;
     uint64_t* dbo = dao + count * p_.N;
     FHE_HIP_CHECK(hipSetDevice(device_));
-    auto gates = [&](size_t o, size_t c) {
-        eval_gate_device(gate, c, da1 + o * n, db1 + o, da2 + o * n, db2 + o, dao + o * n, dbo + o, stream_);
-    };
-    // FHE_HIP_HOST_PIPELINE=0: one-shot copies around one launch (A/B, tools/seam_time.py)
-    static const bool pipeline = [] {
-        const char* v = std::getenv("FHE_HIP_HOST_PIPELINE");
-        return !(v && std::string(v) == "0");
-    }();
-    if (count <= kHostChunk || !pipeline) {
-        FHE_HIP_CHECK(hipMemcpyAsync(da1, a1, count * n * 8, hipMemcpyHostToDevice, stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(db1, b1, count * 8, hipMemcpyHostToDevice, stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(da2, a2, count * n * 8, hipMemcpyHostToDevice, stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(db2, b2, count * 8, hipMemcpyHostToDevice, stream_));
-        gates(0, count);
-        FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * n * 8, hipMemcpyDeviceToHost, stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
-        FHE_HIP_CHECK(hipStreamSynchronize(stream_));
-        return;
-    }
-    constexpr size_t C = kHostChunk;
-    const size_t inW = 2 * C * n + 2 * C, outW = C * n + C;  // words per pinned input / output slot
-    if (!h2d_stream_) FHE_HIP_CHECK(hipStreamCreateWithFlags(&h2d_stream_, hipStreamNonBlocking));
-    if (!d2h_stream_) FHE_HIP_CHECK(hipStreamCreateWithFlags(&d2h_stream_, hipStreamNonBlocking));
-    if (pin_words_ < 2 * (inW + outW)) {
-        if (pin_) FHE_HIP_CHECK(hipHostFree(pin_));
-        pin_ = nullptr;
-        pin_words_ = 0;
-        FHE_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_), 2 * (inW + outW) * 8, hipHostMallocDefault));
-        pin_words_ = 2 * (inW + outW);
-    }
-    ensure_work(C);  // any workspace growth (a device sync) before the pipeline starts
-    const size_t K = (count + C - 1) / C;
-    // per chunk k: ev[3k] inputs on the device (pinned input slot k & 1 free again), ev[3k + 1]
-    // gates done, ev[3k + 2] outputs in pinned output slot k & 1.  On every exit path the three
-    // streams drain before the events go (the pinned slots and the caller's buffers are in use).
-    struct Events {
-        std::vector<hipEvent_t> ev;
-        hipStream_t s[3];
-        ~Events() {
-            for (hipStream_t x : s) (void)hipStreamSynchronize(x);
-            for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-        }
-    } E{{}, {h2d_stream_, stream_, d2h_stream_}};
-    E.ev.reserve(3 * K);
-    for (size_t i = 0; i < 3 * K; ++i) {
-        hipEvent_t e;
-        FHE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        E.ev.push_back(e);
-    }
-    auto chunk = [&](size_t k) { return std::min(C, count - k * C); };
-    auto pin_in = [&](size_t k) { return pin_ + (k & 1) * inW; };
-    auto pin_out = [&](size_t k) { return pin_ + 2 * inW + (k & 1) * outW; };
-    for (size_t k = 0; k < K; ++k) {
-        const size_t o = k * C, c = chunk(k);
-        if (k >= 2) FHE_HIP_CHECK(hipEventSynchronize(E.ev[3 * (k - 2)]));
-        uint64_t* p = pin_in(k);
-        par_copy(p, a1 + o * n, c * n);
-        par_copy(p + C * n, b1 + o, c);
-        par_copy(p + C * n + C, a2 + o * n, c * n);
-        par_copy(p + 2 * C * n + C, b2 + o, c);
-        FHE_HIP_CHECK(hipMemcpyAsync(da1 + o * n, p, c * n * 8, hipMemcpyHostToDevice, h2d_stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(db1 + o, p + C * n, c * 8, hipMemcpyHostToDevice, h2d_stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(da2 + o * n, p + C * n + C, c * n * 8, hipMemcpyHostToDevice, h2d_stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(db2 + o, p + 2 * C * n + C, c * 8, hipMemcpyHostToDevice, h2d_stream_));
-        FHE_HIP_CHECK(hipEventRecord(E.ev[3 * k], h2d_stream_));
-        FHE_HIP_CHECK(hipStreamWaitEvent(stream_, E.ev[3 * k], 0));
-        gates(o, c);
-        FHE_HIP_CHECK(hipEventRecord(E.ev[3 * k + 1], stream_));
-        FHE_HIP_CHECK(hipStreamWaitEvent(d2h_stream_, E.ev[3 * k + 1], 0));
-        uint64_t* q = pin_out(k);
-        FHE_HIP_CHECK(hipMemcpyAsync(q, dao + o * n, c * n * 8, hipMemcpyDeviceToHost, d2h_stream_));
-        FHE_HIP_CHECK(hipMemcpyAsync(q + C * n, dbo + o, c * 8, hipMemcpyDeviceToHost, d2h_stream_));
-        FHE_HIP_CHECK(hipEventRecord(E.ev[3 * k + 2], d2h_stream_));
-        if (k >= 1) {  // chunk k - 1's outputs (its gates finished before chunk k's began)
-            const size_t o1 = (k - 1) * C, c1 = chunk(k - 1);
-            FHE_HIP_CHECK(hipEventSynchronize(E.ev[3 * (k - 1) + 2]));
-            par_copy(a_out + o1 * n, pin_out(k - 1), c1 * n);
-            par_copy(b_out + o1, pin_out(k - 1) + C * n, c1);
-        }
-    }
-    const size_t oL = (K - 1) * C, cL = chunk(K - 1);
-    FHE_HIP_CHECK(hipEventSynchronize(E.ev[3 * (K - 1) + 2]));
-    par_copy(a_out + oL * n, pin_out(K - 1), cL * n);
-    par_copy(b_out + oL, pin_out(K - 1) + C * n, cL);
+    FHE_HIP_CHECK(hipMemcpyAsync(da1, a1, count * n * 8, hipMemcpyHostToDevice, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(db1, b1, count * 8, hipMemcpyHostToDevice, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(da2, a2, count * n * 8, hipMemcpyHostToDevice, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(db2, b2, count * 8, hipMemcpyHostToDevice, stream_));
+    eval_gate_device(gate, count, da1, db1, da2, db2, dao, dbo, stream_);
+    FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * n * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 void Engine::bootstrap_extended_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1,

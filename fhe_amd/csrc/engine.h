@@ -166,11 +166,6 @@ private:
     Params p_;
     int device_;
     hipStream_t stream_ = nullptr;
-    // eval_gate_host's copy pipeline (created on first use): H2D and D2H streams, pinned staging
-    hipStream_t h2d_stream_ = nullptr;
-    hipStream_t d2h_stream_ = nullptr;
-    uint64_t* pin_ = nullptr;
-    size_t pin_words_ = 0;
     BootTables tabs_{};
     void* d_tables_ = nullptr;
     void* d_bsk_ = nullptr;

@@ -237,10 +237,10 @@ def test_gpu_large_batch_truth_and_determinism(name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["std128", "lmkcdey"])
-def test_gpu_pipelined_host_batch_matches_device(name):
-    """host-buffer batches of more than one 8192-gate chunk run the copy/compute pipeline
-    (Engine::eval_gate_host): a ragged 4-chunk batch == one device-resident launch, bit-exact,
-    and every gate decrypts to its truth value"""
+def test_gpu_host_batch_matches_device(name):
+    """the host-buffer entry point (fhe_hip_eval_bingate_batch, Engine::eval_gate_host) on a
+    ragged 24,699-gate batch == the device-resident entry point, bit-exact, and every gate
+    decrypts to its truth value"""
     import ctypes
     from fhe_amd import binfhe as bf
     from fhe_amd._lib import check, lib, ptr, vp
