@@ -1,5 +1,5 @@
-# round-3 end check after the host-path pipeline: seam timings (pipelined and one-shot), every GPU
-# test, smoke()
+# round-3 end check of the host-path copy pipeline (since dropped; FHE_HIP_HOST_PIPELINE=0 was its
+# A/B knob and is a no-op now): seam timings, every GPU test, smoke()
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u tools/seam_time.py ginx 1 16 256 1024 8192 16384 65536 > gpurun_out/r03_seam_ginx_final.txt 2>&1 || { echo seam-failed; tail -5 gpurun_out/r03_seam_ginx_final.txt; exit 1; }
