@@ -84,6 +84,15 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
+#ifndef FHE_LMK_PRE
+#define FHE_LMK_PRE 1    // op-list kernel: a pass's 31 per-lane twiddles requested together at its start
+#endif
+#ifndef FHE_LMK_AKPF
+#define FHE_LMK_AKPF 1   // the same for the automorphism keys (4 slots x 2 rows)
+#endif
+#ifndef FHE_LMK_KPF
+#define FHE_LMK_KPF 1    // op-list kernel: key chunks (4 slots x 4 rows) requested ahead of their MAC
+#endif
 // v_mad_i64_i32 (a * b + c, 32 x 32 -> 64 signed) in plain C, with -Q re-materialised inside each
 // loop body (fresh_nq) so that instruction selection sees a sign-extended 32-bit operand (hoisted,
 // the compiler widens -Q into a 64-bit constant and the product becomes 5 instructions)
@@ -1026,16 +1035,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         if (DM || !(op & 0x8000u)) {
             // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
             const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)op * (4 * 8 * 64);
-            uint4 kq[2][4];
+            constexpr int KPF = FHE_LMK_KPF;
+            uint4 kq[KPF + 1][4];
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass_s<20, LZ, !DM>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
+            inv_pass_s<20, LZ, !DM && FHE_LMK_PRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
-            fwd_pass2<FM, !DM>(dA, dB, tile, l, twAf, s_twBf, m);
+            fwd_pass2<FM, !DM && FHE_LMK_PRE>(dA, dB, tile, l, twAf, s_twBf, m);
             // one 16-byte vector per digit row and 4 slots (boot.h row_off)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) kq[0][d] = kload(kb4, (d * 8 + 0) * 64 + lane);
+            for (int p = 0; p < KPF; ++p)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) kq[p][d] = kload(kb4, (d * 8 + p) * 64 + lane);
             // LMKCDEY: the other half's digits of slots 4(kk+1).. requested before 4kk.. are consumed
             constexpr bool PIPE = !DM;
             uint32_t xq[2][8];
@@ -1049,16 +1061,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             if (PIPE) issue(0, 0);
 #pragma clang loop unroll(full)
             for (int kk = 0; kk < 8; ++kk) {
-                if (kk + 1 < 8) {  // request slots 4(kk+1).. while 4kk.. are consumed
+                if (kk + KPF < 8) {  // request slots 4(kk+KPF).. while 4kk.. are consumed
 #pragma unroll
-                    for (int d = 0; d < 4; ++d) kq[(kk + 1) & 1][d] = kload(kb4, (d * 8 + kk + 1) * 64 + lane);
-                    if (PIPE) issue(kk + 1, (kk + 1) & 1);
+                    for (int d = 0; d < 4; ++d)
+                        kq[(kk + KPF) % (KPF + 1)][d] = kload(kb4, (d * 8 + kk + KPF) * 64 + lane);
                 }
+                if (PIPE && kk + 1 < 8) issue(kk + 1, (kk + 1) & 1);
                 asm volatile("" ::: "memory");
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int r = 4 * kk + e;
-#define KC(d) (e == 0 ? kq[kk & 1][d].x : e == 1 ? kq[kk & 1][d].y : e == 2 ? kq[kk & 1][d].z : kq[kk & 1][d].w)
+#define KC(d) (e == 0 ? kq[kk % (KPF + 1)][d].x : e == 1 ? kq[kk % (KPF + 1)][d].y : e == 2 ? kq[kk % (KPF + 1)][d].z : kq[kk % (KPF + 1)][d].w)
                     const uint32_t D0 = dA[r], D2 = dB[r];
                     const uint32_t D1 = PIPE ? xq[kk & 1][2 * e] : other_half(dA[r], xaddr);
                     const uint32_t D3 = PIPE ? xq[kk & 1][2 * e + 1] : other_half(dB[r], xaddr);
@@ -1099,9 +1112,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             }
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
             const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
-            uint4 ka[2][2];
-            ka[0][0] = kload(kb4, (0 * 8 + 0) * 64 + lane);
-            ka[0][1] = kload(kb4, (1 * 8 + 0) * 64 + lane);
+            constexpr int AKPF = FHE_LMK_AKPF;
+            uint4 ka[AKPF + 1][2];
+#pragma unroll
+            for (int p = 0; p < AKPF; ++p) {
+                ka[p][0] = kload(kb4, (0 * 8 + p) * 64 + lane);
+                ka[p][1] = kload(kb4, (1 * 8 + p) * 64 + lane);
+            }
             uint32_t xa[2][4];
             auto issue = [&](int kk, int b) {
 #pragma unroll
@@ -1110,13 +1127,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             issue(0, 0);
 #pragma clang loop unroll(full)
             for (int kk = 0; kk < 8; ++kk) {
-                if (kk + 1 < 8) {
-                    ka[(kk + 1) & 1][0] = kload(kb4, (0 * 8 + kk + 1) * 64 + lane);
-                    ka[(kk + 1) & 1][1] = kload(kb4, (1 * 8 + kk + 1) * 64 + lane);
-                    issue(kk + 1, (kk + 1) & 1);
+                if (kk + AKPF < 8) {
+                    ka[(kk + AKPF) % (AKPF + 1)][0] = kload(kb4, (0 * 8 + kk + AKPF) * 64 + lane);
+                    ka[(kk + AKPF) % (AKPF + 1)][1] = kload(kb4, (1 * 8 + kk + AKPF) * 64 + lane);
                 }
+                if (kk + 1 < 8) issue(kk + 1, (kk + 1) & 1);
                 asm volatile("" ::: "memory");
-                const uint4 k0 = ka[kk & 1][0], k1 = ka[kk & 1][1];
+                const uint4 k0 = ka[kk % (AKPF + 1)][0], k1 = ka[kk % (AKPF + 1)][1];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int r = 4 * kk + e;

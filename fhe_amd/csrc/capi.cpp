@@ -541,6 +541,26 @@ int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
     });
 }
 
+int fhe_hip_bootstrap_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
+                            uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
+        ctx->eng.refresh_host(count, a, b, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_bootstrap_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                   uint64_t* d_a_out, uint64_t* d_b_out, void* stream) {
+    if (!ctx || !io_ok(count, d_a, d_b, d_a_out, d_b_out, d_a, d_b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const CallOrder order(ctx, stream);
+        ctx->eng.refresh_device(count, d_a, d_b, d_a_out, d_b_out, order.s);
+        return FHE_HIP_OK;
+    });
+}
+
 // ---- the Backend seam (backend.h:73-247) ----
 int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, uint64_t ctmod, uint64_t* acc) {
     if (!ctx || (count && (!a || !acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");

@@ -851,6 +851,21 @@ void Engine::eval_gate_multi_device(int gate, size_t count, uint32_t k, const ui
     if (a_out) keyswitch_workspace_device(count, a_out, b_out, s);
 }
 
+void Engine::refresh_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out,
+                            hipStream_t s) {
+    if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
+    GateArgs g = gate_args(G_AND, count);  // BootstrapGateCore's AND window; b = Q/(2p) + 1, p = 4 (:211)
+    if (count == 0) return;
+    if (!a || !b || !a_out || !b_out) throw std::invalid_argument("null argument");
+    ensure_work(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    // ct + q/4 (EvalAddConstEq, :201) as the prep's b offset
+    GateInputs in{{a, nullptr, nullptr, nullptr}, {b, nullptr, nullptr, nullptr}, 1, 0, p_.q >> 2};
+    prep_device(g, in, 0, s);
+    rotate_device(g, s);
+    keyswitch_workspace_device(count, a_out, b_out, s);
+}
+
 void Engine::eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1,
                               const uint64_t* b1, const uint64_t* a2, const uint64_t* b2, uint64_t* a_out,
                               uint64_t* b_out, hipStream_t s) {
@@ -1073,6 +1088,24 @@ void Engine::eval_gate_multi_host(int gate, size_t count, uint32_t k, const uint
     eval_gate_multi_device(gate, count, k, da, db, p, nullptr, nullptr, stream_);
     (void)N;
     copy_ext_host(count, a_out, b_out);
+}
+
+void Engine::refresh_host(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out) {
+    if (count == 0) return;
+    ensure_host_stage(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    const uint64_t* ha[1] = {a};
+    const uint64_t* hb[1] = {b};
+    const uint64_t* da[4] = {};
+    const uint64_t* db[4] = {};
+    stage_inputs(count, 1, ha, hb, da, db);
+    const size_t n = p_.n;
+    uint64_t* dao = d_io_ + count * 4 * (n + 1);
+    uint64_t* dbo = dao + count * n;
+    refresh_device(count, da[0], db[0], dao, dbo, stream_);
+    FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * n * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 void Engine::eval_cmux_host(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1,

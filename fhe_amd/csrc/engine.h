@@ -102,6 +102,10 @@ public:
                                 const uint64_t* const* b, uint32_t p, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
     // EvalBinGate(CMUX, {ct0, ct1, ct2}) = NAND(NAND(ct0, NOT ct2), NAND(ct1, ct2)) (:172-182):
     // one 2*count-gate NAND level, then one count-gate NAND level
+    // BinFHEScheme::Bootstrap (binfhe-base-scheme.cpp:190-218): BootstrapGateCore(AND, ct + q/4), extraction,
+    // SwitchCTtoqn; ciphertexts mod q of plaintext modulus 4
+    void refresh_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out,
+                        hipStream_t s);
     void eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
                           const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
 
@@ -138,6 +142,7 @@ public:
     // extended = true returns ctExt ([count][N] mod Q) instead of the switched output
     void eval_gate_multi_host(int gate, size_t count, uint32_t k, const uint64_t* const* a, const uint64_t* const* b,
                               uint32_t p, uint64_t* a_out, uint64_t* b_out, bool extended);
+    void refresh_host(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
     void eval_cmux_host(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
                         const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out);
 

@@ -192,6 +192,13 @@ int fhe_hip_eval_gate_multi_batch(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32
 int fhe_hip_eval_gate_multi_batch_device(fhe_hip_ctx* ctx, int gate, uint32_t k, uint32_t ptmod, size_t count,
                                          const uint64_t* const* d_a_in, const uint64_t* const* d_b_in,
                                          uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* BinFHEContext::Bootstrap (binfhecontext.cpp; BinFHEScheme::Bootstrap, binfhe-base-scheme.cpp:190-218):
+ * BootstrapGateCore(AND, ct + q/4), extraction (b = Q/8 + 1 + acc1[0]) and SwitchCTtoqn -- the refresh of
+ * lux_fhe_bootstrap (c_api.cpp:263-276).  Ciphertexts a[count][n], b[count] mod q, plaintext modulus 4. */
+int fhe_hip_bootstrap_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
+                            uint64_t* b_out);
+int fhe_hip_bootstrap_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                   uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
 /* EvalBinGate(CMUX, {ct0, ct1, ct2}) = NAND(NAND(ct0, NOT ct2), NAND(ct1, ct2)), i.e. ct2 ? ct1 : ct0
  * (binfhe-base-scheme.cpp:172-182; EvalCMUXBatch, batch.cpp:212-249, passes {sel, true, false}). */
 int fhe_hip_eval_cmux_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a0, const uint64_t* b0,

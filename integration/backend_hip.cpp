@@ -539,6 +539,194 @@ void BackendHIP::EvalBinGateBatch(BINGATE gate, const RingGSWBTKey& keys, const 
         out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
 }
 
+namespace {
+// rows [first, first + count) of a ciphertext vector as the raw u64 arrays of the C-ABI
+void flatten(const std::vector<LWECiphertext>& v, const std::vector<size_t>& rows, uint32_t n, uint64_t* a,
+             uint64_t* b) {
+    for (size_t g = 0; g < rows.size(); ++g) {
+        const auto& ct = v[rows[g]];
+        if (!ct)
+            throw std::invalid_argument("BackendHIP: null ciphertext");
+        const auto& x = ct->GetA();
+        if (x.GetLength() != n)
+            throw std::invalid_argument("BackendHIP: ciphertexts of dimension n");
+        for (uint32_t i = 0; i < n; ++i)
+            a[g * n + i] = x[i].ConvertToInt();
+        b[g] = ct->GetB().ConvertToInt();
+    }
+}
+std::vector<size_t> all_rows(size_t B) {
+    std::vector<size_t> r(B);
+    for (size_t g = 0; g < B; ++g)
+        r[g] = g;
+    return r;
+}
+}  // namespace
+
+void BackendHIP::EvalFuncBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
+                               const std::vector<NativeInteger>& lut, std::vector<LWECiphertext>& out) {
+    std::lock_guard<std::mutex> lock(mu_);
+    const size_t B = cts.size();
+    out.resize(B);
+    if (B == 0)
+        return;
+    EnsureBSK(keys.BSkey);
+    EnsureKSK(keys.KSkey);
+    std::vector<uint64_t> tab(lut.size());
+    for (size_t i = 0; i < lut.size(); ++i)
+        tab[i] = lut[i].ConvertToInt();
+    // EvalFunc runs at each ciphertext's own modulus (binfhe-base-scheme.cpp:250): one pass per modulus
+    std::vector<std::pair<uint64_t, size_t>> order(B);
+    for (size_t g = 0; g < B; ++g) {
+        if (!cts[g])
+            throw std::invalid_argument("Ciphertext is empty");
+        order[g] = {cts[g]->GetModulus().ConvertToInt(), g};
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [](const auto& x, const auto& y) { return x.first < y.first; });
+    const uint32_t n = p_.n;
+    for (size_t s = 0; s < B;) {
+        const uint64_t q = order[s].first;
+        std::vector<size_t> rows;
+        for (; s < B && order[s].first == q; ++s)
+            rows.push_back(order[s].second);
+        const size_t c = rows.size();
+        std::vector<uint64_t> a(c * n), b(c), ao(c * n), bo(c);
+        flatten(cts, rows, n, a.data(), b.data());
+        Check(fhe_hip_eval_func_batch(ctx_, c, a.data(), b.data(), q, tab.data(), tab.size(), ao.data(), bo.data()),
+              "EvalFuncBatch");
+        const NativeInteger qn(q);
+        for (size_t g = 0; g < c; ++g)
+            out[rows[g]] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, qn), NativeInteger(bo[g]));
+    }
+}
+
+void BackendHIP::RefreshBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
+                              std::vector<LWECiphertext>& out) {
+    std::lock_guard<std::mutex> lock(mu_);
+    const size_t B = cts.size();
+    out.resize(B);
+    if (B == 0)
+        return;
+    const NativeInteger q(p_.q);
+    for (const auto& ct : cts) {
+        if (!ct)
+            throw std::invalid_argument("Ciphertext is empty");
+        if (ct->GetModulus() != q)  // the Q-modulus input of :199 (SwitchCTtoqn first) is not taken here
+            throw std::invalid_argument("BackendHIP::RefreshBatch: ciphertexts mod q");
+        if (ct->GetptModulus() != 4)  // the window and b constant of the device path are p = 4's (:205, :211)
+            throw std::invalid_argument("BackendHIP::RefreshBatch: plaintext modulus 4");
+    }
+    EnsureBSK(keys.BSkey);
+    EnsureKSK(keys.KSkey);
+    const uint32_t n = p_.n;
+    std::vector<uint64_t> a(B * n), b(B), ao(B * n), bo(B);
+    flatten(cts, all_rows(B), n, a.data(), b.data());
+    Check(fhe_hip_bootstrap_batch(ctx_, B, a.data(), b.data(), ao.data(), bo.data()), "RefreshBatch");
+    for (size_t g = 0; g < B; ++g) {
+        out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
+        out[g]->SetptModulus(cts[g]->GetptModulus());
+    }
+}
+
+void BackendHIP::EvalCMUXBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& ct0,
+                               const std::vector<LWECiphertext>& ct1, const std::vector<LWECiphertext>& ct2,
+                               std::vector<LWECiphertext>& out) {
+    std::lock_guard<std::mutex> lock(mu_);
+    const size_t B = ct0.size();
+    if (ct1.size() != B || ct2.size() != B)
+        throw std::invalid_argument("Input size mismatch");
+    out.resize(B);
+    if (B == 0)
+        return;
+    for (size_t g = 0; g < B; ++g)  // binfhe-base-scheme.cpp:136-143
+        if (ct0[g] == ct1[g] || ct0[g] == ct2[g] || ct1[g] == ct2[g])
+            throw std::invalid_argument("Input ciphertexts should be independent");
+    EnsureBSK(keys.BSkey);
+    EnsureKSK(keys.KSkey);
+    const uint32_t n = p_.n;
+    const auto rows  = all_rows(B);
+    std::vector<uint64_t> a0(B * n), b0(B), a1(B * n), b1(B), a2(B * n), b2(B), ao(B * n), bo(B);
+    flatten(ct0, rows, n, a0.data(), b0.data());
+    flatten(ct1, rows, n, a1.data(), b1.data());
+    flatten(ct2, rows, n, a2.data(), b2.data());
+    Check(fhe_hip_eval_cmux_batch(ctx_, B, a0.data(), b0.data(), a1.data(), b1.data(), a2.data(), b2.data(),
+                                  ao.data(), bo.data()),
+          "EvalCMUXBatch");
+    const NativeInteger q(p_.q);
+    for (size_t g = 0; g < B; ++g)
+        out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
+}
+
+namespace {
+BackendHIP* default_hip() {
+    return dynamic_cast<BackendHIP*>(BackendRegistry::Instance().GetDefault());
+}
+RingGSWBTKey context_keys(BinFHEContext& cc) {
+    RingGSWBTKey keys;
+    keys.BSkey = cc.GetRefreshKey();
+    keys.KSkey = cc.GetSwitchKey();
+    return keys;
+}
+// the reference's BatchResult convention: everything processed, or the whole batch failed with the message
+template <typename F>
+BatchResult batch_result(size_t count, F&& f) {
+    try {
+        f();
+        return BatchResult{true, count, 0, ""};
+    }
+    catch (const std::exception& e) {
+        return BatchResult{false, 0, count, e.what()};
+    }
+}
+}  // namespace
+
+BatchResult EvalFuncBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_in,
+                             const std::vector<NativeInteger>& lut, std::vector<LWECiphertext>& ct_out,
+                             uint32_t flags) {
+    auto* hip = default_hip();
+    if (!hip)
+        return lux::fhe::EvalFuncBatch(cc, ct_in, lut, ct_out, flags);
+    if (ct_in.empty())
+        return BatchResult{true, 0, 0, ""};
+    return batch_result(ct_in.size(), [&] { hip->EvalFuncBatch(context_keys(cc), ct_in, lut, ct_out); });
+}
+
+BatchResult EvalFuncMultiOutputBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_in,
+                                        const std::vector<std::vector<NativeInteger>>& luts,
+                                        std::vector<LWECiphertext>& ct_out, uint32_t flags) {
+    auto* hip = default_hip();
+    if (!hip)
+        return lux::fhe::EvalFuncMultiOutputBatch(cc, ct_in, luts, ct_out, flags);
+    if (ct_in.empty() || luts.empty())
+        return BatchResult{true, 0, 0, ""};
+    return batch_result(ct_in.size(), [&] {
+        const size_t L = luts.size(), B = ct_in.size();
+        ct_out.resize(B * L);
+        const RingGSWBTKey keys = context_keys(cc);
+        std::vector<LWECiphertext> part;
+        for (size_t j = 0; j < L; ++j) {  // output j of input i at i * L + j (batch.cpp:160-164)
+            hip->EvalFuncBatch(keys, ct_in, luts[j], part);
+            for (size_t i = 0; i < B; ++i)
+                ct_out[i * L + j] = part[i];
+        }
+    });
+}
+
+BatchResult EvalCMUXBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_sel,
+                             const std::vector<LWECiphertext>& ct_true, const std::vector<LWECiphertext>& ct_false,
+                             std::vector<LWECiphertext>& ct_out, uint32_t flags) {
+    auto* hip = default_hip();
+    if (!hip)
+        return lux::fhe::EvalCMUXBatch(cc, ct_sel, ct_true, ct_false, ct_out, flags);
+    if (ct_sel.size() != ct_true.size() || ct_sel.size() != ct_false.size())
+        return BatchResult{false, 0, ct_sel.size(), "Input size mismatch"};
+    if (ct_sel.empty())
+        return BatchResult{true, 0, 0, ""};
+    return batch_result(ct_sel.size(),
+                        [&] { hip->EvalCMUXBatch(context_keys(cc), ct_sel, ct_true, ct_false, ct_out); });
+}
+
 BatchResult EvalBinGateBatchHIP(BinFHEContext& cc, BINGATE gate, const std::vector<LWECiphertext>& ct1,
                                 const std::vector<LWECiphertext>& ct2, std::vector<LWECiphertext>& ct_out,
                                 uint32_t flags) {

@@ -88,6 +88,20 @@ public:
     void EvalBinGateBatch(BINGATE gate, const RingGSWBTKey& keys, const std::vector<LWECiphertext>& ct1,
                           const std::vector<LWECiphertext>& ct2, std::vector<LWECiphertext>& out);
 
+    // the reference's other batch callers on the GPU, one device pass per batch:
+    //   EvalFuncBatch: BinFHEContext::EvalFunc (binfhe-base-scheme.cpp:241-332) on every ciphertext, at
+    //                  its own modulus (ct->GetModulus(); ciphertexts of one modulus go in one pass)
+    //   EvalCMUXBatch: EvalBinGate(CMUX, {ct0, ct1, ct2}) (binfhe-base-scheme.cpp:172-182) per row: three
+    //                  NAND bootstraps in two dependent launches
+    void EvalFuncBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
+                       const std::vector<NativeInteger>& lut, std::vector<LWECiphertext>& out);
+    //   RefreshBatch:  BinFHEContext::Bootstrap (BinFHEScheme::Bootstrap, binfhe-base-scheme.cpp:190-218) per
+    //                  ciphertext (mod q, plaintext modulus 4)
+    void RefreshBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts, std::vector<LWECiphertext>& out);
+    void EvalCMUXBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& ct0,
+                       const std::vector<LWECiphertext>& ct1, const std::vector<LWECiphertext>& ct2,
+                       std::vector<LWECiphertext>& out);
+
     fhe_hip_ctx* Context() const { return ctx_; }
     // destroys the device context now (the registry owns backends until static destruction, which
     // may run after the HIP runtime's own teardown); the backend is unavailable afterwards
@@ -124,6 +138,23 @@ private:
 BatchResult EvalBinGateBatchHIP(BinFHEContext& cc, BINGATE gate, const std::vector<LWECiphertext>& ct1,
                                 const std::vector<LWECiphertext>& ct2, std::vector<LWECiphertext>& ct_out,
                                 uint32_t flags = 0);
+
+// The same routing for the reference's other batch callers (batch/batch.cpp), each with the reference's
+// BatchResult semantics and its OpenMP loop as the fallback when the default backend is not a BackendHIP:
+//   EvalFuncBatchHIP            <- EvalFuncBatch (batch.cpp:106-139): ct_out[i] = cc.EvalFunc(ct_in[i], lut)
+//   EvalFuncMultiOutputBatchHIP <- EvalFuncMultiOutputBatch (:141-174): ct_out[i * L + j] = EvalFunc(ct_in[i],
+//                                  luts[j]); one GPU pass per LUT; processed = ct_in.size()
+//   EvalCMUXBatchHIP            <- EvalCMUXBatch (:212-249): ct_out[i] = cc.EvalBinGate(CMUX, {ct_sel[i],
+//                                  ct_true[i], ct_false[i]}), the vector order the reference passes
+BatchResult EvalFuncBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_in,
+                             const std::vector<NativeInteger>& lut, std::vector<LWECiphertext>& ct_out,
+                             uint32_t flags = 0);
+BatchResult EvalFuncMultiOutputBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_in,
+                                        const std::vector<std::vector<NativeInteger>>& luts,
+                                        std::vector<LWECiphertext>& ct_out, uint32_t flags = 0);
+BatchResult EvalCMUXBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_sel,
+                             const std::vector<LWECiphertext>& ct_true, const std::vector<LWECiphertext>& ct_false,
+                             std::vector<LWECiphertext>& ct_out, uint32_t flags = 0);
 
 }  // namespace lux::fhe::backend
 

@@ -26,6 +26,8 @@
 
 #include "backend_hip.h"
 #include "batch/binfhe-batch.h"
+#include "c_api_hip.h"
+#include "c_api_hip_types.h"
 #include "rgsw-acc-cggi.h"
 #include "rgsw-acc-dm.h"
 #include "rgsw-acc-lmkcdey.h"
@@ -474,6 +476,119 @@ int bh_pack_roundtrip(void* h, size_t count, const uint64_t* a, const uint64_t* 
         be->Free(pk);
         *ok = (same ? 1 : 0) | (*ek == *cc.GetRefreshKey() ? 2 : 0);
     });
+}
+
+// EvalFuncBatchHIP (multi = 0) or EvalFuncMultiOutputBatchHIP (multi = 1) with BackendHIP as the default vs
+// the reference's EvalFuncBatch / EvalFuncMultiOutputBatch (batch.cpp:106-174) on the same ciphertexts
+// (mod ctmod).  luts [L][lut_len]; outputs [count][L][n] (multi) or, for multi = 0, [L][count][n] from one
+// routed call per LUT.  *ok = every routed BatchResult reported success with processed = count
+int bh_eval_func_routed(void* h, int multi, size_t count, const uint64_t* a, const uint64_t* b, uint64_t ctmod,
+                        const uint64_t* luts, size_t L, size_t lut_len, uint64_t* ga, uint64_t* gb, uint64_t* ra,
+                        uint64_t* rb, int* ok) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        const uint32_t n  = cc.GetParams()->GetLWEParams()->Getn();
+        auto cts          = lwe_vec(a, b, count, n, ctmod);
+        std::vector<std::vector<NativeInteger>> tabs(L, std::vector<NativeInteger>(lut_len));
+        for (size_t j = 0; j < L; ++j)
+            for (size_t i = 0; i < lut_len; ++i)
+                tabs[j][i] = NativeInteger(luts[j * lut_len + i]);
+        *ok = 1;
+        std::vector<LWECiphertext> out, ref;
+        if (multi) {
+            const BatchResult r = EvalFuncMultiOutputBatchHIP(cc, cts, tabs, out, 0);
+            *ok = r.success && r.processed == count && out.size() == count * L;
+            if (!r.success)
+                throw std::runtime_error("EvalFuncMultiOutputBatchHIP: " + r.error);
+            const BatchResult rr = EvalFuncMultiOutputBatch(cc, cts, tabs, ref, 0);
+            if (!rr.success)
+                throw std::runtime_error("reference EvalFuncMultiOutputBatch: " + rr.error);
+            lwe_out(out, ga, gb);
+            lwe_out(ref, ra, rb);
+            return;
+        }
+        for (size_t j = 0; j < L; ++j) {
+            const BatchResult r = EvalFuncBatchHIP(cc, cts, tabs[j], out, 0);
+            *ok = *ok && r.success && r.processed == count && out.size() == count;
+            if (!r.success)
+                throw std::runtime_error("EvalFuncBatchHIP: " + r.error);
+            const BatchResult rr = EvalFuncBatch(cc, cts, tabs[j], ref, 0);
+            if (!rr.success)
+                throw std::runtime_error("reference EvalFuncBatch: " + rr.error);
+            lwe_out(out, ga + j * count * n, gb + j * count);
+            lwe_out(ref, ra + j * count * n, rb + j * count);
+        }
+    });
+}
+
+// EvalCMUXBatchHIP (BackendHIP as the default) vs the reference's EvalCMUXBatch (batch.cpp:212-249): rows
+// (sel, true, false) = (ct0, ct1, ct2)
+int bh_eval_cmux_routed(void* h, size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1,
+                        const uint64_t* b1, const uint64_t* a2, const uint64_t* b2, uint64_t* ga, uint64_t* gb,
+                        uint64_t* ra, uint64_t* rb, int* ok) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        const uint64_t q  = lp->Getq().ConvertToInt();
+        const uint32_t n  = lp->Getn();
+        auto c0 = lwe_vec(a0, b0, count, n, q), c1 = lwe_vec(a1, b1, count, n, q), c2 = lwe_vec(a2, b2, count, n, q);
+        std::vector<LWECiphertext> out, ref;
+        const BatchResult r = EvalCMUXBatchHIP(cc, c0, c1, c2, out, 0);
+        *ok = r.success && r.processed == count;
+        if (!r.success)
+            throw std::runtime_error("EvalCMUXBatchHIP: " + r.error);
+        const BatchResult rr = EvalCMUXBatch(cc, c0, c1, c2, ref, 0);
+        if (!rr.success)
+            throw std::runtime_error("reference EvalCMUXBatch: " + rr.error);
+        lwe_out(out, ga, gb);
+        lwe_out(ref, ra, rb);
+    });
+}
+
+// BackendHIP::RefreshBatch vs the reference's BinFHEContext::Bootstrap on every ciphertext
+int bh_refresh(void* h, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* ga, uint64_t* gb, uint64_t* ra,
+               uint64_t* rb) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        auto cts          = lwe_vec(a, b, count, lp->Getn(), lp->Getq().ConvertToInt());
+        RingGSWBTKey keys;
+        keys.BSkey = cc.GetRefreshKey();
+        keys.KSkey = cc.GetSwitchKey();
+        std::vector<LWECiphertext> out, ref(count);
+        g_be->RefreshBatch(keys, cts, out);
+#pragma omp parallel for
+        for (size_t g = 0; g < count; ++g)
+            ref[g] = cc.Bootstrap(cts[g]);
+        lwe_out(out, ga, gb);
+        lwe_out(ref, ra, rb);
+    });
+}
+
+// ---- the C API (integration/c_api_hip.cpp): the reference's CPU evaluation on the same LuxFheContext ----
+// gate < 6: cc.EvalBinGate(gate, a, b); gate = 6: cc.EvalBinGate(CMUX, {a, b, c}); gate = 7: cc.Bootstrap(a)
+int capi_ref_eval(LuxFheContext* ctx, int gate, const LuxFheCiphertext* a, const LuxFheCiphertext* b,
+                  const LuxFheCiphertext* c, LuxFheCiphertext** out) {
+    return guarded([&] {
+        auto r = std::make_unique<LuxFheCiphertext>();
+        if (gate < 6)
+            r->ct = ctx->cc.EvalBinGate(static_cast<BINGATE>(gate), a->ct, b->ct);
+        else if (gate == 6)
+            r->ct = ctx->cc.EvalBinGate(CMUX, std::vector<LWECiphertext>{a->ct, b->ct, c->ct});
+        else
+            r->ct = ctx->cc.Bootstrap(a->ct);
+        *out = r.release();
+    });
+}
+
+// the two ciphertexts are equal (LWECiphertextImpl::operator==: a and b), and the raw words of x
+int capi_ct_equal(const LuxFheCiphertext* x, const LuxFheCiphertext* y) {
+    return x && y && x->ct && y->ct && *x->ct == *y->ct;
+}
+
+// which backend the context's bootstrapped calls ran on: 1 = a BackendHIP exists for it
+int capi_on_gpu(const LuxFheContext* ctx) {
+    return ctx && ctx->gpu ? 1 : 0;
 }
 
 }  // extern "C"

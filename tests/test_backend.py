@@ -338,3 +338,199 @@ def test_gpu_backend_routed_gate_batch_equals_reference(bset):
         assert ok.value == 1
         assert np.array_equal(ga, ra) and np.array_equal(gb, rb), (name, gate)
         assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), truth), (name, gate)
+
+
+# ---- the reference's other batch callers and its public C API, routed to the GPU ---------------------
+ROUTED = ["std128", "lmkcdey", "std128_3"]
+
+
+@needs_backend
+def test_c_api_library_exports_the_reference_c_api():
+    """integration/c_api_hip.cpp defines every function of the reference's include/lux/fhe/c_api.h (when the
+    reference is present to read the header from) and the batch forms of integration/c_api_hip.h"""
+    import re
+    syms = dyn_symbols(BACKEND_SO)
+    ours = open(os.path.join(ROOT, "integration", "c_api_hip.h")).read()
+    want = set(re.findall(r"LUX_FHE_API[^;(]*?\b(lux_fhe_\w+)\s*\(", ours))
+    hdr = "/root/reference/include/lux/fhe/c_api.h"
+    if os.path.exists(hdr):
+        want |= set(re.findall(r"LUX_FHE_API[^;(]*?\b(lux_fhe_\w+)\s*\(", open(hdr).read()))
+        assert len(want) == 36, sorted(want)   # 33 of the reference + 3 batch forms
+    assert want and not (want - syms), sorted(want - syms)
+
+
+class CApi:
+    """ctypes view of the C API in oracle/_ref/libbackend_hip.so (integration/c_api_hip.cpp)"""
+
+    def __init__(self):
+        L = ctypes.CDLL(BACKEND_SO)
+        for f in ("lux_fhe_context_new", "lux_fhe_keygen_secret", "lux_fhe_keygen_bootstrap", "lux_fhe_encrypt",
+                  "lux_fhe_decrypt", "lux_fhe_and", "lux_fhe_or", "lux_fhe_xor", "lux_fhe_nand", "lux_fhe_nor",
+                  "lux_fhe_xnor", "lux_fhe_mux", "lux_fhe_bootstrap", "lux_fhe_gate_batch", "lux_fhe_mux_batch",
+                  "lux_fhe_bootstrap_batch", "capi_ref_eval", "capi_ct_equal", "capi_on_gpu",
+                  "lux_fhe_ciphertext_marshal", "lux_fhe_ciphertext_unmarshal"):
+            getattr(L, f).restype = ctypes.c_int
+        L.lux_fhe_context_n.restype = ctypes.c_uint32
+        L.lux_fhe_context_ring_dim.restype = ctypes.c_uint32
+        L.lux_fhe_context_modulus.restype = ctypes.c_uint64
+        L.lux_fhe_strerror.restype = ctypes.c_char_p
+        self.L = L
+
+    def ok(self, rc):
+        assert rc == 0, self.L.lux_fhe_strerror(rc).decode()
+
+
+@needs_backend
+def test_c_api_parameter_mapping_and_errors():
+    """c_api.cpp:44-68: STD128 is STD128_LMKCDEY, so GINX / AP on it are incompatible
+    (isMethodCompatible) and lux_fhe_context_new reports LUX_FHE_ERR_ALLOC; null pointers report
+    LUX_FHE_ERR_NULL_PTR.  CPU only: no bootstrapped call is made."""
+    C = CApi()
+    ctx = vp()
+    C.ok(C.L.lux_fhe_context_new(ctypes.byref(ctx), 2, 2))          # STD128 x LMKCDEY
+    assert (C.L.lux_fhe_context_n(ctx), C.L.lux_fhe_context_ring_dim(ctx), C.L.lux_fhe_context_modulus(ctx)) == \
+        (447, 1024, 2048)
+    assert C.L.capi_on_gpu(ctx) == 0                                    # the device context comes with the gates
+    other = vp()
+    assert C.L.lux_fhe_context_new(ctypes.byref(other), 2, 1) == -3   # STD128 x GINX
+    assert C.L.lux_fhe_context_new(None, 2, 2) == -1
+    bsk = vp()
+    assert C.L.lux_fhe_and(ctx, bsk, None, None, ctypes.byref(vp())) == -1
+    C.L.lux_fhe_context_free(ctx)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("bset", ROUTED, indirect=True)
+def test_gpu_backend_routed_eval_func_batches(bset):
+    """EvalFuncBatchHIP / EvalFuncMultiOutputBatchHIP (BackendHIP as the default) == the reference's
+    EvalFuncBatch / EvalFuncMultiOutputBatch (batch.cpp:106-174) on uniformly random ciphertexts mod q,
+    for the negacyclic, periodic and (q <= N) arbitrary LUTs GenerateLUTviaFunction builds"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import fb_luts
+    name = bset
+    b = backend(name)
+    r = b.ref
+    luts = np.stack(list(fb_luts(r.q, r.q // 256 if r.q >= 512 else 2, r.N).values())).astype(np.uint64)
+    L = luts.shape[0]
+    rng = np.random.default_rng(31)
+    for count in (1, 7):
+        a = rng.integers(0, r.q, (count, r.n), dtype=np.uint64)
+        bb = rng.integers(0, r.q, count, dtype=np.uint64)
+        for multi in (0, 1):
+            ga, gb = np.zeros((L * count, r.n), np.uint64), np.zeros(L * count, np.uint64)
+            ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+            ok = ctypes.c_int()
+            b.chk(b.L.bh_eval_func_routed(b.h, multi, sz(count), P(a), P(bb), u64(r.q), P(luts), sz(L),
+                                          sz(r.q), P(ga), P(gb), P(ra), P(rb), ctypes.byref(ok)))
+            assert ok.value == 1, (name, multi)
+            assert np.array_equal(ga, ra) and np.array_equal(gb, rb), (name, count, multi)
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("bset", ROUTED, indirect=True)
+def test_gpu_backend_routed_cmux_and_refresh(bset):
+    """EvalCMUXBatchHIP == the reference's EvalCMUXBatch (batch.cpp:212-249; rows {sel, true, false} as it
+    passes them, so the result is false ? true : sel), and BackendHIP::RefreshBatch == BinFHEContext::
+    Bootstrap, on every input combination"""
+    from fhe_amd import binfhe as bf
+    name = bset
+    b = backend(name)
+    r = b.ref
+    bits = np.array([[x >> 2 & 1, x >> 1 & 1, x & 1] for x in range(8)] * 2)
+    count = len(bits)
+    cts = [bf.encrypt(b.ps, b.m, b.sk, bits[:, j], 811 + j) for j in range(3)]
+    ga, gb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+    ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+    ok = ctypes.c_int()
+    b.chk(b.L.bh_eval_cmux_routed(b.h, sz(count), P(cts[0][0]), P(cts[0][1]), P(cts[1][0]), P(cts[1][1]),
+                                  P(cts[2][0]), P(cts[2][1]), P(ga), P(gb), P(ra), P(rb), ctypes.byref(ok)))
+    assert ok.value == 1
+    assert np.array_equal(ga, ra) and np.array_equal(gb, rb), name
+    want = np.where(bits[:, 2] == 1, bits[:, 1], bits[:, 0])
+    assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), want), name
+    ga, gb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+    ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+    b.chk(b.L.bh_refresh(b.h, sz(count), P(cts[0][0]), P(cts[0][1]), P(ga), P(gb), P(ra), P(rb)))
+    assert np.array_equal(ga, ra) and np.array_equal(gb, rb), name
+    assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), bits[:, 0]), name
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("params", [2, 0])    # LUX_FHE_PARAMS_STD128 (= STD128_LMKCDEY), TOY
+def test_gpu_c_api_gates_mux_bootstrap_vs_reference(params):
+    """The reference's public C API (c_api.h) over the GPU: every gate, lux_fhe_mux and lux_fhe_bootstrap
+    (single and batch forms) == the reference's own cc.EvalBinGate / EvalBinGate(CMUX, ..) / Bootstrap on
+    the same context, keys (the reference's BTKeyGen) and ciphertexts, and decrypt to the truth tables"""
+    for bname in list(_backends):      # one registry default at a time: release the seam tests' backend
+        _backends.pop(bname).close()
+    C = CApi()
+    L = C.L
+    ctx, sk, bsk = vp(), vp(), vp()
+    C.ok(L.lux_fhe_context_new(ctypes.byref(ctx), params, 2))
+    C.ok(L.lux_fhe_keygen_secret(ctx, ctypes.byref(sk)))
+    C.ok(L.lux_fhe_keygen_bootstrap(ctx, sk, ctypes.byref(bsk)))
+    bits = np.array([[x >> 2 & 1, x >> 1 & 1, x & 1] for x in range(8)])
+    cts = [[vp() for _ in range(8)] for _ in range(3)]
+    for j in range(3):
+        for i in range(8):
+            C.ok(L.lux_fhe_encrypt(ctx, sk, ctypes.c_bool(bool(bits[i, j])), ctypes.byref(cts[j][i])))
+
+    def dec(ct):
+        v = ctypes.c_bool()
+        C.ok(L.lux_fhe_decrypt(ctx, sk, ct, ctypes.byref(v)))
+        return int(v.value)
+
+    def same_as_ref(out, code, x, y=None, z=None):
+        ref = vp()
+        assert L.capi_ref_eval(ctx, code, x, y, z, ctypes.byref(ref)) == 0
+        assert L.capi_ct_equal(out, ref) == 1, code
+        L.lux_fhe_ciphertext_free(ref)
+
+    gates = {"or": (0, lambda x, y: x | y), "and": (1, lambda x, y: x & y), "nor": (2, lambda x, y: 1 - (x | y)),
+             "nand": (3, lambda x, y: 1 - (x & y)), "xor": (4, lambda x, y: x ^ y), "xnor": (5, lambda x, y: 1 - (x ^ y))}
+    for gname, (code, f) in gates.items():
+        fn = getattr(L, f"lux_fhe_{gname}")
+        for i in (0, 3, 5, 6):
+            out = vp()
+            C.ok(fn(ctx, bsk, cts[0][i], cts[1][i], ctypes.byref(out)))
+            assert dec(out) == f(bits[i, 0], bits[i, 1]), (gname, i)
+            same_as_ref(out, code, cts[0][i], cts[1][i])
+            L.lux_fhe_ciphertext_free(out)
+        arr = (vp * 8)
+        outs = arr()
+        C.ok(L.lux_fhe_gate_batch(ctx, bsk, code, arr(*cts[0]), arr(*cts[1]), sz(8), outs))
+        for i in range(8):
+            assert dec(outs[i]) == f(bits[i, 0], bits[i, 1]), (gname, i)
+            same_as_ref(vp(outs[i]), code, cts[0][i], cts[1][i])
+            L.lux_fhe_ciphertext_free(vp(outs[i]))
+    assert L.capi_on_gpu(ctx) == 1
+    arr = (vp * 8)
+    outs = arr()
+    C.ok(L.lux_fhe_mux_batch(ctx, bsk, arr(*cts[0]), arr(*cts[1]), arr(*cts[2]), sz(8), outs))
+    for i in range(8):   # EvalBinGate(CMUX, {sel, a, b}) = b ? a : sel
+        assert dec(outs[i]) == (bits[i, 1] if bits[i, 2] else bits[i, 0]), i
+        same_as_ref(vp(outs[i]), 6, cts[0][i], cts[1][i], cts[2][i])
+        L.lux_fhe_ciphertext_free(vp(outs[i]))
+    one = vp()
+    C.ok(L.lux_fhe_mux(ctx, bsk, cts[0][5], cts[1][5], cts[2][5], ctypes.byref(one)))
+    same_as_ref(one, 6, cts[0][5], cts[1][5], cts[2][5])
+    C.ok(L.lux_fhe_bootstrap_batch(ctx, bsk, arr(*cts[0]), sz(8), outs))
+    for i in range(8):
+        assert dec(outs[i]) == bits[i, 0], i
+        same_as_ref(vp(outs[i]), 7, cts[0][i])
+        L.lux_fhe_ciphertext_free(vp(outs[i]))
+    C.ok(L.lux_fhe_bootstrap(ctx, bsk, cts[1][6], ctypes.byref(one)))
+    same_as_ref(one, 7, cts[1][6])
+    # a bootstrap key that was never generated: LUX_FHE_ERR_NOT_INIT, nothing evaluated
+    fake = ctypes.create_string_buffer(8)
+    assert L.lux_fhe_and(ctx, fake, cts[0][0], cts[1][0], ctypes.byref(vp())) == -11
+    for j in range(3):
+        for i in range(8):
+            L.lux_fhe_ciphertext_free(cts[j][i])
+    L.lux_fhe_bootstrapkey_free(bsk)
+    L.lux_fhe_secretkey_free(sk)
+    L.lux_fhe_context_free(ctx)
