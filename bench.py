@@ -174,6 +174,17 @@ def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None):
             "method": method}
 
 
+def per_gpu_hbm(method_name, B, step_s):
+    """per-GPU compulsory bytes of a step = BSK + KSK + B x I/O (two LWE
+    inputs and the output, reference u64 accounting; 561,381,376 B for GINX and 470,056,960 B for LMKCDEY at
+    8192 gates) over the step time, against the HBM peak"""
+    b = BSK_BYTES[method_name] + KSK_BYTES[method_name] + B * (IN_BYTES_PER_GATE[method_name] +
+                                                               OUT_BYTES_PER_GATE[method_name])
+    return {"bytes_per_gpu": b, "GBs": round(b / step_s / 1e9, 2), "frac": round(b / step_s / 1e9 / HBM_PEAK_GBS, 6),
+            "basis": "BASELINE.md 3 (configs 4/5): BSK + KSK + shard x (two LWE inputs + output) per GPU / step "
+                     "time (slowest rank); low by construction, the keys are reused by every gate"}
+
+
 def rooflines(method_name, B, br_ms, ks_ms):
     """roofline (HBM) and valu_roofline of the blind-rotation kernel at B gates per launch."""
     alg_bytes = BSK_BYTES[method_name] + B * (IN_BYTES_PER_GATE[method_name] + EXT_BYTES_PER_GATE)
@@ -184,7 +195,7 @@ def rooflines(method_name, B, br_ms, ks_ms):
         "kernel": k1, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(k1, B),
         "launch_ms": round(br_ms, 4), "launch_note": f"HIP events around {PREP_NAME[method_name]} + {k1} "
-                                                     "(the prep kernel is <1% of it)",
+                                                     "(the prep kernel is <1% of it); max over ranks",
         "keyswitch_ms": round(ks_ms, 4),
         "alg_bytes_per_launch": alg_bytes,
         "alg_bytes_basis": "BSK (reference u64 accounting) + B x (two LWE inputs + ctExt), SURVEY 8(d)",
@@ -281,10 +292,11 @@ def main():
 
     def measure(method_name):
         r = run_config(args, bf, torch, ctx, method_name, total, lo, hi)
-        el, bad, inexact, unknown = max_over_ranks(
+        # launch times as well: the roofline of an N-rank line is the slowest rank's kernel
+        el, bad, inexact, unknown, br, ks = max_over_ranks(
             [r["elapsed"], 0.0 if r["verified"] else 1.0, 1.0 if r["exact"] is False else 0.0,
-             1.0 if r["exact"] is None else 0.0], device=red_dev)
-        r["elapsed"] = el
+             1.0 if r["exact"] is None else 0.0, r["br_ms"], r["ks_ms"]], device=red_dev)
+        r["elapsed"], r["br_ms"], r["ks_ms"] = el, br, ks
         r["verified"] = bad == 0.0
         r["exact"] = None if unknown else inexact == 0.0
         return r
@@ -312,6 +324,7 @@ def main():
             "bit_exact_vs_reference": main_r["exact"],
             "roofline": roofline,
             "valu_roofline": valu,
+            "hbm_per_gpu": per_gpu_hbm(args.method, hi - lo, main_r["elapsed"] / args.steps),
         }
         if lmk_r is not None:
             lr, lv = rooflines("lmkcdey", lmk_r["B"], lmk_r["br_ms"], lmk_r["ks_ms"])
@@ -322,6 +335,7 @@ def main():
                 "ms_per_step": round(lmk_r["elapsed"] / args.steps * 1e3, 3),
                 "verified": lmk_r["verified"], "bit_exact_vs_reference": lmk_r["exact"],
                 "roofline": lr, "valu_roofline": lv, "cpu_baseline": None,
+                "hbm_per_gpu": per_gpu_hbm("lmkcdey", hi - lo, lmk_r["elapsed"] / args.steps),
             }
     if world == 1 and not args.no_config3 and args.method == "ginx":
         c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden="std128_b1024")

@@ -97,6 +97,10 @@ def _setup(L):
     L.fhe_hip_cereal_write_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
     L.fhe_hip_cereal_read_lwe.argtypes = [vp, sz, ctypes.c_int, vp, ctypes.c_uint32, vp, vp, vp]
     L.fhe_hip_cereal_write_lwe.argtypes = [vp, ctypes.c_uint32, u64, u64, ctypes.c_int, vp, sz, vp]
+    L.fhe_hip_cereal_read_context.argtypes = [vp, sz, vp, vp, vp]
+    L.fhe_hip_cereal_write_context.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp]
+    L.fhe_hip_create_from_cereal.argtypes = [vp, sz, ctypes.c_int, vp]
+    L.fhe_hip_bootstrap_batch.argtypes = [vp, sz, vp, vp, vp, vp]
     L.fhe_hip_pack_lwe_batch.argtypes = [ctypes.c_uint32, sz, vp, vp, ctypes.c_uint32, vp, sz, vp]
     L.fhe_hip_unpack_lwe_batch.argtypes = [vp, sz, vp, vp, vp, vp]
     L.fhe_hip_eval_bingate_packed.argtypes = [vp, ctypes.c_int, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp]
@@ -318,14 +322,51 @@ def cereal_write_lwe(a, b, mod, is_key=False):
     return out.tobytes()
 
 
+def cereal_read_context(data):
+    """(paramset, method) of the GenerateBinFHEContext row a serialized BinFHEContext (the cryptoContext
+    archive of boolean-serial-binary.cpp) holds"""
+    d = _buf(data)
+    ps, m = ctypes.c_int(), ctypes.c_int()
+    check(L().fhe_hip_cereal_read_context(ptr(d), d.size, ctypes.byref(ps), ctypes.byref(m), None))
+    return ps.value, m.value
+
+
+def cereal_write_context(paramset, method):
+    """the bytes Serial::Serialize(cc, SerType::BINARY) writes for a context of this row"""
+    size = ctypes.c_size_t()
+    check(L().fhe_hip_cereal_write_context(paramset, method, None, 0, ctypes.byref(size)))
+    out = np.zeros(size.value, np.uint8)
+    check(L().fhe_hip_cereal_write_context(paramset, method, ptr(out), out.size, ctypes.byref(size)))
+    return out.tobytes()
+
+
 class GateEngine:
     """One MI355X context (fhe_hip_ctx): resident keys + batched gate bootstrapping."""
 
-    def __init__(self, paramset, method, device=0):
+    def __init__(self, paramset, method, device=0, _handle=None):
         self._h = vp()
-        check(L().fhe_hip_create(paramset, method, device, ctypes.byref(self._h)))
+        if _handle is None:
+            check(L().fhe_hip_create(paramset, method, device, ctypes.byref(self._h)))
+        else:
+            self._h = _handle
         self.params = params(paramset, method)
         self.device = device
+
+    @classmethod
+    def from_cereal(cls, data, device=0):
+        """a context built from a serialized BinFHEContext alone (fhe_hip_create_from_cereal)"""
+        d = _buf(data)
+        h = vp()
+        check(L().fhe_hip_create_from_cereal(ptr(d), d.size, device, ctypes.byref(h)))
+        ps, m = cereal_read_context(d)
+        return cls(ps, m, device, _handle=h)
+
+    def bootstrap(self, a, b):
+        """BinFHEContext::Bootstrap over a batch (fhe_hip_bootstrap_batch)"""
+        a, b = _u64(a), _u64(b)
+        ao, bo = np.zeros_like(a), np.zeros_like(b)
+        check(L().fhe_hip_bootstrap_batch(self._h, b.size, ptr(a), ptr(b), ptr(ao), ptr(bo)))
+        return ao, bo
 
     def close(self):
         if self._h:
@@ -581,7 +622,8 @@ class SerializedKey:
 
 class Serial:
     """Serial::SerializeToFile / DeserializeFromFile with SerType::BINARY (utils/serial.h:95-125) for
-    the objects of boolean-serial-binary.cpp: LWECiphertext, LWEPrivateKey and the two key streams."""
+    the objects of boolean-serial-binary.cpp: BinFHEContext (the cryptoContext archive), LWECiphertext,
+    LWEPrivateKey and the two key streams."""
 
     @staticmethod
     def SerializeToFile(path, obj):
@@ -591,6 +633,8 @@ class Serial:
             data = cereal_write_lwe(obj.s, None, 1 << 14, is_key=True)
         elif isinstance(obj, SerializedKey):
             data = obj.data
+        elif isinstance(obj, BinFHEContext):   # the key-independent cryptoContext archive
+            data = cereal_write_context(obj.paramset, obj.method)
         else:
             raise TypeError(f"cannot serialize {type(obj).__name__}")
         with open(path, "wb") as f:
@@ -608,6 +652,12 @@ class Serial:
             return LWEPrivateKey(cereal_read_lwe(data, is_key=True)[0])
         if cls is SerializedKey:
             return SerializedKey(data)
+        if cls is BinFHEContext:   # boolean-serial-binary.cpp:108: the parameters come from the archive
+            cc = BinFHEContext()
+            cc.engine = GateEngine.from_cereal(data, cc.device)
+            cc.paramset, cc.method = cereal_read_context(data)
+            cc.params = params(cc.paramset, cc.method)
+            return cc
         raise TypeError(f"cannot deserialize {cls.__name__}")
 
 

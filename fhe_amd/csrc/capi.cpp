@@ -430,6 +430,40 @@ int fhe_hip_cereal_write_lwe(const uint64_t* a, uint32_t n, uint64_t b, uint64_t
     return guarded([&]() -> int { return emit_bytes(cereal_write_lwe(a, n, b, mod, is_key != 0), out, cap, size); });
 }
 
+static void context_row(const uint8_t* data, size_t size, int& paramset, int& method) {
+    if (!cereal_context_paramset(cereal_read_context(data, size), paramset, method))
+        throw std::invalid_argument("cryptoContext archive: its parameters match no supported parameter set");
+}
+
+int fhe_hip_cereal_read_context(const uint8_t* data, size_t size, int* paramset, int* method, fhe_hip_params* out) {
+    if (!data || !paramset || !method) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        context_row(data, size, *paramset, *method);
+        if (out) fill_params(make_params(*paramset, *method), out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_cereal_write_context(int paramset, int method, uint8_t* out, size_t cap, size_t* size) {
+    if (!size) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        if (!is_large(paramset) && !method_compatible(paramset, method))
+            return fail(FHE_HIP_ERR_INVALID_PARAM, "Specified BINFHE_METHOD and BINFHE_PARAMSET are incompatible");
+        return emit_bytes(cereal_write_context(make_params(paramset, method)), out, cap, size);
+    });
+}
+
+int fhe_hip_create_from_cereal(const uint8_t* data, size_t size, int device, fhe_hip_ctx** out) {
+    if (!data || !out) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        *out = nullptr;
+        int ps = 0, m = 0;
+        context_row(data, size, ps, m);
+        *out = new fhe_hip_ctx(ps, m, device);
+        return FHE_HIP_OK;
+    });
+}
+
 int fhe_hip_eval_bingate_batch(fhe_hip_ctx* ctx, int gate, size_t count, const uint64_t* a1, const uint64_t* b1,
                                const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out) {
     if (!ctx || !io_ok(count, a1, b1, a2, b2, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");

@@ -12,7 +12,8 @@ constexpr uint32_t kSameType = 0x40000000u;  // polymorphic id: dynamic type == 
 constexpr uint32_t kNewPtr = 0x80000000u;    // pointer id: first occurrence, object follows
 
 // the classes that carry a version word (first occurrence per archive)
-enum Cls { C_ACC, C_EVALKEY, C_POLY, C_VEC, C_INT, C_ILPARAMS, C_ELEMPARAMS, C_KSK, C_CT, C_SK, C_COUNT };
+enum Cls { C_ACC, C_EVALKEY, C_POLY, C_VEC, C_INT, C_ILPARAMS, C_ELEMPARAMS, C_KSK, C_CT, C_SK, C_CTX, C_CPARAMS,
+           C_LWEP, C_RGSWP, C_COUNT };
 
 struct Reader {
     const uint8_t* p;
@@ -319,6 +320,117 @@ std::string cereal_write_lwe(const uint64_t* a, uint32_t n, uint64_t b, uint64_t
     w.vec(a, n, mod);
     if (!is_key) w.integer(b);
     return std::move(w.s);
+}
+
+// ---- the cryptoContext archive ----------------------------------------------------------------------
+namespace {
+double f64_of(uint64_t bits) {
+    double d;
+    std::memcpy(&d, &bits, 8);
+    return d;
+}
+uint64_t bits_of(double d) {
+    uint64_t b;
+    std::memcpy(&b, &d, 8);
+    return b;
+}
+// lwe-cryptoparameters.h:66-86 / binfhecontext.cpp:161-167: both Gaussians of a row use STD_DEV
+constexpr double kStdDev = 3.19;
+}  // namespace
+
+CerealContext cereal_read_context(const uint8_t* data, size_t size) {
+    Reader r(data, size);
+    CerealContext c;
+    r.version(C_CTX, 1);           // BinFHEContext (the top-level object, by value)
+    r.top(C_CPARAMS);              // "params": shared_ptr<BinFHECryptoParams>
+    r.top(C_LWEP);                 // "lweparams"
+    c.n = r.u32();
+    c.N = r.u32();
+    c.q = r.integer();
+    c.Q = r.integer();
+    c.qKS = r.integer();
+    c.sigma = f64_of(r.u64());
+    c.sigmaKS = f64_of(r.u64());
+    c.baseKS = r.u32();
+    r.top(C_RGSWP);                // "rgswparams"
+    c.rN = r.u32();
+    c.rQ = r.integer();
+    c.rq = r.integer();
+    c.baseR = r.u32();
+    c.baseG = r.u32();
+    c.method = r.u32();
+    c.rsigma = f64_of(r.u64());
+    c.digitsG = r.u32();
+    bool is_new;                   // "bparams": shared_ptr<ILNativeParams>
+    uint32_t id;
+    if (!r.ptr(is_new, id) || !is_new) throw std::invalid_argument("cereal: context without ring parameters");
+    r.version(C_ILPARAMS, 1);
+    r.version(C_ELEMPARAMS, 1);
+    c.order = r.u32();
+    c.ringDim = r.u32();
+    c.mod = r.integer();
+    c.root = r.integer();
+    c.bigMod = r.integer();
+    c.bigRoot = r.integer();
+    c.numAutoKeys = r.u32();
+    r.done();
+    if (c.rN != c.N || c.rQ != c.Q || c.rq != c.q || c.ringDim != c.N || c.order != 2 * c.N || c.mod != c.Q)
+        throw std::invalid_argument("cereal: inconsistent context parameters");
+    return c;
+}
+
+std::string cereal_write_context(const Params& p) {
+    if (is_large(p.paramset)) throw std::invalid_argument("cereal: context archives of the standard rows only");
+    Writer w;
+    w.version(C_CTX);
+    w.new_ptr();
+    w.version(C_CPARAMS);
+    w.new_ptr();
+    w.version(C_LWEP);
+    w.u32(p.n);
+    w.u32(p.N);
+    w.integer(p.q);
+    w.integer(p.Q);
+    w.integer(p.qKS);
+    w.u64(bits_of(kStdDev));
+    w.u64(bits_of(kStdDev));
+    w.u32(p.baseKS);
+    w.new_ptr();
+    w.version(C_RGSWP);
+    w.u32(p.N);
+    w.integer(p.Q);
+    w.integer(p.q);
+    w.u32(p.baseR);
+    w.u32(p.baseG);
+    w.u32((uint32_t)p.method);
+    w.u64(bits_of(kStdDev));
+    w.u32(p.digitsG);
+    w.new_ptr();
+    w.version(C_ILPARAMS);
+    w.version(C_ELEMPARAMS);
+    w.u32(2 * p.N);
+    w.u32(p.N);
+    w.integer(p.Q);
+    w.integer(p.psi);
+    w.integer(0);
+    w.integer(0);
+    w.u32(p.numAutoKeys);
+    return w.s;
+}
+
+bool cereal_context_paramset(const CerealContext& c, int& paramset, int& method) {
+    for (int ps = 0; ps < paramset_rows(); ++ps) {
+        if (!method_compatible(ps, (int)c.method)) continue;
+        const Params p = make_params(ps, (int)c.method);
+        if (p.n == c.n && p.N == c.N && p.q == c.q && p.Q == c.Q && p.qKS == c.qKS && p.baseKS == c.baseKS &&
+            p.baseR == c.baseR && p.baseG == c.baseG && p.digitsG == c.digitsG && p.numAutoKeys == c.numAutoKeys &&
+            p.psi == c.root && c.sigma == kStdDev && c.sigmaKS == kStdDev && c.rsigma == kStdDev) {
+            paramset = ps;
+            method = (int)c.method;
+            return true;
+        }
+    }
+    return false;
 }
 
 }  // namespace fhe_amd

@@ -42,4 +42,24 @@ struct CerealLwe {
 CerealLwe cereal_read_lwe(const uint8_t* data, size_t size, bool is_key);
 std::string cereal_write_lwe(const uint64_t* a, uint32_t n, uint64_t b, uint64_t mod, bool is_key);
 
+// The key-independent cryptoContext archive: Serial::Serialize(BinFHEContext) (boolean-serial-binary.cpp:
+// 65-71, 108) = BinFHEContext (binfhecontext.h:410-422) -> shared_ptr<BinFHECryptoParams>
+// (binfhe-base-params.h:103-116) -> shared_ptr<LWECryptoParams> (lwe-cryptoparameters.h:182-212) and
+// shared_ptr<RingGSWCryptoParams> (rgsw-cryptoparameters.h:181-214, its ILNativeParams as in the keys)
+struct CerealContext {
+    uint32_t n = 0, N = 0, baseKS = 0;                       // LWECryptoParams
+    uint64_t q = 0, Q = 0, qKS = 0;
+    double sigma = 0, sigmaKS = 0;
+    uint32_t rN = 0, baseR = 0, baseG = 0, method = 0, digitsG = 0, numAutoKeys = 0;  // RingGSWCryptoParams
+    uint64_t rQ = 0, rq = 0;
+    double rsigma = 0;
+    uint32_t order = 0, ringDim = 0;                          // ILNativeParams
+    uint64_t mod = 0, root = 0, bigMod = 0, bigRoot = 0;
+};
+CerealContext cereal_read_context(const uint8_t* data, size_t size);
+std::string cereal_write_context(const Params& p);
+// the GenerateBinFHEContext(set, method) row whose parameters the archive holds (the archive records no
+// set name); false when no supported row matches
+bool cereal_context_paramset(const CerealContext& c, int& paramset, int& method);
+
 }  // namespace fhe_amd

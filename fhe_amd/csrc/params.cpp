@@ -183,6 +183,18 @@ constexpr Row kRows[] = {
 constexpr int kNumRows = (int)(sizeof(kRows) / sizeof(kRows[0]));
 }  // namespace
 
+int paramset_rows() { return kNumRows; }
+
+bool method_compatible(int paramset, int method) {
+    if (paramset < 0 || paramset >= kNumRows) return false;
+    const bool lmk_row = paramset == PS_TOY || paramset == 1 || (paramset >= PS_STD128_LMKCDEY && paramset <= 38) ||
+                         paramset == 41 || paramset == 42;   // TOY, MEDIUM, *_LMKCDEY, LPF_*_LMKCDEY
+    const bool cggi_row = paramset <= 20 || paramset == 39 || paramset == 40 || paramset == 43;  // .. SIGNED_MOD_TEST
+    if (method == M_LMKCDEY) return lmk_row;
+    if (method == M_AP || method == M_GINX) return cggi_row;
+    return false;
+}
+
 Params make_params(int paramset, int method) {
     if (is_large(paramset)) return make_params_large(paramset, method);
     if (paramset < 0 || paramset >= kNumRows) throw std::invalid_argument("unknown parameter set");

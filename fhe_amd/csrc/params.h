@@ -62,5 +62,9 @@ struct Params {
 
 // Throws std::invalid_argument on an unsupported set/method.
 Params make_params(int paramset, int method);
+// the rows of the GenerateBinFHEContext(set, method) table (paramset codes 0 .. count - 1) and
+// isMethodCompatible (binfhe-constants-impl.cpp:266-330)
+int paramset_rows();
+bool method_compatible(int paramset, int method);
 
 }  // namespace fhe_amd

@@ -149,6 +149,15 @@ int fhe_hip_cereal_read_lwe(const uint8_t* data, size_t size, int is_key, uint64
                             uint64_t* b, uint64_t* mod);
 int fhe_hip_cereal_write_lwe(const uint64_t* a, uint32_t n, uint64_t b, uint64_t mod, int is_key, uint8_t* out,
                              size_t cap, size_t* size);
+/* The key-independent cryptoContext archive Serial::Serialize(BinFHEContext, BINARY) (boolean-serial-binary.cpp:
+ * 65-71 writes it, :108 reads it back): BinFHEContext -> BinFHECryptoParams -> LWECryptoParams,
+ * RingGSWCryptoParams (binfhecontext-ser.h:43,49,52-53).  read: the GenerateBinFHEContext(set, method) row
+ * whose parameters the archive holds (the archive names none; FHE_HIP_ERR_INVALID_PARAM if no supported row
+ * matches), with its parameters (out may be NULL).  write: the reference's bytes for a row (out = NULL
+ * reports *size).  create_from_cereal: fhe_hip_create on the row a cryptoContext archive describes. */
+int fhe_hip_cereal_read_context(const uint8_t* data, size_t size, int* paramset, int* method, fhe_hip_params* out);
+int fhe_hip_cereal_write_context(int paramset, int method, uint8_t* out, size_t cap, size_t* size);
+int fhe_hip_create_from_cereal(const uint8_t* data, size_t size, int device, fhe_hip_ctx** out);
 /* EvalBinGate on two packed batches, result packed with out_flags (out = NULL reports *size) */
 int fhe_hip_eval_bingate_packed(fhe_hip_ctx* ctx, int gate, const uint8_t* in1, size_t size1, const uint8_t* in2,
                                 size_t size2, uint32_t out_flags, uint8_t* out, size_t capacity, size_t* size);

@@ -43,6 +43,45 @@ def make_ntt():
         print(name, Q, psi, "ok")
 
 
+def ntt4096_inputs(Q):
+    """BASELINE config 2's batch: 4096 polynomials uniform in [0, Q) (seed 0x5EED0002)"""
+    return np.random.default_rng(0x5EED0002).integers(0, Q, size=(4096, 1024), dtype=np.uint64)
+
+
+def make_ntt4096():
+    """the reference's SwitchFormat (transformnat-impl.h:302-373, 511-624) on config 2's whole 4096-polynomial
+    batch, forward and inverse, as hashes added to tests/golden/ntt_<name>.npz (other fields kept)"""
+    ref = Ref(None, None)
+    for name, Q in NTT_MODULI.items():
+        f = os.path.join(HERE, f"ntt_{name}.npz")
+        g = dict(np.load(f))
+        x = ntt4096_inputs(Q)
+        fwd, psi = ref.ntt(Q, x, inverse=False)
+        inv, _ = ref.ntt(Q, x, inverse=True)
+        assert psi == int(g["psi"])
+        g.update(fwd4096_sha=np.array(sha(fwd)), inv4096_sha=np.array(sha(inv)), seed4096=np.uint64(0x5EED0002))
+        np.savez(f, **g)
+        print(name, "4096 ok", flush=True)
+
+
+# cryptoContext archives (Serial::Serialize(cc, BINARY), boolean-serial-binary.cpp:65-71) the reference writes
+CONTEXTS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "ap": (STD128_AP, AP),
+            "std128_3": (4, GINX), "std192": (9, GINX), "std128_4_lmkcdey": (23, LMKCDEY), "toy_lmkcdey": (0, LMKCDEY)}
+
+
+def make_contexts():
+    import ctypes
+    for name, (ps, m) in CONTEXTS.items():
+        ref = Ref(ps, m)
+        out = ctypes.create_string_buffer(1 << 16)
+        size = ctypes.c_size_t()
+        ref.L.ref_serialize_context.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        assert ref.L.ref_serialize_context(ref.h, out, 1 << 16, ctypes.byref(size)) == 0, ref.err()
+        with open(os.path.join(HERE, f"context_{name}.bin"), "wb") as f:
+            f.write(out.raw[:size.value])
+        print("context", name, size.value, flush=True)
+
+
 GATE_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "ap": (STD128_AP, AP)}
 # the other BINFHE_PARAMSET rows (binfhecontext.cpp:113-159) the device path covers: GINX on every
 # non-LMKCDEY set with N = 1024 / 2048 and a power-of-two baseKS / qKS, LMKCDEY on the N = 1024,
@@ -383,6 +422,10 @@ if __name__ == "__main__":
         make_full(sys.argv[2:] or ("std128", "lmkcdey"))
     if what in ("ntt", "all"):
         make_ntt()
+    if what in ("ntt", "ntt4096", "all"):
+        make_ntt4096()
+    if what in ("contexts", "all"):
+        make_contexts()
     if what in ("gates", "all"):
         make_gates(sys.argv[2:] or ("std128",))
     if what == "wider":   # one process per call keeps the reference's memory bounded

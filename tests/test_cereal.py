@@ -161,3 +161,110 @@ def test_gpu_boolean_serial_binary_flow(tmp_path):
     S.SerializeToFile(tmp_path / "out.txt", res)        # the reference reads what we write (CPU tests)
     back = S.DeserializeFromFile(tmp_path / "out.txt", bf.LWECiphertext)
     assert np.array_equal(back.a, res.a) and back.b == res.b
+
+
+# ---- the cryptoContext archive (BinFHEContext -> BinFHECryptoParams -> LWE / RingGSW parameters) ------
+CONTEXTS = {"std128": (3, 2), "lmkcdey": (21, 3), "ap": (2, 1), "std128_3": (4, 2), "std192": (9, 2),
+            "std128_4_lmkcdey": (23, 3), "toy_lmkcdey": (0, 3)}
+
+
+def same_row(x, y):
+    """two rows with the same parameters (STD128 and STD128_AP, for one, differ only in name)"""
+    import dataclasses
+    return dataclasses.replace(x, paramset=0) == dataclasses.replace(y, paramset=0)
+
+
+def context_fixture(name):
+    with open(os.path.join(GOLD, f"context_{name}.bin"), "rb") as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("name", list(CONTEXTS))
+def test_context_fixture_read_and_rewritten_byte_identically(name):
+    """the reference's own archive (tests/golden/make_golden.py contexts) names its row; our writer
+    reproduces its bytes"""
+    from fhe_amd import binfhe as bf
+    data = context_fixture(name)
+    ps, m = CONTEXTS[name]
+    rps, rm = bf.cereal_read_context(data)
+    assert rm == m and same_row(bf.params(rps, rm), bf.params(ps, m))
+    assert bf.cereal_write_context(rps, rm) == data
+    assert bf.cereal_write_context(ps, m) == data
+
+
+def test_context_archive_errors():
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import FheHipError
+    good = context_fixture("std128")
+    bad_q = bytearray(good)
+    bad_q[29] ^= 0x40      # Q of the LWE parameters: inconsistent with the ring's
+    for bad in (good[:-1], good + b"\0", b"\x00" + good[1:], bytes(bad_q)):
+        with pytest.raises(FheHipError):
+            bf.cereal_read_context(bad)
+    with pytest.raises(FheHipError):
+        bf.cereal_write_context(3, 3)    # STD128 x LMKCDEY: isMethodCompatible refuses it
+
+
+@pytest.mark.slow
+def test_context_archive_every_row_vs_reference():
+    """every compatible (set, method) row: our bytes == Serial::Serialize(cc, BINARY) of the reference's
+    context; our reader maps the reference's archive to a row with the same parameters; the reference
+    deserializes our bytes into a context that serializes back to them"""
+    need_ref()
+    import ctypes
+    from oracle_lib import REF_SO, Ref
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import FheHipError
+    L = ctypes.CDLL(REF_SO)
+    vp = ctypes.c_void_p
+    L.ref_serialize_context.argtypes = [vp, vp, ctypes.c_size_t, vp]
+    L.ref_ctx_from_archive.restype = vp
+    L.ref_ctx_from_archive.argtypes = [vp, ctypes.c_size_t]
+    L.ref_ctx_destroy.argtypes = [vp]
+
+    def ser(h):
+        out, size = ctypes.create_string_buffer(1 << 16), ctypes.c_size_t()
+        assert L.ref_serialize_context(h, out, 1 << 16, ctypes.byref(size)) == 0
+        return out.raw[:size.value]
+
+    rows = 0
+    for ps in range(44):
+        for m in (1, 2, 3):
+            try:
+                ours = bf.cereal_write_context(ps, m)
+            except FheHipError:
+                continue     # incompatible (set, method): the reference refuses it too
+            ref = Ref(ps, m)      # held: its context is destroyed with the object
+            theirs = ser(ref.h)
+            assert ours == theirs, (ps, m)
+            rps, rm = bf.cereal_read_context(theirs)
+            assert rm == m and same_row(bf.params(rps, rm), bf.params(ps, m)), (ps, m, rps)
+            h = L.ref_ctx_from_archive(ours, len(ours))
+            assert h, (ps, m)
+            assert ser(vp(h)) == ours
+            L.ref_ctx_destroy(vp(h))
+            rows += 1
+    assert rows == 70    # 24 rows x {AP, GINX} + 22 rows x LMKCDEY
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["std128", "lmkcdey"])
+def test_gpu_context_from_reference_archive_evaluates_gate_goldens(name):
+    """boolean-serial-binary.cpp:108: a GPU context built from the reference's cryptoContext archive alone
+    (no parameter set given), keys loaded, reproduces the reference's gate outputs (tests/golden/gates_*)"""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import gate_inputs
+    from fhe_amd import binfhe as bf
+    g = np.load(os.path.join(GOLD, f"gates_{name}.npz"))
+    keys, _, _, a1, b1, a2, b2 = gate_inputs(int(g["paramset"]), int(g["method"]), int(g["key_seed"]))
+    e = bf.GateEngine.from_cereal(context_fixture(name))
+    assert (e.params.n, e.params.Q) == (bf.params(int(g["paramset"]), int(g["method"])).n,
+                                        bf.params(int(g["paramset"]), int(g["method"])).Q)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    pg = len(g["bits1"]) // len(g["gates"])
+    for i, gate in enumerate(g["gates"]):
+        sl = slice(i * pg, (i + 1) * pg)
+        ao, bo = e.eval_gate(int(gate), a1[sl], b1[sl], a2[sl], b2[sl])
+        assert np.array_equal(ao, g["out_a"][sl]) and np.array_equal(bo, g["out_b"][sl]), int(gate)
+    e.close()

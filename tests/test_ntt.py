@@ -23,6 +23,12 @@ def inputs(g):
     return Q, int(g["psi"]), x
 
 
+def inputs4096(g):
+    """BASELINE config 2's whole batch (tests/golden/make_golden.py ntt4096_inputs)"""
+    Q = int(g["Q"])
+    return Q, np.random.default_rng(int(g["seed4096"])).integers(0, Q, size=(4096, 1024), dtype=np.uint64)
+
+
 def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a, np.uint64).tobytes()).hexdigest()
 
@@ -74,7 +80,30 @@ def test_oracle_kat_unittesttransform(restatement):
     assert list(r[0]) == [94, 109, 11, 18]
 
 
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_ntt4096_matches_reference_hash(name, restatement):
+    """the restatement on config 2's 4096-polynomial batch == the reference's SwitchFormat (hashes)"""
+    g = gold(name)
+    Q, x = inputs4096(g)
+    psi = int(g["psi"])
+    assert sha(restatement.ntt(Q, psi, x)) == str(g["fwd4096_sha"])
+    assert sha(restatement.ntt(Q, psi, x, inverse=True)) == str(g["inv4096_sha"])
+
+
 # ----------------------------------------------------------------- GPU ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_ntt4096_matches_reference_hash(name):
+    """config 2 as measured (one 4096-polynomial launch per direction: k_ntt1024w / k_ntt1024w64) ==
+    the reference's SwitchFormat on the same 4096 polynomials, forward and inverse"""
+    from fhe_amd import NttPlan
+    g = gold(name)
+    Q, x = inputs4096(g)
+    plan = NttPlan(Q)
+    assert sha(plan.forward(x)) == str(g["fwd4096_sha"])
+    assert sha(plan.inverse(x)) == str(g["inv4096_sha"])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", NAMES)
 def test_gpu_ntt_matches_golden(name):
