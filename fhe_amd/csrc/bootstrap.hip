@@ -1522,6 +1522,25 @@ FHE_DEV DecN make_decn(uint32_t Q, uint32_t g, int nd) {
     }
     return DecN{Q >> 1, C, C - Q, g, M};
 }
+// accumulator I/O of the split kernels' seam instantiations: wave c holds component c in layout C, lane L
+// register r <-> EVAL slot ((r >> 2) << 8) | (L << 2) | (r & 3); conventions as acc_load / acc_store
+FHE_DEV uint32_t slot_c(int L, int r) { return ((uint32_t)(r >> 2) << 8) | ((uint32_t)L << 2) | (uint32_t)(r & 3); }
+FHE_DEV void acc_load_c(uint32_t (&acc)[16], const GateArgs& g, uint32_t gate, int c, int L, uint32_t ninvR,
+                        const Mod& m) {
+    const uint64_t* src = g.acc_io + ((size_t)gate * 2 + c) * g.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = csub(mont_mul((uint32_t)src[slot_c(L, r)], ninvR, m), m.Q);
+}
+FHE_DEV void acc_store_c(const uint32_t (&acc)[16], const GateArgs& g, uint32_t gate, int c, int L, uint32_t nR,
+                         const Mod& m) {
+    uint64_t* dst = g.acc_io + ((size_t)gate * 2 + c) * g.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int32_t v = (int32_t)smont_mul(acc[r], nR, m);
+        dst[slot_c(L, r)] = (uint64_t)(uint32_t)(v < 0 ? v + (int32_t)m.Q : v);
+    }
+}
+
 template <int ND>
 FHE_DEV void decompose_n(uint32_t x, const DecN& c, uint32_t (&d)[ND][16], int r) {
     const uint32_t u = x >= c.Qh ? x + c.CmQ : x + c.C;  // d + C, d = x or x - Q
@@ -1533,7 +1552,8 @@ FHE_DEV void decompose_n(uint32_t x, const DecN& c, uint32_t (&d)[ND][16], int r
 
 // MF: ciphertext modulus 2N (q = 2N sets: STD128_4, LPF_STD128, LPF_STD128Q): any exponent, the
 // full-resolution table psi^e - 1 restricted to e in [0, 2N] (the same LDS footprint as the half table)
-template <int ND, bool MF, typename OutT>
+// ACCIO: the Backend::BlindRotate seam (GateArgs::acc_io), as in k_blind_rotate_ginx
+template <int ND, bool MF, typename OutT, bool ACCIO = false>
 __global__ void __launch_bounds__(128 * kG2Gates, 2)
     k_blind_rotate_ginx2(GateArgs g, BootTables T, const uint4* __restrict__ bsk2, const uint16_t* __restrict__ idx,
                          const uint32_t* __restrict__ tvb, OutT* __restrict__ ext_a, OutT* __restrict__ ext_b,
@@ -1566,7 +1586,9 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
 
     // initial accumulator (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[16];
-    if (c == 1) {
+    if (ACCIO && !g.acc_tv) {
+        acc_load_c(acc, g, gate, c, L, T.ninvR, m);
+    } else if (c == 1) {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
         uint32_t tv[1][16];
 #pragma unroll
@@ -1667,6 +1689,10 @@ __global__ void __launch_bounds__(128 * kG2Gates, 2)
         }
     }
 
+    if (ACCIO) {   // every wave of the workgroup leaves here: no barrier is skipped by some only
+        if (live) acc_store_c(acc, g, gate, c, L, T.nR, m);
+        return;
+    }
     // extraction (binfhe-base-scheme.cpp:110-121): canonical COEF in layout A; wave 0 writes the
     // transposed acc0 (coefficient k -> position N - k, negated), wave 1 the b term from acc1[0]
     __syncthreads();   // the partner wave's last MAC has read this wave's region
@@ -1727,7 +1753,7 @@ hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, con
 
 bool ginx3_supported(const GateArgs& g, const BootTables& t) {
     return t.Q < (1u << 27) && g.N == 1024 && g.ctmod <= 2 * g.N && g.tv == nullptr && g.tv64 == nullptr &&
-           g.acc_io == nullptr && g.gbits >= 2 && 4 * g.gbits <= 32 && g.qKS <= 65536;
+           g.gbits >= 2 && 4 * g.gbits <= 32 && g.qKS <= 65536;
 }
 
 hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, const void* bsk3, const uint16_t* idx,
@@ -1735,20 +1761,23 @@ hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, con
     if (g.count == 0) return hipSuccess;
     if (!ginx3_supported(g, t)) return hipErrorInvalidValue;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, false, uint64_t>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, true, uint64_t>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
+        for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, false, uint64_t>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, true, uint64_t>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, false, uint64_t, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx2<3, true, uint64_t, true>)})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g2_lds(3));
         return true;
     }();
     (void)attr;
     const uint32_t blocks = (g.count + kG2Gates - 1) / kG2Gates;
-    if (g.ctmod == 2 * g.N)
-        hipLaunchKernelGGL((k_blind_rotate_ginx2<3, true, uint64_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s,
-                           g, t, static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd);
-    else
-        hipLaunchKernelGGL((k_blind_rotate_ginx2<3, false, uint64_t>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s,
-                           g, t, static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd);
+#define FHE_LAUNCH_G3(MF, IO)                                                                                    \
+    hipLaunchKernelGGL((k_blind_rotate_ginx2<3, MF, uint64_t, IO>), dim3(blocks), dim3(128 * kG2Gates), g2_lds(3), s, \
+                       g, t, static_cast<const uint4*>(bsk3), idx, tvb, ext_a, ext_b, t.twA_fwd)
+    const bool mf = g.ctmod == 2 * g.N;
+    if (g.acc_io) { if (mf) FHE_LAUNCH_G3(true, true); else FHE_LAUNCH_G3(false, true); }
+    else if (mf) FHE_LAUNCH_G3(true, false);
+    else FHE_LAUNCH_G3(false, false);
+#undef FHE_LAUNCH_G3
     return hipGetLastError();
 }
 
@@ -1794,6 +1823,7 @@ FHE_DEV void automorphism_c(uint32_t (&v)[16], uint32_t* region, int L, uint32_t
 }
 }  // namespace
 
+template <bool ACCIO>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_blind_rotate_lmk3(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
                         const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
@@ -1821,7 +1851,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     // BootstrapGateCore (binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0; then
     // acc1 <- acc1(X^(2N-5)) (:99; acc0 = 0 is invariant)
     uint32_t acc[16];
-    if (c == 1) {
+    if (ACCIO && !g.acc_tv) {
+        acc_load_c(acc, g, gate, c, L, T.ninvR, m);
+        if (c == 1) automorphism_c(acc, region, L, M - 5);   // acc1 <- acc1(X^(2N-5)) (:99)
+    } else if (c == 1) {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
         uint32_t tv[1][16];
 #pragma unroll
@@ -1943,6 +1976,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
     }
 
+    if (ACCIO) {
+        acc_store_c(acc, g, gate, c, L, T.nR, m);
+        return;
+    }
     // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_ginx2
     __syncthreads();
     inv_wave_s<kAccBoundLZ, true>(acc, t0, L, s_tabI, T.w1R, m.oneR, m);
@@ -1965,11 +2002,17 @@ hipError_t launch_blind_rotate_lmk3(const GateArgs& g, const BootTables& t, cons
                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
                                     uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if (!(t.Q < (1u << 27) && g.N == 1024 && g.tv == nullptr && g.tv64 == nullptr && g.acc_io == nullptr &&
-          g.gbits >= 2 && 4 * g.gbits <= 32 && g.qKS <= 65536))
+    if (!(t.Q < (1u << 27) && g.N == 1024 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 &&
+          4 * g.gbits <= 32 && g.qKS <= 65536))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_lmk3, dim3(g.count), dim3(128), l3_lds(), s, g, t, static_cast<const uint4*>(ek),
-                       static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a, ext_b, t.twA_fwd);
+    if (g.acc_io)
+        hipLaunchKernelGGL(k_blind_rotate_lmk3<true>, dim3(g.count), dim3(128), l3_lds(), s, g, t,
+                           static_cast<const uint4*>(ek), static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a,
+                           ext_b, t.twA_fwd);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_lmk3<false>, dim3(g.count), dim3(128), l3_lds(), s, g, t,
+                           static_cast<const uint4*>(ek), static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a,
+                           ext_b, t.twA_fwd);
     return hipGetLastError();
 }
 

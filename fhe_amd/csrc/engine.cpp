@@ -663,7 +663,7 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.acc_io = g.acc_io;
         w.acc_tv = g.acc_tv;
         if (g3_ && p_.method == M_LMKCDEY && d_bsk2_ && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64 &&
-            !g.tv && !g.tv64 && !g.acc_io) {
+            !g.tv && !g.tv64) {
             const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);
             FHE_HIP_CHECK(launch_blind_rotate_lmk3(g, tabs_, ek, ek + (size_t)p_.n * 12288, d_ops_, d_nops_, maxops_,
                                                    d_tvb_, d_wext_a_, d_wext_b_, s));
