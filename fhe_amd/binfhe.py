@@ -156,7 +156,8 @@ def params(paramset, method):
 def kernel_path(paramset, method):
     """the accumulator kernels (paramset, method) runs on, as the engine chooses them
     (fhe_hip_params.kernel): 1 = 32-bit one-wave, 2 = 32-bit split (digitsG = 4), 3 = one gate per
-    workgroup in 32-bit residues, 0 = one gate per workgroup in 64-bit residues"""
+    workgroup in 32-bit residues, 4 = GINX gates at N = 2048 on the register-resident split kernel (the
+    rest as 3), 0 = one gate per workgroup in 64-bit residues"""
     return params(paramset, method).kernel
 
 

@@ -127,6 +127,13 @@ __host__ __device__ constexpr uint32_t g2_key_word(uint32_t nd, uint32_t c, uint
                                                    uint32_t e4) {
     return (((c * 2 * nd + p) * 8 + k2) * 64 + L) * 4 + e4;
 }
+// K1w: GINX at N = 2048, Q < 2^27, digitsG = 4, q < 2N (STD256Q) with the accumulator in registers
+// (two waves per gate); keys in Engine::pack_n2k's layout, tables of Engine::build_tables_n2k (BootTables
+// with 2048-word tabF / tabI and the 2113-pair half monomial table), u64 ctExt into the 64-bit path's
+// workspace
+hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const void* keys, const uint16_t* idx,
+                                   const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
+bool n2k_supported(const GateArgs& g, const BootTables& t);
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);

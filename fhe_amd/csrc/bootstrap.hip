@@ -84,6 +84,9 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_WAVES
 #define FHE_LMK_WAVES 2  // waves per SIMD of the LMKCDEY op-list kernel
 #endif
+#ifndef FHE_LMK_OPAQUE
+#define FHE_LMK_OPAQUE 0 // op-list kernel: per-lane addresses recomputed per op (register pressure)
+#endif
 #ifndef FHE_LMK_PRE
 #define FHE_LMK_PRE 1    // op-list kernel: a pass's 31 per-lane twiddles requested together at its start
 #endif
@@ -1030,6 +1033,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         const uint32_t* twAf = T.twA_fwd;
         const uint32_t* twAi = T.twA_inv;
         asm volatile("" : "+s"(twAf), "+s"(twAi));
+#if FHE_LMK_OPAQUE
+        // the lane index and the wave's LDS regions made opaque per op as well: every per-lane address
+        // of the op body is then derived inside it instead of being hoisted as a loop-invariant VGPR
+        int l_o = l, lane_o = lane;
+        uint32_t *tile_o = tile, *tileW_o = tileW;
+        asm volatile("" : "+v"(l_o), "+v"(lane_o), "+v"(tile_o), "+v"(tileW_o));
+        const int l = l_o, lane = lane_o, xaddr = (lane ^ 32) << 2;
+        uint32_t* const tile  = tile_o;
+        uint32_t* const tileW = tileW_o;
+#endif
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
         uint32_t dA[32], dB[32];
         if (DM || !(op & 0x8000u)) {
@@ -1541,8 +1554,8 @@ FHE_DEV void acc_store_c(const uint32_t (&acc)[16], const GateArgs& g, uint32_t 
     }
 }
 
-template <int ND>
-FHE_DEV void decompose_n(uint32_t x, const DecN& c, uint32_t (&d)[ND][16], int r) {
+template <int ND, int R>
+FHE_DEV void decompose_n(uint32_t x, const DecN& c, uint32_t (&d)[ND][R], int r) {
     const uint32_t u = x >= c.Qh ? x + c.CmQ : x + c.C;  // d + C, d = x or x - Q
     const int32_t w  = (int32_t)(u ^ c.M);
 #pragma unroll
@@ -2013,6 +2026,422 @@ hipError_t launch_blind_rotate_lmk3(const GateArgs& g, const BootTables& t, cons
         hipLaunchKernelGGL(k_blind_rotate_lmk3<false>, dim3(g.count), dim3(128), l3_lds(), s, g, t,
                            static_cast<const uint4*>(ek), static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a,
                            ext_b, t.twA_fwd);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// K1w: GINX at N = 2048 with the accumulator in registers (k_blind_rotate_n2k<ND, ACCIO>) for the
+// Q < 2^27 rows with even monomial exponents (ciphertext modulus q < 2N): STD256Q (digitsG = 4,
+// ND = 3 retained digits), which otherwise run the one-gate-per-workgroup accumulator K5
+// (bootstrap_wide.hip) with every butterfly through LDS.  As K1s, wave c of a gate owns RLWE
+// component c, here as 32 registers x 64 lanes, through the three layouts (x: 11-bit coefficient
+// or EVAL slot index)
+//   A: lane = x5..x0, register = x10..x6      (COEF; forward stages on bits 10..6, uniform twiddles)
+//   B: lane = (x10..x6) << 1 | x0, register = x5..x1   (stages on bits 5..1, per-lane twiddles)
+//   C: lane = x6..x1, register = (x10..x7) << 1 | x0   (EVAL; the stage on bit 0)
+// with one LDS tile per wave (word of x: x + 2 (x >> 6): A and B conflict-free, C moved as 8-byte
+// pairs).  Per index i (AddToAccCGGI, rgsw-acc-cggi.cpp:102-151): wave c inverse-transforms acc_c
+// (signed, its own reduction plan), decomposes it into its ND digits (SignedDigitDecompose,
+// rgsw-acc.cpp:54-91; rows 2j + c of the RGSW keys) and forward-transforms them; it then multiplies
+// its own digits by the key columns of BOTH components: the sum for its own component stays in its
+// registers, the other one is reduced to a word per slot and handed to the partner through this
+// wave's tile (8 KiB instead of the ND digit polynomials: four gates per CU fit in LDS), and after
+// one barrier each wave adds the partner's word.  acc_c <- acc_c + S+_c (X^a - 1) + S-_c (X^-a - 1)
+// exactly as in K1s; only the order of the modular additions differs.
+// Keys (Engine::pack_n2k, u32 Montgomery with N^-1 folded in), per index and wave c:
+//   [c][q < 2 ND][k2 < 16][64 lanes] uint4 = (K+[r], K+[r + 1], K-[r], K-[r + 1]), r = 2 k2, slot
+//   x(L, r) of layout C; q = 2 j + o: digit row 2 j + c, column c (o = 0) or 1 - c (o = 1).
+// Bounds (Q < 2^27): digits |d| <= 2^(g-1) grow to < 11 Q + 2^(g-1) in the forward transform;
+// |S+-| < ND (11 Q + 2^(g-1)) Q; each reduced sum < 2.6 Q; acc < 5.3 Q after the exchange (the
+// inverse plan's BIN).
+// ===========================================================================
+namespace {
+#ifndef FHE_N2K_OPAQUE
+#define FHE_N2K_OPAQUE 0
+#endif
+#ifndef FHE_N2K_KPF
+#define FHE_N2K_KPF 1   // key chunks requested ahead of their MAC (0: on use)
+#endif
+constexpr int kW2Gates = 2;               // gates per workgroup (2 waves each)
+constexpr int kW2Tile  = 2048 + 64;       // words of one wave's tile
+constexpr int kW2Mono  = 2048 + 1 + 64;   // (plain, Montgomery) pairs psi^(2f) - 1, f in [0, 2048], entry f + (f >> 5)
+constexpr int kW2AccBound = 53;           // |acc| < 5.3 Q between indices (units of Q/10)
+constexpr size_t w2_lds() { return (size_t)(2048 + 2048 + 2 * kW2Mono + 2 * kW2Gates * kW2Tile) * 4; }
+// LDS word of x: x + 2 (x >> 6) (wa2k / wb2k / wc2k below)
+FHE_DEV uint32_t slot_2k(int L, int r) {
+    return ((uint32_t)(r >> 1) << 7) | ((uint32_t)L << 1) | (uint32_t)(r & 1);
+}
+
+// signed forward NTT, layout A (|v| < B) -> C (|v| < B + 11 Q), NP polynomials through one tile
+// (transposed one after the other); twA: Table[0..31] (uniform), s_tab: Table[0..2047] in LDS
+// word of x in each layout as a per-lane base plus a per-register constant (so that every LDS access
+// is base + immediate): A x = (r << 6) | L -> L + 66 r; B x = (G << 6) | (r << 1) | j -> 66 G + j + 2 r;
+// C pair x = (rh << 7) | (L << 1) -> 2 L + 2 (L >> 5) + 132 rh
+FHE_DEV int wa2k(int L) { return L; }
+FHE_DEV int wb2k(int L) { return 66 * (L >> 1) + (L & 1); }
+FHE_DEV int wc2k(int L) { return 2 * L + 2 * (L >> 5); }
+
+template <int NP>
+FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t* __restrict__ twA,
+                      const uint32_t* s_tab, const Mod& m) {
+    const int G = L >> 1;
+    uint32_t* ta = t + wa2k(L);
+    uint32_t* tb = t + wb2k(L);
+    uint32_t* tc = t + wc2k(L);
+#pragma unroll
+    for (int b = 10; b >= 6; --b) {
+        const int rb = b - 6;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            const uint32_t w = twA[(1 << (10 - b)) + (r >> (rb + 1))];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {  // A -> B
+#pragma unroll
+        for (int r = 0; r < 32; ++r) ta[66 * r] = v[p][r];
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[p][r] = tb[2 * r];
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int b = 5; b >= 1; --b) {
+        const int rb = b - 1;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            const uint32_t w = s_tab[(1 << (10 - b)) + (G << (5 - b)) + (r >> b)];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {  // B -> C
+#pragma unroll
+        for (int r = 0; r < 32; ++r) tb[2 * r] = v[p][r];
+        wave_lds_sync();
+#pragma unroll
+        for (int rh = 0; rh < 16; ++rh) {
+            const uint2 q = *reinterpret_cast<const uint2*>(tc + 132 * rh);
+            v[p][2 * rh]     = q.x;
+            v[p][2 * rh + 1] = q.y;
+        }
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int rh = 0; rh < 16; ++rh) {
+        const uint32_t w = s_tab[1024 + (rh << 6) + L];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) ct_bf_s(v[p][2 * rh], v[p][2 * rh + 1], w, m);
+    }
+}
+
+// the signed inverse's reduction plan (as InvPlanS / make_inv_plan_ww): stage st = 0 (C, register bit
+// 0), 1..5 (B, register bits 0..4), 6..9 (A, register bits 0..3), 10 (the last, register bit 4); a
+// transpose precedes stages 1 and 6
+struct InvPlan2k {
+    bool red[11][32];
+    int fin[16];
+};
+template <int BIN, int LIM>
+constexpr InvPlan2k make_inv_plan_2k() {
+    InvPlan2k p{};
+    int B[32] = {};
+    for (int r = 0; r < 32; ++r) B[r] = BIN;
+    const int bits[11] = {0, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4};
+    for (int st = 0; st < 11; ++st) {
+        if (st == 1 || st == 6) {
+            int U = 0;
+            for (int r = 0; r < 32; ++r) U = B[r] > U ? B[r] : U;
+            for (int r = 0; r < 32; ++r) B[r] = U;
+        }
+        const int bt = bits[st];
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << bt)) continue;
+            const int q = r | (1 << bt);
+            while (B[r] + B[q] > LIM) {
+                const int e = B[r] >= B[q] ? r : q;
+                B[e]        = 10;
+                p.red[st][e] = true;
+            }
+            if (st == 10) {
+                int f = 0;
+                while ((10 << f) < B[r] + B[q]) ++f;
+                p.fin[r] = f;
+            }
+            B[r] = B[r] + B[q];
+            B[q] = 10;
+        }
+    }
+    return p;
+}
+// signed inverse NTT, layout C (EVAL, |v| < BIN Q / 10) -> A (COEF), canonical [0, Q); the keys carry
+// N^-1, so the last stage scales by TableI[1] only (w1R)
+template <int BIN>
+FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __restrict__ twAi,
+                      const uint32_t* s_tabI, uint32_t w1R, uint32_t oneR, const Mod& m) {
+    constexpr InvPlan2k P = make_inv_plan_2k<BIN, 160>();
+    auto redp = [&](int st) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r)
+            if (P.red[st][r]) v[r] = smont_mul(v[r], oneR, m);
+    };
+    auto gs = [&](uint32_t& x, uint32_t& y, uint32_t w) {
+        const uint32_t s = x + y;
+        y                = smont_mul(x - y, w, m);
+        x                = s;
+    };
+    const int G = L >> 1;
+    uint32_t* ta = t + wa2k(L);
+    uint32_t* tb = t + wb2k(L);
+    uint32_t* tc = t + wc2k(L);
+    redp(0);
+#pragma unroll
+    for (int rh = 0; rh < 16; ++rh) gs(v[2 * rh], v[2 * rh + 1], s_tabI[1024 + (rh << 6) + L]);
+    // C -> B
+#pragma unroll
+    for (int rh = 0; rh < 16; ++rh)
+        *reinterpret_cast<uint2*>(tc + 132 * rh) = make_uint2(v[2 * rh], v[2 * rh + 1]);
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = tb[2 * r];
+    wave_lds_sync();
+#pragma unroll
+    for (int b = 1; b <= 5; ++b) {
+        const int rb = b - 1;
+        redp(b);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            gs(v[r], v[r | (1 << rb)], s_tabI[(1 << (10 - b)) + (G << (5 - b)) + (r >> b)]);
+        }
+    }
+    // B -> A
+#pragma unroll
+    for (int r = 0; r < 32; ++r) tb[2 * r] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = ta[66 * r];
+    wave_lds_sync();
+#pragma unroll
+    for (int b = 6; b <= 9; ++b) {
+        const int rb = b - 6;
+        redp(b);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & (1 << rb)) continue;
+            gs(v[r], v[r | (1 << rb)], twAi[(1 << (10 - b)) + (r >> (rb + 1))]);
+        }
+    }
+    // bit 10 (transformnat-impl.h:599-623), canonical results as inv_pass_s
+    redp(10);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t x = v[r], y = v[r | 16];
+        uint32_t s       = x + y + (m.Q << P.fin[r]);
+#pragma unroll
+        for (int f = P.fin[r]; f >= 0; --f) s = csub(s, m.Q << f);
+        const uint32_t d = smont_mul(x - y, w1R, m);
+        v[r]             = s;
+        v[r | 16]        = min(d, d + m.Q);
+    }
+}
+}  // namespace
+
+template <int ND, bool ACCIO>
+__global__ void __launch_bounds__(128 * kW2Gates, 2)
+    k_blind_rotate_n2k(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
+                       const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
+                       const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
+    constexpr int kQ = 2 * ND;  // key vectors per slot pair: ND digit rows x 2 columns
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_tab  = sm;
+    uint32_t* s_tabI = sm + 2048;
+    uint2* s_mono2   = reinterpret_cast<uint2*>(sm + 4096);
+    uint32_t* s_tile = sm + 4096 + 2 * kW2Mono;
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) {
+        s_tab[i]  = T.tabF[i];
+        s_tabI[i] = T.tabI[i];
+    }
+    for (int i = threadIdx.x; i < kW2Mono; i += blockDim.x) s_mono2[i] = make_uint2(T.monoP[i], T.mono[i]);
+
+    const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int c = wave & 1;  // RLWE component of this wave
+    const uint32_t gslot = blockIdx.x * kW2Gates + (wave >> 1);
+    const bool live = gslot < g.count;
+    const uint32_t gate = live ? gslot : g.count - 1;  // spare waves shadow the last gate: every wave meets every barrier
+    uint32_t* tile    = s_tile + wave * kW2Tile;
+    uint32_t* partner = s_tile + (wave ^ 1) * kW2Tile;
+    const Mod m0 = make_mod(T);
+    const Mod& m = m0;
+    __syncthreads();
+
+    // initial accumulator (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
+    uint32_t acc[32];
+    if (ACCIO && !g.acc_tv) {
+        const uint64_t* src = g.acc_io + ((size_t)gate * 2 + c) * g.N;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = csub(mont_mul((uint32_t)src[slot_2k(L, r)], T.ninvR, m), m.Q);
+    } else if (c == 1) {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        uint32_t tv[1][32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            uint32_t v       = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v                 = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            tv[0][r] = v;
+        }
+        fwd_2k_s<1>(tv, tile, L, twAf, s_tab, m);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
+    } else {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = 0;
+    }
+
+    const uint16_t* gidx = idx + (size_t)gate * g.n;
+    const DecN dec       = make_decn(m.Q, g.gbits, ND);
+    // monomial of slot x(L, r): e = m (2 brv11(x) + 1) mod 2N, m = a 2N / ctmod even, in half units
+    // f = e / 2 = as (32 brv6(L) + 1) + as 2 brv4(r >> 1) mod 2048 (bit 0 of x adds as 2048 = 0)
+    const uint32_t lmul = 32 * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1;
+    const uint4* kc     = keys + (size_t)c * (kQ * 16 * 64) + L;
+    for (uint32_t i = 0; i < g.n; ++i) {
+        const Mod m       = fresh_nq(m0);
+        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> 1;
+        const uint4* kb   = kc + (size_t)i * (2 * kQ * 16 * 64);
+        // the uniform twiddles re-read per index (hoisted, the 62 of them would sit in VGPRs across the loop)
+        const uint32_t* twF = twAf;
+        const uint32_t* twI = twAi;
+        asm volatile("" : "+s"(twF), "+s"(twI));
+#if FHE_N2K_OPAQUE
+        // the lane index and this wave's tiles opaque per index: the per-lane LDS bases are re-derived
+        // inside the body instead of being kept (spilled) across the loop
+        int L_o = L;
+        uint32_t *tile_o = tile, *partner_o = partner;
+        asm volatile("" : "+v"(L_o), "+v"(tile_o), "+v"(partner_o));
+        const int L = L_o;
+        uint32_t* const tile    = tile_o;
+        uint32_t* const partner = partner_o;
+#endif
+        constexpr int KB = FHE_N2K_KPF + 1;
+        uint4 kq[KB][kQ];
+        __syncthreads();  // the partner has read this wave's tile (previous index)
+        uint32_t d[ND][32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
+        inv_2k_s<kW2AccBound>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+        fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
+        const uint32_t fl = (as * lmul) & 2047u;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) kq[0][q] = kb[(q * 16 + 0) * 64];
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) {
+            if (KB == 2 && k2 + 1 < 16) {
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) kq[(k2 + 1) % KB][q] = kb[(q * 16 + k2 + 1) * 64];
+            } else if (KB == 1 && k2 > 0) {
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) kq[0][q] = kb[(q * 16 + k2) * 64];
+            }
+            asm volatile("" ::: "memory");
+            const uint32_t ur = __builtin_amdgcn_readfirstlane(
+                (as * 2u * (__builtin_bitreverse32((uint32_t)k2) >> 28)) & 2047u);
+            const uint32_t f = (fl + ur) & 2047u, fn = 2048u - f;
+            const uint2 mp = s_mono2[f + (f >> 5)], mn = s_mono2[fn + (fn >> 5)];
+            const uint4* q4 = kq[k2 % KB];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r = 2 * k2 + e;
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {  // o = 0: this wave's component, 1: the partner's
+                    int64_t S1 = 0, S2 = 0;
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) {
+                        const uint4 kv = q4[2 * j + o];
+                        S1 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.y : kv.x);
+                        S2 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.w : kv.z);
+                    }
+                    int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
+                    S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
+                    if (o == 0) {
+                        S += (int64_t)(int32_t)acc[r] * (int32_t)T.oneR;
+                        acc[r] = smont_red(S, m);
+                    } else {
+                        tile[(r << 6) | L] = smont_red(S, m);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // both waves' partner words are in LDS
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] += partner[(r << 6) | L];
+    }
+
+    if (ACCIO) {  // every wave of the workgroup leaves here: no barrier is skipped by some only
+        if (live) {
+            uint64_t* dst = g.acc_io + ((size_t)gate * 2 + c) * g.N;
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const int32_t v = (int32_t)smont_mul(acc[r], T.nR, m);
+                dst[slot_2k(L, r)] = (uint64_t)(uint32_t)(v < 0 ? v + (int32_t)m.Q : v);
+            }
+        }
+        return;
+    }
+    // extraction (binfhe-base-scheme.cpp:110-121): canonical COEF in layout A; wave 0 writes the
+    // transposed acc0 (coefficient k -> position N - k, negated), wave 1 the b term from acc1[0]
+    __syncthreads();  // the partner has read this wave's tile
+    inv_2k_s<kW2AccBound>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
+    if (!live) return;
+    if (c == 0) {
+        uint64_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            const uint32_t v = acc[r];
+            const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
+            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+        }
+    } else if (L == 0) {
+        const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
+        ext_b[gate]       = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+bool n2k_supported(const GateArgs& g, const BootTables& t) {
+    return t.Q < (1u << 27) && g.N == 2048 && g.ctmod < 2 * g.N && g.tv == nullptr && g.tv64 == nullptr &&
+           g.gbits >= 2 && 4 * g.gbits <= 32;
+}
+
+hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const void* keys, const uint16_t* idx,
+                                   const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!n2k_supported(g, t)) return hipErrorInvalidValue;
+    static const bool attr = [] {
+        for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true>)})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)w2_lds());
+        return true;
+    }();
+    (void)attr;
+    const uint32_t blocks = (g.count + kW2Gates - 1) / kW2Gates;
+    const uint4* k = static_cast<const uint4*>(keys);
+    if (g.acc_io)
+        hipLaunchKernelGGL((k_blind_rotate_n2k<3, true>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), s, g, t, k,
+                           idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+    else
+        hipLaunchKernelGGL((k_blind_rotate_n2k<3, false>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), s, g, t, k,
+                           idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
     return hipGetLastError();
 }
 

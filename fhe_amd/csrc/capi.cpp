@@ -72,7 +72,7 @@ struct fhe_hip_ctx {
 
 static void fill_params(const Params& p, fhe_hip_params* o) {
     o->paramset = p.paramset; o->method = p.method; o->n = p.n; o->N = p.N; o->q = p.q; o->qKS = p.qKS;
-    o->kernel = Engine::fast_path(p) ? 1u : Engine::g3_set(p) ? 2u : Engine::narrow_set(p) ? 3u : 0u;
+    o->kernel = Engine::fast_path(p) ? 1u : Engine::g3_set(p) ? 2u : Engine::n2k_set(p) ? 4u : Engine::narrow_set(p) ? 3u : 0u;
     o->baseKS = p.baseKS; o->digitsKS = p.digitsKS; o->baseG = p.baseG; o->digitsG = p.digitsG;
     o->numAutoKeys = p.numAutoKeys; o->keyDist = p.keyDist; o->Q = p.Q; o->psi = p.psi;
     o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows_all();

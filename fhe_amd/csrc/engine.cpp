@@ -40,6 +40,86 @@ bool Engine::g3_set(const Params& p) {
            p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.qKS <= 65536 && p.n < 1024;
 }
 
+bool Engine::n2k_set(const Params& p) {
+    const uint64_t g = p.gBits, h = 1ull << (g - 1);
+    const uint64_t C = h * (1 + (1ull << g) + (1ull << (2 * g)) + (1ull << (3 * g)));
+    return !is_large(p.paramset) && !p.timeopt && p.method == M_GINX && p.N == 2048 && p.Q < (1ull << 27) &&
+           p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.q < 2 * p.N;
+}
+
+// K1w tables (bootstrap.hip k_blind_rotate_n2k): Table / TableI (2048 words each, u32 Montgomery; the
+// uniform stages read words 0..31 of them), the half-resolution monomial pairs psi^(2f) - 1 for
+// f in [0, 2048] at f + (f >> 5)
+void Engine::build_tables_n2k() {
+    const uint64_t Q = p_.Q;
+    HostNtt h;
+    h.init(p_.N, Q, p_.psi);
+    constexpr size_t kMono = 2048 + 1 + 64;
+    std::vector<uint32_t> t(2048 + 2048 + 2 * kMono, 0);
+    uint32_t* tabF = t.data();
+    uint32_t* tabI = tabF + 2048;
+    uint32_t* mono = tabI + 2048;
+    uint32_t* monoP = mono + kMono;
+    for (uint32_t i = 0; i < 2048; ++i) {
+        tabF[i] = to_mont(h.tab[i], Q);
+        tabI[i] = to_mont(h.tabI[i], Q);
+    }
+    const uint64_t psi2 = mulmod(p_.psi, p_.psi, Q);
+    uint64_t x = 1;
+    for (uint32_t f = 0; f <= 2048; ++f) {
+        mono[f + (f >> 5)]  = to_mont(submod(x, 1, Q), Q);
+        monoP[f + (f >> 5)] = (uint32_t)submod(x, 1, Q);
+        x = mulmod(x, psi2, Q);
+    }
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    FHE_HIP_CHECK(hipMalloc(&d_tables2k_, t.size() * 4));
+    FHE_HIP_CHECK(hipMemcpy(d_tables2k_, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    const uint32_t* d = static_cast<const uint32_t*>(d_tables2k_);
+    tabs2k_ = BootTables{};
+    tabs2k_.tabF = d;
+    tabs2k_.tabI = d + 2048;
+    tabs2k_.twA_fwd = tabs2k_.tabF;
+    tabs2k_.twA_inv = tabs2k_.tabI;
+    tabs2k_.mono = d + 4096;
+    tabs2k_.monoP = tabs2k_.mono + kMono;
+    tabs2k_.Q = (uint32_t)Q;
+    tabs2k_.Q2 = (uint32_t)(2 * Q);
+    tabs2k_.qinv = neg_inv32((uint32_t)Q);
+    tabs2k_.ninvR = to_mont(h.ninv, Q);
+    tabs2k_.w1R = to_mont(h.tabI[1], Q);
+    tabs2k_.oneR = to_mont(1, Q);
+    tabs2k_.nR = to_mont(p_.N, Q);
+}
+
+// K1w key layout, u32 Montgomery with N^-1 folded in, per index i and wave c:
+// [c][q < 6][k2 < 16][64][4] = (K+[r], K+[r+1], K-[r], K-[r+1]), r = 2 k2 + e, slot x(L, r) of layout C,
+// q = 2 j + o: digit row 2 j + c, column c (o = 0) or 1 - c (o = 1); raw BSK [n][2][dG2 = 6][2][N]
+void Engine::pack_n2k(const uint64_t* bsk) {
+    const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
+    const uint64_t Q = p_.Q, ninv = invmod(N, Q);
+    const size_t per = (size_t)2 * 6 * 16 * 64 * 4;
+    std::vector<uint32_t> dev((size_t)n * per);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i)
+        for (uint32_t c = 0; c < 2; ++c)
+            for (uint32_t q = 0; q < 6; ++q)
+                for (uint32_t k2 = 0; k2 < 16; ++k2)
+                    for (uint32_t L = 0; L < 64; ++L)
+                        for (uint32_t e4 = 0; e4 < 4; ++e4) {
+                            const uint32_t r = 2 * k2 + (e4 & 1), ks = e4 >> 1;
+                            const uint32_t x = ((r >> 1) << 7) | (L << 1) | (r & 1);
+                            const uint32_t row = 2 * (q >> 1) + c, col = (q & 1) ? 1 - c : c;
+                            const size_t src = ((((size_t)i * 2 + ks) * dG2 + row) * 2 + col) * N + x;
+                            dev[(size_t)i * per + ((((c * 6 + q) * 16 + k2) * 64 + L) * 4 + e4)] =
+                                to_mont(mulmod(bsk[src] % Q, ninv, Q), Q);
+                        }
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    if (d_bsk2_) FHE_HIP_CHECK(hipFree(d_bsk2_));
+    d_bsk2_ = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&d_bsk2_, dev.size() * 4));
+    FHE_HIP_CHECK(hipMemcpy(d_bsk2_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+}
+
 // the split kernels' nd = 3 key layouts, u32 Montgomery with N^-1 folded in (as the resident 32-bit
 // layouts).  GINX (boot.h g2_key_word) from the raw BSK [n][2][dG2 = 8][2][N]; LMKCDEY
 // (launch_blind_rotate_lmk3) from [n][dG2][2][N] ++ [numAutoKeys + 1][3][2][N]
@@ -119,6 +199,11 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
             g3_ = !(e && std::string(e) == "0");
             if (g3_) build_tables();
         }
+        if (n2k_set(p_)) {
+            const char* e = std::getenv("FHE_HIP_N2K");
+            n2k_ = !(e && std::string(e) == "0");
+            if (n2k_) build_tables_n2k();
+        }
         if (method == M_LMKCDEY) {  // op lists (k_prep_lmk_w) for k_blind_rotate_wide_ops
             if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");
             build_loggen();
@@ -146,7 +231,7 @@ Engine::~Engine() {
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
                       (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
-                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_})
+                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_, d_tables2k_})
         if (ptr) (void)hipFree(ptr);
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -372,6 +457,7 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
         FHE_HIP_CHECK(hipMalloc(&d_bsk_, words * wb));
         FHE_HIP_CHECK(hipMemcpy(d_bsk_, dev.data(), words * wb, hipMemcpyHostToDevice));
         if (g3_) pack_ginx3(bsk);
+        if (n2k_) pack_n2k(bsk);
         return;
     }
     const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
@@ -673,6 +759,11 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
             const bool dm = p_.method == M_AP;
             FHE_HIP_CHECK(launch_blind_rotate_wide_ops(w, wtabs_, wkey(0), wkey(dm ? 0 : (size_t)p_.n * p_.digitsG2 * 2 * p_.N),
                                                        d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, dm, s));
+            return;
+        }
+        if (n2k_ && d_bsk2_ && n2k_supported(g, tabs2k_) && g.lv == g.lv64 && g.uv == g.uv64 &&
+            g.b_const == g.b64) {
+            FHE_HIP_CHECK(launch_blind_rotate_n2k(g, tabs2k_, d_bsk2_, d_idx_, d_tvb_, d_wext_a_, d_wext_b_, s));
             return;
         }
         if (g3_ && d_bsk2_ && ginx3_supported(g, tabs_) && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64) {

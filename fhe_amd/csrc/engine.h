@@ -58,6 +58,7 @@ public:
     static bool narrow_set(const Params& p);  // the 64-bit accumulator runs its 32-bit policy (A32)
     // the digitsG = 4 sets at N = 1024, Q < 2^27 the split kernels take (K1s / K1m)
     static bool g3_set(const Params& p);
+    static bool n2k_set(const Params& p);     // GINX gates on K1w (N = 2048 in registers)
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -197,6 +198,14 @@ private:
     // 32-bit tables tabs_, the rest of the 64-bit path unchanged.  FHE_HIP_GINX3=0 keeps them on the 64-bit accumulator (A/B, tests).
     bool g3_ = false;
     void pack_ginx3(const uint64_t* bsk);
+    // GINX at N = 2048, Q < 2^27, digitsG = 4, q < 2N (STD256Q): gates on K1w (launch_blind_rotate_n2k)
+    // over its own 32-bit tables, keys packed into d_bsk2_; the rest of the 64-bit path (prep, key
+    // switch, functional bootstrapping) unchanged.  FHE_HIP_N2K=0 keeps them on K5 (A/B, tests).
+    bool n2k_ = false;
+    BootTables tabs2k_{};
+    void* d_tables2k_ = nullptr;
+    void build_tables_n2k();
+    void pack_n2k(const uint64_t* bsk);
     // cross-stream ordering (use_stream)
     hipStream_t last_stream_ = nullptr;
     hipEvent_t order_ev_ = nullptr;

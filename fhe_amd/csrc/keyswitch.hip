@@ -117,7 +117,10 @@ constexpr int kKsIPR = 4;                 // values of i per round (4: one uint4
 #define FHE_KS_WIDE_BATCH 16384
 #endif
 constexpr uint32_t kKsWideBatch = FHE_KS_WIDE_BATCH;  // from here: G 512, IPR 2
-constexpr int kKsSplitG = 512;            // the row split's gate tile
+constexpr int kKsSplitG = 512;
+#ifndef FHE_KS_XCD
+#define FHE_KS_XCD 0
+#endif            // the row split's gate tile
 // LOGB = log2(baseKS): 5 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 6 (STD128_3/4,
 // LPF_STD128Q: 64 slices, 2 values of i per round so that the double buffer keeps the same 104 KB;
 // slices d and d + 32 share a bank slot, a 2-way conflict)
@@ -144,9 +147,18 @@ __global__ void __launch_bounds__(G)
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
     __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][kBase * kKsRowB];
     const uint32_t t = threadIdx.x;
-    const uint32_t gate = blockIdx.x * G + t;
+    // FHE_KS_XCD: workgroups are dispatched round-robin over the 8 XCDs by linear id, so with the
+    // 8 column tiles of a 512-column KSK mapped to (linear id mod 8) every XCD stages one column
+    // tile only and its workgroups share each staged slice through that XCD's L2
+    uint32_t bx = blockIdx.x, by = blockIdx.y;
+    if (FHE_KS_XCD && !SPLIT && gridDim.y == 8) {
+        const uint32_t lin = blockIdx.x + blockIdx.y * gridDim.x;
+        by = lin & 7u;
+        bx = lin >> 3;
+    }
+    const uint32_t gate = bx * G + t;
     const bool valid = gate < g.count;
-    const uint32_t col0 = blockIdx.y * kKsCols;
+    const uint32_t col0 = by * kKsCols;
     const uint32_t rounds = SPLIT ? g.N / kIPR / gridDim.z : g.N / kIPR;  // this workgroup's share
     const uint32_t r0 = SPLIT ? blockIdx.z * rounds : 0;
     using AV = typename std::conditional<kIPR == 4, uint4, uint2>::type;

@@ -91,6 +91,8 @@ typedef struct {
                          Q < 2^28, digitsG = 3); 2 = 32-bit split, two waves per gate (digitsG = 4, N = 1024,
                          Q < 2^27); 3 = the one-gate-per-workgroup accumulator with 32-bit residues
                          (Q < 2^30, digitsG2 Q < 2^32: the N = 2048 STD256 / STD256Q rows, TOY, ...);
+                         4 = GINX gates at N = 2048, Q < 2^27, digitsG = 4, q < 2N (STD256Q) with the
+                         accumulator in registers, two waves per gate (the rest as 3);
                          0 = the same accumulator with 64-bit residues (every other set, the
                          large-precision family) */
     uint64_t Q, psi, qKS, bsk_words, ksk_rows;  /* ksk_rows: of the raw layout (timeOptimization: 3 keys) */
