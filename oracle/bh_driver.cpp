@@ -16,9 +16,16 @@
 //   null accumulators    BootstrapGateCore(AND, ct + q/4) (binfhe-base-scheme.cpp:190-205, 525-583),
 //                        and lux::fhe::BootstrapBatch / KeySwitchBatch / ModSwitchBatch (batch.cpp:53-104,
 //                        251-314) with BackendHIP as the registry's default
+#include <execinfo.h>
+#include <fcntl.h>
 #include <omp.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -36,6 +43,53 @@ using namespace lux::fhe;
 using namespace lux::fhe::backend;
 
 extern "C" void* ref_ctx_context(void* h);  // ref_driver.cpp
+
+namespace {
+// test diagnostics: the native stack of the first thread that faults (FHE_SEGV_TRACE=1, tests/conftest.py)
+std::atomic<int> g_fault{0};
+void on_fault(int sig, siginfo_t* si, void*) {
+    if (g_fault.exchange(1) == 0) {
+        char msg[128];
+        const int len = snprintf(msg, sizeof msg, "\n[segv-trace] signal %d at address %p, thread %ld\n", sig,
+                                 si->si_addr, (long)syscall(SYS_gettid));
+        (void)!write(2, msg, len);
+        void* frames[64];
+        const int n = backtrace(frames, 64);
+        backtrace_symbols_fd(frames, n, 2);
+        const int fd = open("/proc/self/maps", O_RDONLY);
+        char buf[4096];
+        for (ssize_t r; fd >= 0 && (r = read(fd, buf, sizeof buf)) > 0;)
+            (void)!write(2, buf, r);
+        signal(sig, SIG_DFL);
+        raise(sig);
+    }
+    for (;;)
+        pause();
+}
+
+bool g_trace = false;
+void step(const char* what) {
+    if (g_trace)
+        fprintf(stderr, "[bh] %s\n", what);
+}
+}  // namespace
+
+extern "C" void bh_install_fault_trace() {
+    void* warm[4];
+    backtrace(warm, 4);  // loads the unwinder now, not inside the handler
+    static char alt[1 << 16];
+    stack_t ss{};
+    ss.ss_sp   = alt;
+    ss.ss_size = sizeof alt;
+    sigaltstack(&ss, nullptr);
+    g_trace = true;
+    struct sigaction sa {};
+    sa.sa_sigaction = on_fault;
+    sa.sa_flags     = SA_SIGINFO | SA_ONSTACK;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+    sigaction(SIGABRT, &sa, nullptr);
+}
 
 namespace {
 
@@ -121,10 +175,13 @@ const char* bh_last_error() {
 // BackendRegistry::Instance().Register(BackendHIP) + SetDefault, for the context's parameter set
 int bh_register(int paramset, int method, int device) {
     return guarded([&] {
+        step("register: BackendHIP");
         auto be = std::make_unique<BackendHIP>(static_cast<BINFHE_PARAMSET>(paramset),
                                                static_cast<BINFHE_METHOD>(method), device);
         g_be = be.get();
+        step("register: Register");
         BackendRegistry::Instance().Register(std::move(be));
+        step("register: done");
         BackendRegistry::Instance().SetDefault(kBackendHIP);
         if (CurrentBackend() != g_be)
             throw std::runtime_error("registry does not return the registered backend");
@@ -443,12 +500,15 @@ int bh_eval_gates_routed(void* h, int gate, size_t count, const uint64_t* a1, co
         const uint64_t q  = lp->Getq().ConvertToInt();
         auto c1 = lwe_vec(a1, b1, count, lp->Getn(), q), c2 = lwe_vec(a2, b2, count, lp->Getn(), q);
         std::vector<LWECiphertext> out, ref;
+        step("routed: EvalBinGateBatchHIP");
         const BatchResult r = EvalBinGateBatchHIP(cc, static_cast<BINGATE>(gate), c1, c2, out, 0);
         *ok = r.success && r.processed == count;
         if (!r.success)
             throw std::runtime_error("EvalBinGateBatchHIP: " + r.error);
         lwe_out(out, ga, gb);
+        step("routed: reference EvalBinGateBatch");
         const BatchResult rr = EvalBinGateBatch(cc, static_cast<BINGATE>(gate), c1, c2, ref, 0);
+        step("routed: done");
         if (!rr.success)
             throw std::runtime_error("reference EvalBinGateBatch: " + rr.error);
         lwe_out(ref, ra, rb);

@@ -93,6 +93,8 @@ class Backend:
         self.ref = Ref(paramset, method, so=BACKEND_SO)
         self.L = self.ref.L
         self.L.bh_last_error.restype = ctypes.c_char_p
+        if os.environ.get("FHE_SEGV_TRACE") == "1":   # native stack of a fault (oracle/bh_driver.cpp)
+            self.L.bh_install_fault_trace()
         self.ps, self.m = paramset, method
         if keys is None:     # the reference's own key generation
             self.sk, bsk, A, B = self.ref.keygen()
