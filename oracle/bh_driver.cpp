@@ -60,8 +60,8 @@ void on_fault(int sig, siginfo_t* si, void*) {
         char buf[4096];
         for (ssize_t r; fd >= 0 && (r = read(fd, buf, sizeof buf)) > 0;)
             (void)!write(2, buf, r);
-        signal(sig, SIG_DFL);
-        raise(sig);
+        signal(sig, SIG_DFL);  // returning re-executes the faulting access under the default action
+        return;
     }
     for (;;)
         pause();

@@ -376,6 +376,11 @@ class CApi:
         L.lux_fhe_context_ring_dim.restype = ctypes.c_uint32
         L.lux_fhe_context_modulus.restype = ctypes.c_uint64
         L.lux_fhe_strerror.restype = ctypes.c_char_p
+        # pointer arguments as pointers (a bare Python int would be passed as a 32-bit int)
+        L.lux_fhe_decrypt.argtypes = [vp, vp, vp, vp]
+        L.lux_fhe_ciphertext_free.argtypes = [vp]
+        L.capi_ct_equal.argtypes = [vp, vp]
+        L.capi_ref_eval.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp]
         self.L = L
 
     def ok(self, rc):
@@ -506,7 +511,7 @@ def test_gpu_c_api_gates_mux_bootstrap_vs_reference(params):
         outs = arr()
         C.ok(L.lux_fhe_gate_batch(ctx, bsk, code, arr(*cts[0]), arr(*cts[1]), sz(8), outs))
         for i in range(8):
-            assert dec(outs[i]) == f(bits[i, 0], bits[i, 1]), (gname, i)
+            assert dec(vp(outs[i])) == f(bits[i, 0], bits[i, 1]), (gname, i)
             same_as_ref(vp(outs[i]), code, cts[0][i], cts[1][i])
             L.lux_fhe_ciphertext_free(vp(outs[i]))
     assert L.capi_on_gpu(ctx) == 1
@@ -514,7 +519,7 @@ def test_gpu_c_api_gates_mux_bootstrap_vs_reference(params):
     outs = arr()
     C.ok(L.lux_fhe_mux_batch(ctx, bsk, arr(*cts[0]), arr(*cts[1]), arr(*cts[2]), sz(8), outs))
     for i in range(8):   # EvalBinGate(CMUX, {sel, a, b}) = b ? a : sel
-        assert dec(outs[i]) == (bits[i, 1] if bits[i, 2] else bits[i, 0]), i
+        assert dec(vp(outs[i])) == (bits[i, 1] if bits[i, 2] else bits[i, 0]), i
         same_as_ref(vp(outs[i]), 6, cts[0][i], cts[1][i], cts[2][i])
         L.lux_fhe_ciphertext_free(vp(outs[i]))
     one = vp()
@@ -522,7 +527,7 @@ def test_gpu_c_api_gates_mux_bootstrap_vs_reference(params):
     same_as_ref(one, 6, cts[0][5], cts[1][5], cts[2][5])
     C.ok(L.lux_fhe_bootstrap_batch(ctx, bsk, arr(*cts[0]), sz(8), outs))
     for i in range(8):
-        assert dec(outs[i]) == bits[i, 0], i
+        assert dec(vp(outs[i])) == bits[i, 0], i
         same_as_ref(vp(outs[i]), 7, cts[0][i])
         L.lux_fhe_ciphertext_free(vp(outs[i]))
     C.ok(L.lux_fhe_bootstrap(ctx, bsk, cts[1][6], ctypes.byref(one)))

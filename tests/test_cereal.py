@@ -262,7 +262,7 @@ def test_gpu_context_from_reference_archive_evaluates_gate_goldens(name):
     assert (e.params.n, e.params.Q) == (bf.params(int(g["paramset"]), int(g["method"])).n,
                                         bf.params(int(g["paramset"]), int(g["method"])).Q)
     e.load_keys(keys.bsk, keys.kskA, keys.kskB)
-    pg = len(g["bits1"]) // len(g["gates"])
+    pg = g["bits1"].shape[1]
     for i, gate in enumerate(g["gates"]):
         sl = slice(i * pg, (i + 1) * pg)
         ao, bo = e.eval_gate(int(gate), a1[sl], b1[sl], a2[sl], b2[sl])
