@@ -53,8 +53,11 @@ __host__ __device__ constexpr size_t ginx_u4_off(uint32_t ks, uint32_t d, uint32
 }
 
 // u16 key-switching-key rows: A[n] then B at column n, zero-padded to 512 columns (n < 512, both
-// STD128 sets) or 1024 (n < 1024: STD128_3, LPF_STD128, ...)
-__host__ __device__ constexpr uint32_t ksk_width(uint32_t n) { return n < 512 ? 512u : 1024u; }
+// STD128 sets), 1024 (n < 1024: STD128_3, LPF_STD128, ...) or the next multiple of 128 (STD256Q:
+// n = 1225 -> 1280)
+__host__ __device__ constexpr uint32_t ksk_width(uint32_t n) {
+    return n < 512 ? 512u : n < 1024 ? 1024u : (n + 1 + 127) / 128 * 128;  // n >= 1024: the N = 2048 rows
+}
 
 struct GateArgs {
     uint32_t count, n, N, q, qKS;
@@ -134,6 +137,13 @@ __host__ __device__ constexpr uint32_t g2_key_word(uint32_t nd, uint32_t c, uint
 hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const void* keys, const uint16_t* idx,
                                    const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
 bool n2k_supported(const GateArgs& g, const BootTables& t);
+// K1w for LMKCDEY (k_blind_rotate_lmk2k): N = 2048, Q < 2^27, digitsG = 4 (STD256Q_LMKCDEY,
+// STD256Q_3_LMKCDEY); op lists of launch_prep_lmk, keys in Engine::pack_n2k's LMKCDEY layout (ek per
+// index, then ak per automorphism key), tables as launch_blind_rotate_n2k
+hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
+                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                     uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
+bool lmk2k_supported(const GateArgs& g, const BootTables& t);
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);

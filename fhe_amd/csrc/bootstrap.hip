@@ -2445,6 +2445,240 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
     return hipGetLastError();
 }
 
+// ===========================================================================
+// K1w for LMKCDEY: k_blind_rotate_lmk2k<ACCIO> (RingGSWAccumulatorLMKCDEY::EvalAcc,
+// rgsw-acc-lmkcdey.cpp:70-287) at N = 2048, Q < 2^27, digitsG = 4 (ND = 3 retained digits):
+// STD256Q_LMKCDEY and STD256Q_3_LMKCDEY, which otherwise run K5's op-list form.  One gate per
+// 128-thread workgroup (op lists differ per gate, so a barrier may only join the two waves of one
+// gate); wave c owns component c in K1w's layout C.  Per op of k_prep_lmk_w's list:
+//   EXT(i)  (AddToAccLMKCDEY, :228-254): each wave inverse-transforms its component, decomposes it into
+//           its 3 digits (rows 2 j + c) and forward-transforms them, then multiplies them by both key
+//           columns: the sum for its own component replaces acc_c, the other one is reduced to a word
+//           per slot and handed over through this wave's tile (as K1w's GINX exchange).
+//   AUTO(t) (Automorphism, :257-287): both components permuted in EVAL through the wave's tile; wave 0
+//           inverse-transforms acc0', decomposes and forward-transforms it, acc0 <- sum_d D_d ak[t][d][0]
+//           and hands sum_d D_d ak[t][d][1] to wave 1, which adds it to acc1'.
+// Keys (Engine::pack_n2k, u32 Montgomery with N^-1 folded in), one uint4 = 4 consecutive registers:
+//   ek: [i][c][q < 6][k4 < 8][64 lanes], q = 2 j + o: digit row 2 j + c, column c (o = 0) or 1 - c (o = 1);
+//   ak: [t][q < 6][k4 < 8][64 lanes], q = 2 d + col.
+// Bounds (Q < 2^27): |D| < 11 Q + 2^(g-1) after the forward transform, |S| < 3 (11 Q + 2^6) Q < 2^59,
+// each reduced sum < 1.6 Q, acc < 3.2 Q after an exchange (the inverse plan's BIN = 33).
+// ===========================================================================
+namespace {
+constexpr int kL2AccBound = 33;  // |acc| < 3.3 Q between ops (units of Q/10)
+constexpr size_t l2k_lds() { return (size_t)(2048 + 2048 + 2 * kW2Tile) * 4; }
+
+// EVAL automorphism X -> X^k on layout C through this wave's tile (as automorphism_c at N = 1024):
+// slot x(L, r) evaluates at psi^(2 brv11(x) + 1), 2 brv11(x) + 1 = 32 brv6(L) + 1 + 2048 (r & 1) +
+// 2 brv4(r >> 1); the value at x moves from the slot y with 2 brv11(y) + 1 = k (2 brv11(x) + 1) mod 4N
+FHE_DEV void automorphism_2k(uint32_t (&v)[32], uint32_t* t, int L, uint32_t k) {
+    uint32_t* tc = t + wc2k(L);
+#pragma unroll
+    for (int rh = 0; rh < 16; ++rh) *reinterpret_cast<uint2*>(tc + 132 * rh) = make_uint2(v[2 * rh], v[2 * rh + 1]);
+    wave_lds_sync();
+    const uint32_t cl = (32u * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1u) * k;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const uint32_t sr = (2048u * (uint32_t)(r & 1) + 2u * (__builtin_bitreverse32((uint32_t)(r >> 1)) >> 28)) * k;
+        const uint32_t e  = (cl + sr) & 4095u;                  // odd
+        const uint32_t sx = __builtin_bitreverse32(e >> 1) >> 21;  // source slot brv11((e - 1) / 2)
+        v[r] = t[sx + 2 * (sx >> 6)];
+    }
+    wave_lds_sync();
+}
+
+// acc_c <- (own sum), partner word <- (other sum) over ND digits and the 2 ND key vectors of kb
+// (q = 2 j + o); keys one chunk of 4 registers ahead
+template <int ND>
+FHE_DEV void mac_2k(uint32_t (&acc)[32], const uint32_t (&d)[ND][32], const uint4* kb, uint32_t* tile, int L,
+                    const Mod& m) {
+    constexpr int kQ = 2 * ND;
+    uint4 kq[2][kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) kq[0][q] = kb[(q * 8 + 0) * 64];
+#pragma unroll
+    for (int k4 = 0; k4 < 8; ++k4) {
+        if (k4 + 1 < 8) {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) kq[(k4 + 1) & 1][q] = kb[(q * 8 + k4 + 1) * 64];
+        }
+        asm volatile("" ::: "memory");
+        const uint4* q4 = kq[k4 & 1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * k4 + e;
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                int64_t S = 0;
+#pragma unroll
+                for (int j = 0; j < ND; ++j) {
+                    const uint4 kv   = q4[2 * j + o];
+                    const uint32_t w = e == 0 ? kv.x : e == 1 ? kv.y : e == 2 ? kv.z : kv.w;
+                    S += (int64_t)(int32_t)d[j][r] * (int32_t)w;
+                }
+                if (o == 0) acc[r] = smont_red(S, m);
+                else tile[(r << 6) | L] = smont_red(S, m);
+            }
+        }
+    }
+}
+}  // namespace
+
+template <bool ACCIO>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
+    k_blind_rotate_lmk2k(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
+                         const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
+                         const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
+                         const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
+    constexpr int ND = 3, kQ = 2 * ND;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_tab  = sm;
+    uint32_t* s_tabI = sm + 2048;
+    uint32_t* s_tile = sm + 4096;
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) {
+        s_tab[i]  = T.tabF[i];
+        s_tabI[i] = T.tabI[i];
+    }
+    const int c = threadIdx.x >> 6, L = threadIdx.x & 63;  // wave c: RLWE component c
+    const uint32_t gate = blockIdx.x;
+    uint32_t* tile    = s_tile + c * kW2Tile;
+    uint32_t* partner = s_tile + (c ^ 1) * kW2Tile;
+    const Mod m0 = make_mod(T);
+    const Mod& m = m0;
+    const uint32_t M = 2 * g.N;
+    __syncthreads();
+
+    // BootstrapGateCore (binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0; then
+    // acc1 <- acc1(X^(2N-5)) (rgsw-acc-lmkcdey.cpp:99; acc0 = 0 is invariant)
+    uint32_t acc[32];
+    if (ACCIO && !g.acc_tv) {
+        const uint64_t* src = g.acc_io + ((size_t)gate * 2 + c) * g.N;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = csub(mont_mul((uint32_t)src[slot_2k(L, r)], T.ninvR, m), m.Q);
+        if (c == 1) automorphism_2k(acc, tile, L, M - 5);
+    } else if (c == 1) {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        uint32_t tv[1][32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            uint32_t v       = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v                 = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            tv[0][r] = v;
+        }
+        fwd_2k_s<1>(tv, tile, L, twAf, s_tab, m);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
+        automorphism_2k(acc, tile, L, M - 5);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) acc[r] = 0;
+    }
+
+    const DecN dec       = make_decn(m.Q, g.gbits, ND);
+    const uint16_t* gops = ops + (size_t)gate * maxops;
+    const uint32_t cnt   = __builtin_amdgcn_readfirstlane(nops[gate]);
+    for (uint32_t it = 0; it < cnt; ++it) {
+        const Mod m       = fresh_nq(m0);
+        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+        const uint32_t* twF = twAf;
+        const uint32_t* twI = twAi;
+        asm volatile("" : "+s"(twF), "+s"(twI));
+        __syncthreads();  // the partner has read this wave's tile (previous op)
+        uint32_t d[ND][32];
+        if (!(op & 0x8000u)) {
+            // ---- AddToAccLMKCDEY: acc_c <- sum over both components' digits of D ek[op][row][c]
+#pragma unroll
+            for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
+            inv_2k_s<kL2AccBound>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+            fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
+            mac_2k<ND>(acc, d, ek + ((size_t)op * 2 + c) * (kQ * 8 * 64) + L, tile, L, m);
+            __syncthreads();  // both waves' partner words are in LDS
+#pragma unroll
+            for (int r = 0; r < 32; ++r) acc[r] += partner[(r << 6) | L];
+        } else {
+            // ---- Automorphism(5^t or 2N - 5, ak[t])
+            const uint32_t t = op & 0x7fffu;
+            uint32_t kexp = M - 5;
+            if (t) {
+                kexp = 1;
+                for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5u) & (M - 1);
+            }
+            automorphism_2k(acc, tile, L, kexp);
+            if (c == 0) {  // acc0' -> COEF -> 3 digits -> EVAL; acc0 replaced, acc1's share to the tile
+#pragma unroll
+                for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
+                inv_2k_s<kL2AccBound>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+                for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+                fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
+                mac_2k<ND>(acc, d, ak + (size_t)t * (kQ * 8 * 64) + L, tile, L, m);
+            }
+            __syncthreads();  // wave 0's share of acc1 is in its tile
+            if (c == 1) {
+#pragma unroll
+                for (int r = 0; r < 32; ++r) {
+                    const int64_t S = (int64_t)(int32_t)acc[r] * (int32_t)m.oneR +
+                                      (int64_t)(int32_t)partner[(r << 6) | L] * (int32_t)m.oneR;
+                    acc[r] = smont_red(S, m);
+                }
+            }
+        }
+    }
+
+    if (ACCIO) {
+        uint64_t* dst = g.acc_io + ((size_t)gate * 2 + c) * g.N;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const int32_t v = (int32_t)smont_mul(acc[r], T.nR, m);
+            dst[slot_2k(L, r)] = (uint64_t)(uint32_t)(v < 0 ? v + (int32_t)m.Q : v);
+        }
+        return;
+    }
+    // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_n2k
+    __syncthreads();  // the partner has read this wave's tile
+    inv_2k_s<kL2AccBound>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
+    if (c == 0) {
+        uint64_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            const uint32_t v = acc[r];
+            const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
+            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+        }
+    } else if (L == 0) {
+        const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
+        ext_b[gate]       = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+bool lmk2k_supported(const GateArgs& g, const BootTables& t) {
+    return t.Q < (1u << 27) && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 &&
+           4 * g.gbits <= 32;
+}
+
+hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
+                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                     uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!lmk2k_supported(g, t)) return hipErrorInvalidValue;
+    const uint4* e = static_cast<const uint4*>(ek);
+    const uint4* a = static_cast<const uint4*>(ak);
+    if (g.acc_io)
+        hipLaunchKernelGGL(k_blind_rotate_lmk2k<true>, dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, nops,
+                           maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_lmk2k<false>, dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, nops,
+                           maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // ExternalProduct seam (Backend::ExternalProduct[Batch], backend.h:141-146, 187-192): per-item
 // RGSW keys in the reference's raw EVAL layout [dG2 = 4][2][N] packed into the op-list kernel's

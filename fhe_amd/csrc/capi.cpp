@@ -47,27 +47,36 @@ int guarded(F&& f) {
         return fail(FHE_HIP_ERR_INVALID_PARAM, "unknown exception");
     }
 }
-// device scratch for a synchronous host-buffer call (freed on every exit path)
-// (hipFreeAsync on the call's stream: an error path frees it after the work already enqueued there,
-// without waiting for other contexts' work on the device)
-struct DeviceScratch {
-    uint64_t* p = nullptr;
-    hipStream_t s = nullptr;
-    DeviceScratch(int device, size_t bytes, hipStream_t stream) : s(stream) {
-        FHE_HIP_CHECK(hipSetDevice(device));
-        FHE_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&p), bytes, s));
-    }
-    ~DeviceScratch() {
-        if (p) (void)hipFreeAsync(p, s);
-    }
-    DeviceScratch(const DeviceScratch&) = delete;
-    DeviceScratch& operator=(const DeviceScratch&) = delete;
-};
 }  // namespace
 
+// A context's device scratch for its synchronous host-buffer calls (seam BlindRotate / ExternalProduct):
+// grow-only, owned by the context, reused by every such call (each ends with a stream synchronize).
+// Round 4 replaced a stream-ordered pool allocation (hipMallocAsync / hipFreeAsync per call): after a few
+// such calls on one context, a block handed out again read back as zeros right after the kernel that
+// wrote it had finished (tests/test_backend.py, std192_lmkcdey null accumulators).
 struct fhe_hip_ctx {
     Engine eng;
+    uint64_t* scr = nullptr;
+    size_t scr_bytes = 0;
     fhe_hip_ctx(int ps, int m, int dev) : eng(ps, m, dev) {}
+    ~fhe_hip_ctx() {
+        if (scr) {
+            (void)hipSetDevice(eng.device());
+            (void)hipFree(scr);
+        }
+    }
+    uint64_t* scratch(size_t bytes, hipStream_t s) {
+        FHE_HIP_CHECK(hipSetDevice(eng.device()));
+        if (bytes > scr_bytes) {
+            FHE_HIP_CHECK(hipStreamSynchronize(s));
+            if (scr) FHE_HIP_CHECK(hipFree(scr));
+            scr = nullptr;
+            scr_bytes = 0;
+            FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&scr), bytes));
+            scr_bytes = bytes;
+        }
+        return scr;
+    }
 };
 
 static void fill_params(const Params& p, fhe_hip_params* o) {
@@ -608,11 +617,11 @@ int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_
         for (size_t i = 0; i < accw; ++i)
             if (acc[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "accumulator not reduced mod Q");
         hipStream_t s = ctx_stream(ctx, nullptr);
-        DeviceScratch d(ctx->eng.device(), (aw + accw) * 8, s);
-        FHE_HIP_CHECK(hipMemcpyAsync(d.p, a, aw * 8, hipMemcpyHostToDevice, s));
-        FHE_HIP_CHECK(hipMemcpyAsync(d.p + aw, acc, accw * 8, hipMemcpyHostToDevice, s));
-        ctx->eng.blind_rotate_acc_device(count, d.p, (uint32_t)ctmod, d.p + aw, s);
-        FHE_HIP_CHECK(hipMemcpyAsync(acc, d.p + aw, accw * 8, hipMemcpyDeviceToHost, s));
+        uint64_t* d = ctx->scratch((aw + accw) * 8, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(d, a, aw * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(d + aw, acc, accw * 8, hipMemcpyHostToDevice, s));
+        ctx->eng.blind_rotate_acc_device(count, d, (uint32_t)ctmod, d + aw, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(acc, d + aw, accw * 8, hipMemcpyDeviceToHost, s));
         FHE_HIP_CHECK(hipStreamSynchronize(s));
         return FHE_HIP_OK;
     });
@@ -642,11 +651,11 @@ int fhe_hip_blind_rotate_init_batch(fhe_hip_ctx* ctx, size_t count, const uint64
         for (size_t i = 0; i < count; ++i)
             if (b[i] >= p.q) return fail(FHE_HIP_ERR_INVALID_PARAM, "b not reduced mod q");
         hipStream_t s = ctx_stream(ctx, nullptr);
-        DeviceScratch d(ctx->eng.device(), (aw + count + accw) * 8, s);
-        FHE_HIP_CHECK(hipMemcpyAsync(d.p, a, aw * 8, hipMemcpyHostToDevice, s));
-        FHE_HIP_CHECK(hipMemcpyAsync(d.p + aw, b, count * 8, hipMemcpyHostToDevice, s));
-        ctx->eng.blind_rotate_init_device(count, d.p, d.p + aw, d.p + aw + count, s);
-        FHE_HIP_CHECK(hipMemcpyAsync(acc, d.p + aw + count, accw * 8, hipMemcpyDeviceToHost, s));
+        uint64_t* d = ctx->scratch((aw + count + accw) * 8, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(d, a, aw * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(d + aw, b, count * 8, hipMemcpyHostToDevice, s));
+        ctx->eng.blind_rotate_init_device(count, d, d + aw, d + aw + count, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(acc, d + aw + count, accw * 8, hipMemcpyDeviceToHost, s));
         FHE_HIP_CHECK(hipStreamSynchronize(s));
         return FHE_HIP_OK;
     });
@@ -674,11 +683,11 @@ int fhe_hip_external_product_batch(fhe_hip_ctx* ctx, size_t count, const uint64_
         for (size_t i = 0; i < rw; ++i)
             if (rlwe[i] >= p.Q) return fail(FHE_HIP_ERR_INVALID_PARAM, "RLWE ciphertext not reduced mod Q");
         hipStream_t s = ctx_stream(ctx, nullptr);
-        DeviceScratch d(ctx->eng.device(), (kw + rw) * 8, s);
-        FHE_HIP_CHECK(hipMemcpyAsync(d.p, rgsw, kw * 8, hipMemcpyHostToDevice, s));
-        FHE_HIP_CHECK(hipMemcpyAsync(d.p + kw, rlwe, rw * 8, hipMemcpyHostToDevice, s));
-        ctx->eng.external_product_device(count, d.p, d.p + kw, d.p + kw, s);
-        FHE_HIP_CHECK(hipMemcpyAsync(result, d.p + kw, rw * 8, hipMemcpyDeviceToHost, s));
+        uint64_t* d = ctx->scratch((kw + rw) * 8, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(d, rgsw, kw * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(d + kw, rlwe, rw * 8, hipMemcpyHostToDevice, s));
+        ctx->eng.external_product_device(count, d, d + kw, d + kw, s);
+        FHE_HIP_CHECK(hipMemcpyAsync(result, d + kw, rw * 8, hipMemcpyDeviceToHost, s));
         FHE_HIP_CHECK(hipStreamSynchronize(s));
         return FHE_HIP_OK;
     });

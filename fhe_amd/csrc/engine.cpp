@@ -2,6 +2,7 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -43,8 +44,17 @@ bool Engine::g3_set(const Params& p) {
 bool Engine::n2k_set(const Params& p) {
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
     const uint64_t C = h * (1 + (1ull << g) + (1ull << (2 * g)) + (1ull << (3 * g)));
-    return !is_large(p.paramset) && !p.timeopt && p.method == M_GINX && p.N == 2048 && p.Q < (1ull << 27) &&
-           p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.q < 2 * p.N;
+    // GINX with even monomial exponents (q < 2N: the half-resolution table), LMKCDEY at any q
+    const bool ginx = p.method == M_GINX && p.q < 2 * p.N;
+    return !is_large(p.paramset) && !p.timeopt && (ginx || p.method == M_LMKCDEY) && p.N == 2048 &&
+           p.Q < (1ull << 27) && p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32);
+}
+
+bool Engine::ks32_set(const Params& p) {
+    const bool pow2ks = !(p.qKS & (p.qKS - 1)), pow2b = !(p.baseKS & (p.baseKS - 1));
+    const bool shape = ((p.baseKS == 32 || p.baseKS == 64) && p.digitsKS == 3) || (p.baseKS == 16 && p.digitsKS == 4);
+    return !is_large(p.paramset) && !p.timeopt && pow2ks && pow2b && shape && p.qKS <= 65536 && p.n < 2048 &&
+           p.N <= 2048;
 }
 
 // K1w tables (bootstrap.hip k_blind_rotate_n2k): Table / TableI (2048 words each, u32 Montgomery; the
@@ -94,9 +104,47 @@ void Engine::build_tables_n2k() {
 // K1w key layout, u32 Montgomery with N^-1 folded in, per index i and wave c:
 // [c][q < 6][k2 < 16][64][4] = (K+[r], K+[r+1], K-[r], K-[r+1]), r = 2 k2 + e, slot x(L, r) of layout C,
 // q = 2 j + o: digit row 2 j + c, column c (o = 0) or 1 - c (o = 1); raw BSK [n][2][dG2 = 6][2][N]
+// LMKCDEY (k_blind_rotate_lmk2k): ek [i][c][q < 6][k4 < 8][64][4], register r = 4 k4 + e4 of lane L is
+// slot x(L, r), q = 2 j + o: row 2 j + c, column c (o = 0) or 1 - c (o = 1), from [n][dG2 = 6][2][N];
+// then ak [t][q < 6][k4][64][4], q = 2 d + column, from [numAutoKeys + 1][3][2][N]
 void Engine::pack_n2k(const uint64_t* bsk) {
     const uint32_t n = p_.n, N = p_.N, dG2 = p_.digitsG2;
     const uint64_t Q = p_.Q, ninv = invmod(N, Q);
+    auto word = [&](uint64_t v) { return to_mont(mulmod(v % Q, ninv, Q), Q); };
+    auto slot = [](uint32_t L, uint32_t r) { return ((r >> 1) << 7) | (L << 1) | (r & 1); };
+    if (p_.method == M_LMKCDEY) {
+        const size_t per = (size_t)2 * 6 * 8 * 64 * 4, aper = (size_t)6 * 8 * 64 * 4;
+        const size_t nauto = (size_t)p_.numAutoKeys + 1;
+        std::vector<uint32_t> dev((size_t)n * per + nauto * aper);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < (int64_t)n; ++i)
+            for (uint32_t c = 0; c < 2; ++c)
+                for (uint32_t q = 0; q < 6; ++q)
+                    for (uint32_t k4 = 0; k4 < 8; ++k4)
+                        for (uint32_t L = 0; L < 64; ++L)
+                            for (uint32_t e = 0; e < 4; ++e) {
+                                const uint32_t row = 2 * (q >> 1) + c, col = (q & 1) ? 1 - c : c;
+                                const size_t src = (((size_t)i * dG2 + row) * 2 + col) * N + slot(L, 4 * k4 + e);
+                                dev[(size_t)i * per + ((((c * 6 + q) * 8 + k4) * 64 + L) * 4 + e)] = word(bsk[src]);
+                            }
+        const uint64_t* asrc = bsk + (size_t)n * dG2 * 2 * N;
+        uint32_t* adst = dev.data() + (size_t)n * per;
+        for (size_t t = 0; t < nauto; ++t)
+            for (uint32_t q = 0; q < 6; ++q)
+                for (uint32_t k4 = 0; k4 < 8; ++k4)
+                    for (uint32_t L = 0; L < 64; ++L)
+                        for (uint32_t e = 0; e < 4; ++e) {
+                            const uint32_t d = q >> 1, col = q & 1;
+                            adst[t * aper + (((q * 8 + k4) * 64 + L) * 4 + e)] =
+                                word(asrc[((t * 3 + d) * 2 + col) * N + slot(L, 4 * k4 + e)]);
+                        }
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        if (d_bsk2_) FHE_HIP_CHECK(hipFree(d_bsk2_));
+        d_bsk2_ = nullptr;
+        FHE_HIP_CHECK(hipMalloc(&d_bsk2_, dev.size() * 4));
+        FHE_HIP_CHECK(hipMemcpy(d_bsk2_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+        return;
+    }
     const size_t per = (size_t)2 * 6 * 16 * 64 * 4;
     std::vector<uint32_t> dev((size_t)n * per);
 #pragma omp parallel for schedule(static)
@@ -203,6 +251,12 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
             const char* e = std::getenv("FHE_HIP_N2K");
             n2k_ = !(e && std::string(e) == "0");
             if (n2k_) build_tables_n2k();
+        }
+        if (g3_) {
+            ks32_ = true;
+        } else if (ks32_set(p_)) {
+            const char* e = std::getenv("FHE_HIP_KS32");
+            ks32_ = !(e && std::string(e) == "0");
         }
         if (method == M_LMKCDEY) {  // op lists (k_prep_lmk_w) for k_blind_rotate_wide_ops
             if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");
@@ -556,8 +610,8 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
             FHE_HIP_CHECK(hipMemcpy(d_wksk_ + k * one, A + k * rows * p_.n, rows * p_.n * 8, hipMemcpyHostToDevice));
             FHE_HIP_CHECK(hipMemcpy(d_wksk_ + k * one + rows * p_.n, B + k * rows, rows * 8, hipMemcpyHostToDevice));
         }
-        if (!g3_) return;
-        // g3_: also the u16 rows of the 32-bit key switch (qKS <= 2^16, n < 1024; g3_set)
+        if (!ks32_) return;
+        // ks32_: also the u16 rows of the 32-bit key switch (qKS <= 2^16; ks32_set)
     }
     const size_t W = ksk_width(p_.n);
     std::vector<uint16_t> dev(rows * W, 0);
@@ -688,7 +742,7 @@ void Engine::ensure_work(size_t count) {
         FHE_HIP_CHECK(hipMalloc(&d_wext_a_, count * p_.N * sizeof(uint64_t)));
         FHE_HIP_CHECK(hipMalloc(&d_wext_b_, count * sizeof(uint64_t)));
     }
-    if (!wide_ || g3_) {  // g3_: the 32-bit key switch's input (keyswitch_ext)
+    if (!wide_ || ks32_) {  // ks32_: the 32-bit key switch's input (keyswitch_ext)
         FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
         FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
     }
@@ -753,6 +807,13 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
             const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);
             FHE_HIP_CHECK(launch_blind_rotate_lmk3(g, tabs_, ek, ek + (size_t)p_.n * 12288, d_ops_, d_nops_, maxops_,
                                                    d_tvb_, d_wext_a_, d_wext_b_, s));
+            return;
+        }
+        if (n2k_ && p_.method == M_LMKCDEY && d_bsk2_ && lmk2k_supported(g, tabs2k_) && g.lv == g.lv64 &&
+            g.uv == g.uv64 && g.b_const == g.b64) {
+            const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);
+            FHE_HIP_CHECK(launch_blind_rotate_lmk2k(g, tabs2k_, ek, ek + (size_t)p_.n * 24576, d_ops_, d_nops_, maxops_,
+                                                    d_tvb_, d_wext_a_, d_wext_b_, s));
             return;
         }
         if (p_.method == M_LMKCDEY || p_.method == M_AP) {
@@ -848,6 +909,17 @@ void Engine::blind_rotate_init_device(size_t count, const uint64_t* a, const uin
     prep_device(g, in, 0, s);
     rotate_device(g, s);
     rot_count_ = 0;
+    if (std::getenv("FHE_HIP_DEBUG")) {  // diagnostics: the op count and accumulator words of gate 0
+        uint32_t nops0 = 0;
+        uint64_t w[4] = {};
+        FHE_HIP_CHECK(hipStreamSynchronize(s));
+        if (d_nops_) FHE_HIP_CHECK(hipMemcpy(&nops0, d_nops_, 4, hipMemcpyDeviceToHost));
+        FHE_HIP_CHECK(hipMemcpy(w, acc, sizeof w, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[fhe_hip] blind_rotate_init count=%zu cap=%zu maxops=%u nops0=%u wide=%d narrow=%d "
+                     "acc=%llu %llu %llu %llu err=%d\n", count, cap_, maxops_, nops0, (int)wide_, (int)narrow_,
+                     (unsigned long long)w[0], (unsigned long long)w[1], (unsigned long long)w[2],
+                     (unsigned long long)w[3], (int)hipGetLastError());
+    }
 }
 
 void Engine::external_product_device(size_t count, const uint64_t* rgsw, const uint64_t* rlwe, uint64_t* result,
@@ -999,9 +1071,9 @@ void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t*
 }
 
 void Engine::keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
-    if (wide_ && g3_ && d_ksk_ && d_ext_a_ && count <= cap_) {
-        // digitsG = 4 sets: the u64 ctExt mod qKS narrowed to u32, then the 32-bit (u16-row, gate-tiled
-        // for baseKS = 32) key switch instead of u64 row gathers
+    if (wide_ && ks32_ && d_ksk_ && d_ext_a_ && count <= cap_) {
+        // the u64 ctExt mod qKS narrowed to u32, then the 32-bit (u16-row, gate-tiled) key switch instead
+        // of u64 row gathers
         FHE_HIP_CHECK(launch_narrow_u32(d_wext_a_, d_wext_b_, d_ext_a_, d_ext_b_, p_.N, count, s));
         GateArgs g = gate_args(G_AND, count);
         FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, q_out, a_out, b_out, s,

@@ -59,6 +59,9 @@ public:
     // the digitsG = 4 sets at N = 1024, Q < 2^27 the split kernels take (K1s / K1m)
     static bool g3_set(const Params& p);
     static bool n2k_set(const Params& p);     // GINX gates on K1w (N = 2048 in registers)
+    // 64-bit-path sets whose key switch runs on the 32-bit tiled kernel (u16 rows): qKS <= 2^16 a power
+    // of two and a tiled shape (baseKS 32 / 64 with digitsKS 3, baseKS 16 with digitsKS 4), n < 2048
+    static bool ks32_set(const Params& p);
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -202,6 +205,9 @@ private:
     // over its own 32-bit tables, keys packed into d_bsk2_; the rest of the 64-bit path (prep, key
     // switch, functional bootstrapping) unchanged.  FHE_HIP_N2K=0 keeps them on K5 (A/B, tests).
     bool n2k_ = false;
+    // the 32-bit key switch on the 64-bit path (ks32_set; g3_ sets always, FHE_HIP_KS32=0 keeps the
+    // u64 row gathers of launch_keyswitch_wide for the others: A/B, tests)
+    bool ks32_ = false;
     BootTables tabs2k_{};
     void* d_tables2k_ = nullptr;
     void build_tables_n2k();

@@ -11,6 +11,7 @@
 #include "arith.h"
 #include "boot.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace fhe_amd {
@@ -38,7 +39,7 @@ __global__ void __launch_bounds__(512)
     k_keyswitch(GateArgs g, uint32_t logBase, uint32_t digitsKS, const uint32_t* __restrict__ ksk,
                 const uint32_t* __restrict__ ms_a, const uint32_t* __restrict__ ms_b, uint64_t q_out,
                 uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
-    __shared__ uint32_t s_a[1024];
+    __shared__ uint32_t s_a[2048];
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
     for (uint32_t i = t; i < g.N; i += blockDim.x) s_a[i] = ms_a[(size_t)gate * g.N + i];
     __syncthreads();
@@ -103,7 +104,6 @@ constexpr int kKsCols  = FHE_KS_COLS;           // columns per workgroup (packed
 // choices never conflict (16-byte reads with a 144-B stride collide for slices d, d + 16).
 constexpr int kKsRowB  = kKsCols * 2 + (FHE_KS_B64 ? 8 : 16);
 constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
-constexpr int kKsDigits = 3;                    // digitsKS
 // Tile shapes (G gates per workgroup, IPR values of i per round at baseKS = 32), by batch size
 // (round 3, profiles/r03_ab_keyswitch.txt, per launch at 65,536 / 8192 / 1024 gates):
 //   G 256, IPR 4 (104 KB of LDS, one workgroup per CU):       6.64 ms / 0.82 ms / 125 + 11 us
@@ -122,12 +122,13 @@ constexpr int kKsSplitG = 512;
 #define FHE_KS_XCD 0
 #endif            // the row split's gate tile
 // LOGB = log2(baseKS): 5 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 6 (STD128_3/4,
-// LPF_STD128Q: 64 slices, 2 values of i per round so that the double buffer keeps the same 104 KB;
-// slices d and d + 32 share a bank slot, a 2-way conflict)
-template <int LOGB, int IPR> struct KsShape {
+// LPF_STD128Q, STD256Q_3_LMKCDEY: 64 slices, 2 values of i per round so that the double buffer keeps the
+// same 104 KB; slices d and d + 32 share a bank slot, a 2-way conflict), both with KD = digitsKS = 3; or
+// 4 with KD = 4 (STD256Q: baseKS 16, qKS 2^16; 2 values of i per round, 35 KB)
+template <int LOGB, int IPR, int KD = 3> struct KsShape {
     static constexpr int base  = 1 << LOGB;
     static constexpr int ipr   = LOGB == 5 ? IPR : 2;
-    static constexpr int step  = ipr * kKsDigits;                 // (i, j) steps per round / LDS buffer / barrier
+    static constexpr int step  = ipr * KD;                        // (i, j) steps per round / LDS buffer / barrier
     static constexpr int parts = base * kKsCols * 2 / 16;         // 16-byte parts staged per step
 };
 
@@ -136,12 +137,13 @@ template <int LOGB, int IPR> struct KsShape {
 // (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
 // 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
-template <int G, bool SPLIT, int LOGB, int IPR>
+template <int G, bool SPLIT, int LOGB, int IPR, int KD = 3>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                       uint64_t* __restrict__ b_out, uint32_t* __restrict__ part) {
-    using S_ = KsShape<LOGB, IPR>;
+    using S_ = KsShape<LOGB, IPR, KD>;
+    constexpr int kKsDigits = KD;
     constexpr int kKsParts = S_::parts, kKsStep = S_::step, kIPR = S_::ipr, kBase = S_::base;
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
@@ -278,27 +280,31 @@ __global__ void __launch_bounds__(G)
     }
 }
 
-// the S row-split partials of a gate, one thread per packed column pair, then the epilogue
+// the S row-split partials of a gate, one packed column pair per thread and step (hw = W / 2 pairs, up
+// to 640 at W = 1280, on at most 512 threads), then the epilogue
 __global__ void __launch_bounds__(512)
-    k_keyswitch_reduce(GateArgs g, const uint32_t* __restrict__ part, uint32_t S, const uint32_t* __restrict__ ms_b,
-                       uint64_t q_out, uint64_t* __restrict__ a_out, uint64_t* __restrict__ b_out) {
-    const uint32_t gate = blockIdx.x, t = threadIdx.x, hw = blockDim.x;
-    uint32_t acc = 0;
-    for (uint32_t z = 0; z < S; ++z) {
-        const uint32_t w = part[((size_t)z * g.count + gate) * hw + t];
-        asm("v_pk_add_u16 %0, %1, %2" : "=v"(acc) : "v"(acc), "v"(w));
-    }
+    k_keyswitch_reduce(GateArgs g, const uint32_t* __restrict__ part, uint32_t S, uint32_t hw,
+                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
+                       uint64_t* __restrict__ b_out) {
+    const uint32_t gate = blockIdx.x;
     const uint32_t qm = g.qKS - 1;
     const uint32_t b = ms_b[gate];
     uint64_t* oa = a_out + (size_t)gate * g.n;
+    for (uint32_t t = threadIdx.x; t < hw; t += blockDim.x) {
+        uint32_t acc = 0;
+        for (uint32_t z = 0; z < S; ++z) {
+            const uint32_t w = part[((size_t)z * g.count + gate) * hw + t];
+            asm("v_pk_add_u16 %0, %1, %2" : "=v"(acc) : "v"(acc), "v"(w));
+        }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t c = 2 * t + h;
-        const uint32_t neg = h ? (acc >> 16) : (acc & 0xffffu);  // -sum mod 2^16
-        uint64_t v = ((c == g.n ? b : 0u) + neg) & qm;
-        if (q_out) v = mod_switch_up(v, g.qKS, q_out);
-        if (c < g.n) oa[c] = v;
-        else if (c == g.n) b_out[gate] = v;
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t c = 2 * t + h;
+            const uint32_t neg = h ? (acc >> 16) : (acc & 0xffffu);  // -sum mod 2^16
+            uint64_t v = ((c == g.n ? b : 0u) + neg) & qm;
+            if (q_out) v = mod_switch_up(v, g.qKS, q_out);
+            if (c < g.n) oa[c] = v;
+            else if (c == g.n) b_out[gate] = v;
+        }
     }
 }
 
@@ -321,7 +327,7 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
                             uint64_t* b_out, hipStream_t s, uint32_t* part, size_t part_words) {
     if (g.count == 0) return hipSuccess;
     if (baseKS & (baseKS - 1)) return hipErrorInvalidValue;
-    if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 1024 || g.N > 1024) return hipErrorInvalidValue;
+    if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 2048 || g.N > 2048) return hipErrorInvalidValue;
     const uint32_t W = ksk_width(g.n);
     const uint32_t logBase = (uint32_t)__builtin_ctz(baseKS);
 #ifndef FHE_KS_TILE
@@ -330,17 +336,22 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     int tile = FHE_KS_TILE;
     // tiles need >= 16 x 8 workgroups to pay, or a row split (scratch) below 4096 gates
     if (tile == 0) tile = g.count >= 4096 || part ? 256 : 1;
-    if (tile > 1 && ((logBase != 5 && logBase != 6) || digitsKS != (uint32_t)kKsDigits || g.N % kKsIPR)) tile = 1;
+    const bool shape3 = (logBase == 5 || logBase == 6) && digitsKS == 3, shape4 = logBase == 4 && digitsKS == 4;
+    if (tile > 1 && (!(shape3 || shape4) || g.N % kKsIPR)) tile = 1;
+    // the per-gate kernel: one thread per column pair, at most 512
+    if (tile == 1 && W > 1024) return hipErrorInvalidValue;
     if (tile > 1) {
         // baseKS = 32: the tile shape by batch size (kKsIPR above); baseKS = 64: G 256
         const uint32_t Gs = logBase == 5 ? (uint32_t)kKsSplitG : 256u;
         const uint32_t S = part ? split_factor(g.count, g.n, g.N, part_words, Gs) : 1;
         const uint32_t G = S > 1 ? Gs : logBase == 5 && g.count >= kKsWideBatch ? 512u : 256u;
         const dim3 grid((g.count + G - 1) / G, W / kKsCols, S);
-#define FHE_KS_LAUNCH(G_, SP, LB, IPR_)                                                                           \
-    hipLaunchKernelGGL((k_keyswitch_tiled<G_, SP, LB, IPR_>), grid, dim3(G_), 0, s, g, ksk, ms_a, ms_b, q_out,      \
-                       a_out, b_out, SP ? part : nullptr)
-        if (logBase == 5) {
+#define FHE_KS_LAUNCH(G_, SP, LB, IPR_, ...)                                                                      \
+    hipLaunchKernelGGL((k_keyswitch_tiled<G_, SP, LB, IPR_, ##__VA_ARGS__>), grid, dim3(G_), 0, s, g, ksk, ms_a, ms_b, \
+                       q_out, a_out, b_out, SP ? part : nullptr)
+        if (shape4) {
+            if (S > 1) FHE_KS_LAUNCH(256, true, 4, 2, 4); else FHE_KS_LAUNCH(256, false, 4, 2, 4);
+        } else if (logBase == 5) {
             if (S > 1) FHE_KS_LAUNCH(kKsSplitG, true, 5, 4);
             else if (G == 512) FHE_KS_LAUNCH(512, false, 5, 2);
             else FHE_KS_LAUNCH(256, false, 5, 4);
@@ -351,8 +362,8 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
         if (S > 1) {
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(k_keyswitch_reduce, dim3(g.count), dim3(W / 2), 0, s, g, part, S, ms_b, q_out, a_out,
-                               b_out);
+            hipLaunchKernelGGL(k_keyswitch_reduce, dim3(g.count), dim3(std::min(W / 2, 512u)), 0, s, g, part, S, W / 2,
+                               ms_b, q_out, a_out, b_out);
         }
     } else {
         hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(W / 2), 0, s, g, logBase, digitsKS,

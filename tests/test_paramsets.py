@@ -169,15 +169,17 @@ def test_gpu_digitsg4_multi_input_gates_vs_reference(name):
 
 
 @pytest.mark.gpu
-def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch):
-    """STD256Q (N = 2048, Q < 2^27, digitsG = 4, q = 1024): K1w, the register-resident two-waves-per-gate
-    accumulator (launch_blind_rotate_n2k, the default), against the one-gate-per-workgroup accumulator the
-    set ran on before (FHE_HIP_N2K=0, bootstrap_wide.hip A32) on 333 gates of every 2-input type (final
-    and extended outputs) and on the seam's BlindRotate (random accumulators, q and ragged counts); the
-    gates also decrypt to the truth table.  The reference goldens of the set run in
+@pytest.mark.parametrize("name", ["std256q", "std256q_3_lmkcdey"])
+def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
+    """N = 2048, Q < 2^27, digitsG = 4: K1w, the register-resident two-waves-per-gate accumulators
+    (STD256Q, q = 1024: launch_blind_rotate_n2k; STD256Q_3_LMKCDEY: launch_blind_rotate_lmk2k; the default),
+    against the one-gate-per-workgroup accumulator the sets ran on before (FHE_HIP_N2K=0,
+    bootstrap_wide.hip A32) on 333 gates of every 2-input type (final and extended outputs) and on the seam's
+    BlindRotate (random accumulators, ciphertexts mod q for GINX and mod 2N for LMKCDEY, as EvalAcc reads
+    them); the gates also decrypt to the truth table.  The reference goldens of the sets run in
     test_gpu_wider_paramset_gates_bit_exact_vs_reference on the default kernel."""
     from fhe_amd import binfhe as bf
-    ps, m = WIDER_SETS["std256q"]
+    ps, m = WIDER_SETS[name]
     assert bf.kernel_path(ps, m) == 4
     keys = bf.keygen(ps, m, 41)
     P = bf.params(ps, m)
@@ -186,7 +188,8 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch):
     x1, x2 = rng.integers(0, 2, B), rng.integers(0, 2, B)
     a1, b1 = bf.encrypt(ps, m, keys.sk, x1, 21)
     a2, b2 = bf.encrypt(ps, m, keys.sk, x2, 22)
-    acc_a = rng.integers(0, P.q, (5, P.n), dtype=np.uint64)
+    amod = 2 * P.N if m == 3 else P.q
+    acc_a = rng.integers(0, amod, (5, P.n), dtype=np.uint64)
     acc = rng.integers(0, P.Q, (5, 2, P.N), dtype=np.uint64)
     res = {}
     for flag in ("1", "0"):
@@ -195,7 +198,7 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch):
         e.load_keys(keys.bsk, keys.kskA, keys.kskB)
         res[flag] = [(e.eval_gate(gate, a1, b1, a2, b2), e.eval_gate_extended(gate, a1, b1, a2, b2))
                      for gate in GATES.values()]
-        res[flag].append(((e.blind_rotate_acc(acc_a, P.q, acc),), ))
+        res[flag].append(((e.blind_rotate_acc(acc_a, amod, acc),), ))
         e.close()
     for (gname, gate), (fast, ref) in zip(GATES.items(), zip(res["1"], res["0"])):
         for u, v in zip(fast, ref):
