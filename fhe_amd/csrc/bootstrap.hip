@@ -2539,7 +2539,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
         s_tab[i]  = T.tabF[i];
         s_tabI[i] = T.tabI[i];
     }
-    const int c = threadIdx.x >> 6, L = threadIdx.x & 63;  // wave c: RLWE component c
+    // wave c: RLWE component c.  (Giving component 0's role, the one the AUTO ops load, to the second
+    // wave in half the workgroups was measured 1.7% slower: profiles/r04_lmk2k_swap_ab.txt)
+    const int c = threadIdx.x >> 6, L = threadIdx.x & 63;
     const uint32_t gate = blockIdx.x;
     uint32_t* tile    = s_tile + c * kW2Tile;
     uint32_t* partner = s_tile + (c ^ 1) * kW2Tile;
