@@ -175,6 +175,12 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
                             uint64_t* b_out, hipStream_t s, uint32_t* part = nullptr, size_t part_words = 0);
 // the row-split factor launch_keyswitch uses for count gates with that scratch
 uint32_t keyswitch_split(size_t count, uint32_t n, uint32_t N, size_t part_words);
+// the u32-sum form of the tiled kernel (u32 rows of ksk_width(n), any power-of-two qKS <= 2^32) for the
+// (baseKS, digitsKS) shapes keyswitch_w32_shape accepts: (16, 5), (16, 6), (64, 3)
+bool keyswitch_w32_shape(uint32_t baseKS, uint32_t digitsKS);
+hipError_t launch_keyswitch_w32(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint32_t* ksk,
+                                const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
+                                uint64_t* b_out, hipStream_t s, uint32_t* part = nullptr, size_t part_words = 0);
 // LWE element-wise operations on [count][len] / [count] u64 arrays (lwe.hip):
 //   reduce: (a, b) mod m (LWECiphertextImpl::SetModulus, lwe-ciphertext.h:116-120)
 //   sub:    x - y mod m, inputs < m (EvalSubEq / EvalSubEq2, lwe-pke.cpp:234-242); outputs may alias

@@ -57,6 +57,12 @@ bool Engine::ks32_set(const Params& p) {
            p.N <= 2048;
 }
 
+bool Engine::ks32w_set(const Params& p) {
+    const bool pow2ks = p.qKS && !(p.qKS & (p.qKS - 1));
+    return !is_large(p.paramset) && !p.timeopt && pow2ks && p.qKS > 65536 && p.qKS <= (1ull << 32) &&
+           keyswitch_w32_shape(p.baseKS, p.digitsKS) && p.n < 2048 && p.N <= 2048;
+}
+
 // K1w tables (bootstrap.hip k_blind_rotate_n2k): Table / TableI (2048 words each, u32 Montgomery; the
 // uniform stages read words 0..31 of them), the half-resolution monomial pairs psi^(2f) - 1 for
 // f in [0, 2048] at f + (f >> 5)
@@ -257,6 +263,9 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         } else if (ks32_set(p_)) {
             const char* e = std::getenv("FHE_HIP_KS32");
             ks32_ = !(e && std::string(e) == "0");
+        } else if (ks32w_set(p_)) {
+            const char* e = std::getenv("FHE_HIP_KS32W");
+            ks32w_ = e && std::string(e) == "1";
         }
         if (method == M_LMKCDEY) {  // op lists (k_prep_lmk_w) for k_blind_rotate_wide_ops
             if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");
@@ -285,7 +294,8 @@ Engine::~Engine() {
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
                       (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
-                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_, d_tables2k_})
+                      (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_, d_tables2k_,
+                      (void*)d_ksk32_})
         if (ptr) (void)hipFree(ptr);
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -610,6 +620,20 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
             FHE_HIP_CHECK(hipMemcpy(d_wksk_ + k * one, A + k * rows * p_.n, rows * p_.n * 8, hipMemcpyHostToDevice));
             FHE_HIP_CHECK(hipMemcpy(d_wksk_ + k * one + rows * p_.n, B + k * rows, rows * 8, hipMemcpyHostToDevice));
         }
+        if (ks32w_) {  // u32 rows of launch_keyswitch_w32: A then B at column n, zero-padded
+            const size_t W = ksk_width(p_.n);
+            std::vector<uint32_t> dev(rows * W, 0);
+#pragma omp parallel for schedule(static)
+            for (int64_t r = 0; r < (int64_t)rows; ++r) {
+                for (uint32_t k = 0; k < p_.n; ++k) dev[(size_t)r * W + k] = (uint32_t)A[(size_t)r * p_.n + k];
+                dev[(size_t)r * W + p_.n] = (uint32_t)B[r];
+            }
+            if (d_ksk32_) FHE_HIP_CHECK(hipFree(d_ksk32_));
+            d_ksk32_ = nullptr;
+            FHE_HIP_CHECK(hipMalloc(&d_ksk32_, dev.size() * 4));
+            FHE_HIP_CHECK(hipMemcpy(d_ksk32_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+            return;
+        }
         if (!ks32_) return;
         // ks32_: also the u16 rows of the 32-bit key switch (qKS <= 2^16; ks32_set)
     }
@@ -742,7 +766,7 @@ void Engine::ensure_work(size_t count) {
         FHE_HIP_CHECK(hipMalloc(&d_wext_a_, count * p_.N * sizeof(uint64_t)));
         FHE_HIP_CHECK(hipMalloc(&d_wext_b_, count * sizeof(uint64_t)));
     }
-    if (!wide_ || ks32_) {  // ks32_: the 32-bit key switch's input (keyswitch_ext)
+    if (!wide_ || ks32_ || ks32w_) {  // ks32_ / ks32w_: the tiled key switch's u32 input (keyswitch_ext)
         FHE_HIP_CHECK(hipMalloc(&d_ext_a_, count * p_.N * sizeof(uint32_t)));
         FHE_HIP_CHECK(hipMalloc(&d_ext_b_, count * sizeof(uint32_t)));
     }
@@ -1078,6 +1102,13 @@ void Engine::keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64
         GateArgs g = gate_args(G_AND, count);
         FHE_HIP_CHECK(launch_keyswitch(g, p_.baseKS, p_.digitsKS, d_ksk_, d_ext_a_, d_ext_b_, q_out, a_out, b_out, s,
                                        ks_part(count), kKsPartWords));
+        return;
+    }
+    if (wide_ && ks32w_ && d_ksk32_ && d_ext_a_ && count <= cap_) {
+        FHE_HIP_CHECK(launch_narrow_u32(d_wext_a_, d_wext_b_, d_ext_a_, d_ext_b_, p_.N, count, s));
+        GateArgs g = gate_args(G_AND, count);
+        FHE_HIP_CHECK(launch_keyswitch_w32(g, p_.baseKS, p_.digitsKS, d_ksk32_, d_ext_a_, d_ext_b_, q_out, a_out, b_out,
+                                           s, ks_part(count), kKsPartWords));
         return;
     }
     if (wide_) {

@@ -62,6 +62,8 @@ public:
     // 64-bit-path sets whose key switch runs on the 32-bit tiled kernel (u16 rows): qKS <= 2^16 a power
     // of two and a tiled shape (baseKS 32 / 64 with digitsKS 3, baseKS 16 with digitsKS 4), n < 2048
     static bool ks32_set(const Params& p);
+    // the u32-sum form for power-of-two qKS above 2^16 (launch_keyswitch_w32 shapes)
+    static bool ks32w_set(const Params& p);
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -208,6 +210,8 @@ private:
     // the 32-bit key switch on the 64-bit path (ks32_set; g3_ sets always, FHE_HIP_KS32=0 keeps the
     // u64 row gathers of launch_keyswitch_wide for the others: A/B, tests)
     bool ks32_ = false;
+    bool ks32w_ = false;
+    uint32_t* d_ksk32_ = nullptr;  // ks32w_: u32 rows of ksk_width(n)
     BootTables tabs2k_{};
     void* d_tables2k_ = nullptr;
     void build_tables_n2k();

@@ -102,8 +102,6 @@ constexpr int kKsCols  = FHE_KS_COLS;           // columns per workgroup (packed
 // LDS bytes per staged slice.  FHE_KS_B64: 136 B, read as 8-byte pieces: slice d's piece k sits in
 // 8-byte bank slot (17 d + k) mod 32, distinct for all 32 slices, so the random per-gate slice
 // choices never conflict (16-byte reads with a 144-B stride collide for slices d, d + 16).
-constexpr int kKsRowB  = kKsCols * 2 + (FHE_KS_B64 ? 8 : 16);
-constexpr int kKsPartsPerSlice = kKsCols * 2 / 16;
 // Tile shapes (G gates per workgroup, IPR values of i per round at baseKS = 32), by batch size
 // (round 3, profiles/r03_ab_keyswitch.txt, per launch at 65,536 / 8192 / 1024 gates):
 //   G 256, IPR 4 (104 KB of LDS, one workgroup per CU):       6.64 ms / 0.82 ms / 125 + 11 us
@@ -125,11 +123,17 @@ constexpr int kKsSplitG = 512;
 // LPF_STD128Q, STD256Q_3_LMKCDEY: 64 slices, 2 values of i per round so that the double buffer keeps the
 // same 104 KB; slices d and d + 32 share a bank slot, a 2-way conflict), both with KD = digitsKS = 3; or
 // 4 with KD = 4 (STD256Q: baseKS 16, qKS 2^16; 2 values of i per round, 35 KB)
-template <int LOGB, int IPR, int KD = 3> struct KsShape {
+// W32: u32 rows and u32 column sums (exact mod any power-of-two qKS <= 2^32: STD192Q_4, STD256Q_4,
+// STD256Q_4_LMKCDEY), one value of i per round, 264-byte slices (8-byte piece k of slice d in bank slot
+// (d + k) mod 32)
+template <int LOGB, int IPR, int KD = 3, bool W32 = false> struct KsShape {
     static constexpr int base  = 1 << LOGB;
-    static constexpr int ipr   = LOGB == 5 ? IPR : 2;
+    static constexpr int eb    = W32 ? 4 : 2;                     // bytes per KSK element
+    static constexpr int ipr   = W32 ? 1 : LOGB == 5 ? IPR : 2;
     static constexpr int step  = ipr * KD;                        // (i, j) steps per round / LDS buffer / barrier
-    static constexpr int parts = base * kKsCols * 2 / 16;         // 16-byte parts staged per step
+    static constexpr int rowb  = kKsCols * eb + (W32 || FHE_KS_B64 ? 8 : 16);  // LDS bytes per staged slice
+    static constexpr int pps   = kKsCols * eb / 16;               // 16-byte parts per slice
+    static constexpr int parts = base * pps;                      // 16-byte parts staged per step
 };
 
 // Row split (blockIdx.z, small batches): a workgroup sums the rounds [z R/S, (z+1) R/S) only and
@@ -137,17 +141,19 @@ template <int LOGB, int IPR, int KD = 3> struct KsShape {
 // (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
 // 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
-template <int G, bool SPLIT, int LOGB, int IPR, int KD = 3>
+template <int G, bool SPLIT, int LOGB, int IPR, int KD = 3, bool W32 = false>
 __global__ void __launch_bounds__(G)
-    k_keyswitch_tiled(GateArgs g, const uint16_t* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
+    k_keyswitch_tiled(GateArgs g, const void* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                       uint64_t* __restrict__ b_out, uint32_t* __restrict__ part) {
-    using S_ = KsShape<LOGB, IPR, KD>;
+    using S_ = KsShape<LOGB, IPR, KD, W32>;
     constexpr int kKsDigits = KD;
     constexpr int kKsParts = S_::parts, kKsStep = S_::step, kIPR = S_::ipr, kBase = S_::base;
+    constexpr int kRowB = S_::rowb, kPps = S_::pps, kEB = S_::eb;
+    constexpr int kAcc = W32 ? kKsCols : kKsCols / 2;  // u32 sums, or packed u16 pairs
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
-    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][kBase * kKsRowB];
+    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][kBase * kRowB];
     const uint32_t t = threadIdx.x;
     // FHE_KS_XCD: workgroups are dispatched round-robin over the 8 XCDs by linear id, so with the
     // 8 column tiles of a 512-column KSK mapped to (linear id mod 8) every XCD stages one column
@@ -163,20 +169,21 @@ __global__ void __launch_bounds__(G)
     const uint32_t col0 = by * kKsCols;
     const uint32_t rounds = SPLIT ? g.N / kIPR / gridDim.z : g.N / kIPR;  // this workgroup's share
     const uint32_t r0 = SPLIT ? blockIdx.z * rounds : 0;
-    using AV = typename std::conditional<kIPR == 4, uint4, uint2>::type;
-    static_assert(kIPR == 4 || kIPR == 2, "a_i vector width");
+    using AV = typename std::conditional<kIPR == 4, uint4, typename std::conditional<kIPR == 2, uint2, uint32_t>::type>::type;
+    static_assert(kIPR == 4 || kIPR == 2 || kIPR == 1, "a_i vector width");
     const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N) + r0;
 
-    // staging role: part x = t + G*r -> slice x / kKsPartsPerSlice, 16-byte part x % kKsPartsPerSlice
+    // staging role: part x = t + G*r -> slice x / kPps, 16-byte part x % kPps
     auto slice_src = [&](uint32_t round, int q, int r) -> const uint4* {
-        const uint32_t x = t + G * r, sd = x / kKsPartsPerSlice, sp = x % kKsPartsPerSlice;
+        const uint32_t x = t + G * r, sd = x / kPps, sp = x % kPps;
         const uint32_t i = (r0 + round) * kIPR + q / kKsDigits, j = q % kKsDigits;
         const size_t row = ((size_t)i * kBase + sd) * kKsDigits + j;
-        return reinterpret_cast<const uint4*>(ksk + row * ksk_width(g.n) + col0) + sp;
+        return reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(ksk) +
+                                              (row * ksk_width(g.n) + col0) * kEB) + sp;
     };
     auto slice_dst = [&](unsigned char* sb, int r) -> unsigned char* {
         const uint32_t x = t + G * r;
-        return sb + (x / kKsPartsPerSlice) * kKsRowB + (x % kKsPartsPerSlice) * 16;
+        return sb + (x / kPps) * kRowB + (x % kPps) * 16;
     };
     auto put = [&](unsigned char* dst, const uint4& v) {
         if (FHE_KS_B64) {  // 8-byte aligned only
@@ -187,9 +194,9 @@ __global__ void __launch_bounds__(G)
         }
     };
 
-    uint32_t acc[kKsCols / 2];
+    uint32_t acc[kAcc];
 #pragma unroll
-    for (int k = 0; k < kKsCols / 2; ++k) acc[k] = 0;
+    for (int k = 0; k < kAcc; ++k) acc[k] = 0;
 
     uint4 st[kKsStep][P];
     // threads past kKsParts (narrow column tiles) stage nothing: their slice index would run past
@@ -226,8 +233,21 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q) {
             const uint32_t dig = (as[q / kKsDigits] >> (LOGB * (q % kKsDigits))) & (kBase - 1);
-            if (FHE_KS_B64) {
-                const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kKsRowB);
+            if (W32) {  // u32 columns: 32 8-byte pieces, one v_sub_u32 per column
+                const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kRowB);
+                uint2 w[kKsCols / 2];
+#pragma unroll
+                for (int k = 0; k < kKsCols / 2; ++k) {
+                    w[k] = src[k];
+                    asm volatile("" ::: "memory");
+                }
+#pragma unroll
+                for (int k = 0; k < kKsCols / 2; ++k) {
+                    acc[2 * k + 0] -= w[k].x;
+                    acc[2 * k + 1] -= w[k].y;
+                }
+            } else if (FHE_KS_B64) {
+                const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kRowB);
                 uint2 w[kKsCols / 4];
 #pragma unroll
                 for (int k = 0; k < kKsCols / 4; ++k) {
@@ -242,7 +262,7 @@ __global__ void __launch_bounds__(G)
                     acc[2 * k + 1] = pk_sub_u16(acc[2 * k + 1], w[k].y);
                 }
             } else {
-                const uint4* src = reinterpret_cast<const uint4*>(s_buf[buf][q] + dig * kKsRowB);
+                const uint4* src = reinterpret_cast<const uint4*>(s_buf[buf][q] + dig * kRowB);
 #pragma unroll
                 for (int k = 0; k < kKsCols / 8; ++k) {
                     const uint4 w = src[k];
@@ -255,17 +275,28 @@ __global__ void __launch_bounds__(G)
         }
     }
     if (!valid) return;
-    if (SPLIT) {
-        uint4* pp = reinterpret_cast<uint4*>(part + ((size_t)blockIdx.z * g.count + gate) * (ksk_width(g.n) / 2) +
-                                             col0 / 2);
+    if (SPLIT) {  // partial rows of ksk_width / 2 packed pairs, or ksk_width u32 sums (W32)
+        const size_t hw = W32 ? ksk_width(g.n) : ksk_width(g.n) / 2;
+        uint4* pp = reinterpret_cast<uint4*>(part + ((size_t)blockIdx.z * g.count + gate) * hw + (W32 ? col0 : col0 / 2));
 #pragma unroll
-        for (int k = 0; k < kKsCols / 8; ++k)
+        for (int k = 0; k < kAcc / 4; ++k)
             pp[k] = make_uint4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
         return;
     }
     const uint32_t qm = g.qKS - 1;
     const uint32_t b = ms_b[gate];
     uint64_t* oa = a_out + (size_t)gate * g.n;
+    if (W32) {
+#pragma unroll
+        for (int k = 0; k < kKsCols; ++k) {
+            const uint32_t c = col0 + k;
+            uint64_t v = ((c == g.n ? b : 0u) + acc[k]) & qm;  // acc = -sum mod 2^32
+            if (q_out) v = mod_switch_up(v, g.qKS, q_out);
+            if (c < g.n) oa[c] = v;
+            else if (c == g.n) b_out[gate] = v;
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kKsCols / 2; ++k) {
 #pragma unroll
@@ -282,6 +313,7 @@ __global__ void __launch_bounds__(G)
 
 // the S row-split partials of a gate, one packed column pair per thread and step (hw = W / 2 pairs, up
 // to 640 at W = 1280, on at most 512 threads), then the epilogue
+template <bool W32>
 __global__ void __launch_bounds__(512)
     k_keyswitch_reduce(GateArgs g, const uint32_t* __restrict__ part, uint32_t S, uint32_t hw,
                        const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
@@ -290,6 +322,17 @@ __global__ void __launch_bounds__(512)
     const uint32_t qm = g.qKS - 1;
     const uint32_t b = ms_b[gate];
     uint64_t* oa = a_out + (size_t)gate * g.n;
+    if (W32) {  // hw = ksk_width u32 sums (mod 2^32)
+        for (uint32_t c = threadIdx.x; c < hw; c += blockDim.x) {
+            uint32_t acc = 0;
+            for (uint32_t z = 0; z < S; ++z) acc += part[((size_t)z * g.count + gate) * hw + c];
+            uint64_t v = ((c == g.n ? b : 0u) + acc) & qm;
+            if (q_out) v = mod_switch_up(v, g.qKS, q_out);
+            if (c < g.n) oa[c] = v;
+            else if (c == g.n) b_out[gate] = v;
+        }
+        return;
+    }
     for (uint32_t t = threadIdx.x; t < hw; t += blockDim.x) {
         uint32_t acc = 0;
         for (uint32_t z = 0; z < S; ++z) {
@@ -362,12 +405,52 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
         if (S > 1) {
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(k_keyswitch_reduce, dim3(g.count), dim3(std::min(W / 2, 512u)), 0, s, g, part, S, W / 2,
-                               ms_b, q_out, a_out, b_out);
+            hipLaunchKernelGGL(k_keyswitch_reduce<false>, dim3(g.count), dim3(std::min(W / 2, 512u)), 0, s, g, part, S,
+                               W / 2, ms_b, q_out, a_out, b_out);
         }
     } else {
         hipLaunchKernelGGL(k_keyswitch, dim3(g.count), dim3(W / 2), 0, s, g, logBase, digitsKS,
                            reinterpret_cast<const uint32_t*>(ksk), ms_a, ms_b, q_out, a_out, b_out);
+    }
+    return hipGetLastError();
+}
+
+bool keyswitch_w32_shape(uint32_t baseKS, uint32_t digitsKS) {
+    return (baseKS == 16 && (digitsKS == 5 || digitsKS == 6)) || (baseKS == 64 && digitsKS == 3);
+}
+
+// u32 rows (ksk_width(n) columns: A then B at column n), any power-of-two qKS <= 2^32, the shapes of
+// keyswitch_w32_shape; row split below 4096 gates into part (u32 [S][count][W])
+hipError_t launch_keyswitch_w32(const GateArgs& g, uint32_t baseKS, uint32_t digitsKS, const uint32_t* ksk,
+                                const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
+                                uint64_t* b_out, hipStream_t s, uint32_t* part, size_t part_words) {
+    if (g.count == 0) return hipSuccess;
+    if (!keyswitch_w32_shape(baseKS, digitsKS) || (g.qKS & (g.qKS - 1)) || g.qKS == 0 || g.n >= 2048 || g.N > 2048)
+        return hipErrorInvalidValue;
+    const uint32_t W = ksk_width(g.n);
+    constexpr uint32_t G = 256;
+    uint32_t S = 1;
+    if (part) {  // enough workgroups for 4 per CU, at least 16 rounds each, within the scratch
+        const size_t tiles = ((g.count + G - 1) / G) * (W / kKsCols);
+        while (tiles * S < 1024 && g.N / (2 * S) >= 16 && (size_t)2 * S * g.count * W <= part_words) S *= 2;
+    }
+    const dim3 grid((g.count + G - 1) / G, W / kKsCols, S);
+#define FHE_KSW_LAUNCH(SP, LB, KD_)                                                                               \
+    hipLaunchKernelGGL((k_keyswitch_tiled<G, SP, LB, 1, KD_, true>), grid, dim3(G), 0, s, g, ksk, ms_a, ms_b, q_out, \
+                       a_out, b_out, SP ? part : nullptr)
+    if (baseKS == 16 && digitsKS == 5) {
+        if (S > 1) FHE_KSW_LAUNCH(true, 4, 5); else FHE_KSW_LAUNCH(false, 4, 5);
+    } else if (baseKS == 16) {
+        if (S > 1) FHE_KSW_LAUNCH(true, 4, 6); else FHE_KSW_LAUNCH(false, 4, 6);
+    } else {
+        if (S > 1) FHE_KSW_LAUNCH(true, 6, 3); else FHE_KSW_LAUNCH(false, 6, 3);
+    }
+#undef FHE_KSW_LAUNCH
+    if (S > 1) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_keyswitch_reduce<true>, dim3(g.count), dim3(512), 0, s, g, part, S, W, ms_b, q_out, a_out,
+                           b_out);
     }
     return hipGetLastError();
 }
