@@ -137,13 +137,13 @@ __host__ __device__ constexpr uint32_t g2_key_word(uint32_t nd, uint32_t c, uint
 hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const void* keys, const uint16_t* idx,
                                    const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
 bool n2k_supported(const GateArgs& g, const BootTables& t);
-// K1w for LMKCDEY (k_blind_rotate_lmk2k): N = 2048, Q < 2^27, digitsG = 4 (STD256Q_LMKCDEY,
-// STD256Q_3_LMKCDEY); op lists of launch_prep_lmk, keys in Engine::pack_n2k's LMKCDEY layout (ek per
-// index, then ak per automorphism key), tables as launch_blind_rotate_n2k
+// K1w for LMKCDEY (k_blind_rotate_lmk2k<nd>): N = 2048, Q < 2^27, digitsG = nd + 1 = 4 or 5
+// (STD256Q_3_LMKCDEY, STD256Q_4_LMKCDEY); op lists of launch_prep_lmk, keys in Engine::pack_n2k's
+// LMKCDEY layout (ek per index, then ak per automorphism key), tables as launch_blind_rotate_n2k
 hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
                                      const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
-                                     uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
-bool lmk2k_supported(const GateArgs& g, const BootTables& t);
+                                     uint64_t* ext_a, uint64_t* ext_b, int nd, hipStream_t s);
+bool lmk2k_supported(const GateArgs& g, const BootTables& t, int nd);
 // fused blind rotation (EvalAcc CGGI) + Transpose + iNTT + b fix-up + ModSwitch(Q -> qKS)
 hipError_t launch_blind_rotate_ginx(const GateArgs& g, const BootTables& t, const void* bsk, const uint16_t* idx,
                                     const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);

@@ -2465,7 +2465,8 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
 // each reduced sum < 1.6 Q, acc < 3.2 Q after an exchange (the inverse plan's BIN = 33).
 // ===========================================================================
 namespace {
-constexpr int kL2AccBound = 33;  // |acc| < 3.3 Q between ops (units of Q/10)
+// |acc| between ops, units of Q/10: 2 (ND (11 Q + 2^(g-1)) Q 2^-32 + Q/2) for Q < 2^27
+template <int ND> constexpr int kL2AccBound = ND == 3 ? 33 : 38;
 constexpr size_t l2k_lds() { return (size_t)(2048 + 2048 + 2 * kW2Tile) * 4; }
 
 // EVAL automorphism X -> X^k on layout C through this wave's tile (as automorphism_c at N = 1024):
@@ -2524,13 +2525,14 @@ FHE_DEV void mac_2k(uint32_t (&acc)[32], const uint32_t (&d)[ND][32], const uint
 }
 }  // namespace
 
-template <bool ACCIO>
+template <int ND, bool ACCIO>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_blind_rotate_lmk2k(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
                          const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
                          const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                          const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
-    constexpr int ND = 3, kQ = 2 * ND;
+    constexpr int kQ = 2 * ND;
+    constexpr int BIN = kL2AccBound<ND>;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 2048;
@@ -2595,7 +2597,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             // ---- AddToAccLMKCDEY: acc_c <- sum over both components' digits of D ek[op][row][c]
 #pragma unroll
             for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-            inv_2k_s<kL2AccBound>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+            inv_2k_s<BIN>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
             fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
@@ -2615,7 +2617,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             if (c == 0) {  // acc0' -> COEF -> 3 digits -> EVAL; acc0 replaced, acc1's share to the tile
 #pragma unroll
                 for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-                inv_2k_s<kL2AccBound>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+                inv_2k_s<BIN>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
                 for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
                 fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
@@ -2644,7 +2646,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_n2k
     __syncthreads();  // the partner has read this wave's tile
-    inv_2k_s<kL2AccBound>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
+    inv_2k_s<BIN>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
     if (c == 0) {
         uint64_t* oa = ext_a + (size_t)gate * g.N;
 #pragma unroll
@@ -2660,24 +2662,24 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
-bool lmk2k_supported(const GateArgs& g, const BootTables& t) {
+bool lmk2k_supported(const GateArgs& g, const BootTables& t, int nd) {
     return t.Q < (1u << 27) && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 &&
-           4 * g.gbits <= 32;
+           (nd == 3 || nd == 4) && (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
 hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
                                      const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
-                                     uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+                                     uint64_t* ext_a, uint64_t* ext_b, int nd, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if (!lmk2k_supported(g, t)) return hipErrorInvalidValue;
+    if (!lmk2k_supported(g, t, nd)) return hipErrorInvalidValue;
     const uint4* e = static_cast<const uint4*>(ek);
     const uint4* a = static_cast<const uint4*>(ak);
-    if (g.acc_io)
-        hipLaunchKernelGGL(k_blind_rotate_lmk2k<true>, dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, nops,
-                           maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
-    else
-        hipLaunchKernelGGL(k_blind_rotate_lmk2k<false>, dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, nops,
-                           maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+#define FHE_L2K(ND_, IO)                                                                                           \
+    hipLaunchKernelGGL((k_blind_rotate_lmk2k<ND_, IO>), dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, nops, \
+                       maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
+    if (nd == 3) { if (g.acc_io) FHE_L2K(3, true); else FHE_L2K(3, false); }
+    else { if (g.acc_io) FHE_L2K(4, true); else FHE_L2K(4, false); }
+#undef FHE_L2K
     return hipGetLastError();
 }
 

@@ -42,12 +42,17 @@ bool Engine::g3_set(const Params& p) {
 }
 
 bool Engine::n2k_set(const Params& p) {
+    // GINX with even monomial exponents (q < 2N: the half-resolution table) and digitsG = 4; LMKCDEY at
+    // any q with digitsG = 4 or 5 (3 or 4 retained digits); the digit fields of d + C in 32 bits
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
-    const uint64_t C = h * (1 + (1ull << g) + (1ull << (2 * g)) + (1ull << (3 * g)));
-    // GINX with even monomial exponents (q < 2N: the half-resolution table), LMKCDEY at any q
-    const bool ginx = p.method == M_GINX && p.q < 2 * p.N;
-    return !is_large(p.paramset) && !p.timeopt && (ginx || p.method == M_LMKCDEY) && p.N == 2048 &&
-           p.Q < (1ull << 27) && p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32);
+    const bool ginx = p.method == M_GINX && p.q < 2 * p.N && p.digitsG == 4;
+    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || p.digitsG == 5);
+    if (is_large(p.paramset) || p.timeopt || !(ginx || lmk) || p.N != 2048 || p.Q >= (1ull << 27) || g < 2 ||
+        (uint64_t)p.digitsG * g > 32)
+        return false;
+    uint64_t C = 0;
+    for (uint32_t j = 0; j < p.digitsG; ++j) C += h << (j * g);
+    return C + p.Q < (1ull << 32);
 }
 
 bool Engine::ks32_set(const Params& p) {
@@ -119,30 +124,31 @@ void Engine::pack_n2k(const uint64_t* bsk) {
     auto word = [&](uint64_t v) { return to_mont(mulmod(v % Q, ninv, Q), Q); };
     auto slot = [](uint32_t L, uint32_t r) { return ((r >> 1) << 7) | (L << 1) | (r & 1); };
     if (p_.method == M_LMKCDEY) {
-        const size_t per = (size_t)2 * 6 * 8 * 64 * 4, aper = (size_t)6 * 8 * 64 * 4;
+        const uint32_t nd = p_.digitsG - 1, kq = 2 * nd;  // retained digits, key vectors per slot
+        const size_t per = (size_t)2 * kq * 8 * 64 * 4, aper = (size_t)kq * 8 * 64 * 4;
         const size_t nauto = (size_t)p_.numAutoKeys + 1;
         std::vector<uint32_t> dev((size_t)n * per + nauto * aper);
 #pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < (int64_t)n; ++i)
             for (uint32_t c = 0; c < 2; ++c)
-                for (uint32_t q = 0; q < 6; ++q)
+                for (uint32_t q = 0; q < kq; ++q)
                     for (uint32_t k4 = 0; k4 < 8; ++k4)
                         for (uint32_t L = 0; L < 64; ++L)
                             for (uint32_t e = 0; e < 4; ++e) {
                                 const uint32_t row = 2 * (q >> 1) + c, col = (q & 1) ? 1 - c : c;
                                 const size_t src = (((size_t)i * dG2 + row) * 2 + col) * N + slot(L, 4 * k4 + e);
-                                dev[(size_t)i * per + ((((c * 6 + q) * 8 + k4) * 64 + L) * 4 + e)] = word(bsk[src]);
+                                dev[(size_t)i * per + ((((c * kq + q) * 8 + k4) * 64 + L) * 4 + e)] = word(bsk[src]);
                             }
         const uint64_t* asrc = bsk + (size_t)n * dG2 * 2 * N;
         uint32_t* adst = dev.data() + (size_t)n * per;
         for (size_t t = 0; t < nauto; ++t)
-            for (uint32_t q = 0; q < 6; ++q)
+            for (uint32_t q = 0; q < kq; ++q)
                 for (uint32_t k4 = 0; k4 < 8; ++k4)
                     for (uint32_t L = 0; L < 64; ++L)
                         for (uint32_t e = 0; e < 4; ++e) {
                             const uint32_t d = q >> 1, col = q & 1;
                             adst[t * aper + (((q * 8 + k4) * 64 + L) * 4 + e)] =
-                                word(asrc[((t * 3 + d) * 2 + col) * N + slot(L, 4 * k4 + e)]);
+                                word(asrc[((t * nd + d) * 2 + col) * N + slot(L, 4 * k4 + e)]);
                         }
         FHE_HIP_CHECK(hipSetDevice(device_));
         if (d_bsk2_) FHE_HIP_CHECK(hipFree(d_bsk2_));
@@ -833,11 +839,13 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
                                                    d_tvb_, d_wext_a_, d_wext_b_, s));
             return;
         }
-        if (n2k_ && p_.method == M_LMKCDEY && d_bsk2_ && lmk2k_supported(g, tabs2k_) && g.lv == g.lv64 &&
+        const int nd = (int)p_.digitsG - 1;
+        if (n2k_ && p_.method == M_LMKCDEY && d_bsk2_ && lmk2k_supported(g, tabs2k_, nd) && g.lv == g.lv64 &&
             g.uv == g.uv64 && g.b_const == g.b64) {
             const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);
-            FHE_HIP_CHECK(launch_blind_rotate_lmk2k(g, tabs2k_, ek, ek + (size_t)p_.n * 24576, d_ops_, d_nops_, maxops_,
-                                                    d_tvb_, d_wext_a_, d_wext_b_, s));
+            const size_t per = (size_t)2 * 2 * nd * 8 * 64 * 4;  // pack_n2k's ek words per index
+            FHE_HIP_CHECK(launch_blind_rotate_lmk2k(g, tabs2k_, ek, ek + (size_t)p_.n * per, d_ops_, d_nops_, maxops_,
+                                                    d_tvb_, d_wext_a_, d_wext_b_, nd, s));
             return;
         }
         if (p_.method == M_LMKCDEY || p_.method == M_AP) {
