@@ -2081,7 +2081,9 @@ FHE_DEV int wa2k(int L) { return L; }
 FHE_DEV int wb2k(int L) { return 66 * (L >> 1) + (L & 1); }
 FHE_DEV int wc2k(int L) { return 2 * L + 2 * (L >> 5); }
 
-template <int NP>
+// RED (2^27 <= Q < 2^28, 8Q of signed headroom): one signed Montgomery product by 2^32 mod Q after the
+// five A stages (|v| < 5Q + 2^(g-1) -> < 0.82 Q), so the six stages after it end below 6.82 Q
+template <int NP, bool RED = false>
 FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t* __restrict__ twA,
                       const uint32_t* s_tab, const Mod& m) {
     const int G = L >> 1;
@@ -2098,6 +2100,12 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
 #pragma unroll
             for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
         }
+    }
+    if (RED) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 32; ++r) v[p][r] = smont_mul(v[p][r], m.oneR, m);
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {  // A -> B
@@ -2181,10 +2189,12 @@ constexpr InvPlan2k make_inv_plan_2k() {
 }
 // signed inverse NTT, layout C (EVAL, |v| < BIN Q / 10) -> A (COEF), canonical [0, Q); the keys carry
 // N^-1, so the last stage scales by TableI[1] only (w1R)
-template <int BIN>
+// LIM: the signed headroom in units of Q/10 (160: Q < 2^27; 80: Q < 2^28, where the last stage's
+// x + y + (Q << fin) stays below 16 Q < 2^32)
+template <int BIN, int LIM = 160>
 FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __restrict__ twAi,
                       const uint32_t* s_tabI, uint32_t w1R, uint32_t oneR, const Mod& m) {
-    constexpr InvPlan2k P = make_inv_plan_2k<BIN, 160>();
+    constexpr InvPlan2k P = make_inv_plan_2k<BIN, LIM>();
     auto redp = [&](int st) {
 #pragma unroll
         for (int r = 0; r < 32; ++r)
@@ -2465,8 +2475,9 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
 // each reduced sum < 1.6 Q, acc < 3.2 Q after an exchange (the inverse plan's BIN = 33).
 // ===========================================================================
 namespace {
-// |acc| between ops, units of Q/10: 2 (ND (11 Q + 2^(g-1)) Q 2^-32 + Q/2) for Q < 2^27
-template <int ND> constexpr int kL2AccBound = ND == 3 ? 33 : 38;
+// |acc| between ops, units of Q/10: 2 (ND (11 Q + 2^(g-1)) Q 2^-32 + Q/2) for Q < 2^27; Q28 (ND = 2,
+// 2^27 <= Q < 2^28, the forward transform reduced once): 2 (2 (6.82 Q) Q 2^-32 + Q/2) < 2.8 Q
+template <int ND, bool Q28> constexpr int kL2AccBound = Q28 ? 28 : ND == 4 ? 38 : 33;
 constexpr size_t l2k_lds() { return (size_t)(2048 + 2048 + 2 * kW2Tile) * 4; }
 
 // EVAL automorphism X -> X^k on layout C through this wave's tile (as automorphism_c at N = 1024):
@@ -2525,14 +2536,14 @@ FHE_DEV void mac_2k(uint32_t (&acc)[32], const uint32_t (&d)[ND][32], const uint
 }
 }  // namespace
 
-template <int ND, bool ACCIO>
+template <int ND, bool ACCIO, bool Q28 = false>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_blind_rotate_lmk2k(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
                          const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
                          const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                          const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
     constexpr int kQ = 2 * ND;
-    constexpr int BIN = kL2AccBound<ND>;
+    constexpr int BIN = kL2AccBound<ND, Q28>, LIM = Q28 ? 80 : 160;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 2048;
@@ -2573,7 +2584,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             }
             tv[0][r] = v;
         }
-        fwd_2k_s<1>(tv, tile, L, twAf, s_tab, m);
+        fwd_2k_s<1, Q28>(tv, tile, L, twAf, s_tab, m);
 #pragma unroll
         for (int r = 0; r < 32; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
         automorphism_2k(acc, tile, L, M - 5);
@@ -2597,10 +2608,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             // ---- AddToAccLMKCDEY: acc_c <- sum over both components' digits of D ek[op][row][c]
 #pragma unroll
             for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-            inv_2k_s<BIN>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+            inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
-            fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
+            fwd_2k_s<ND, Q28>(d, tile, L, twF, s_tab, m);
             mac_2k<ND>(acc, d, ek + ((size_t)op * 2 + c) * (kQ * 8 * 64) + L, tile, L, m);
             __syncthreads();  // both waves' partner words are in LDS
 #pragma unroll
@@ -2617,10 +2628,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             if (c == 0) {  // acc0' -> COEF -> 3 digits -> EVAL; acc0 replaced, acc1's share to the tile
 #pragma unroll
                 for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-                inv_2k_s<BIN>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+                inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
                 for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
-                fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
+                fwd_2k_s<ND, Q28>(d, tile, L, twF, s_tab, m);
                 mac_2k<ND>(acc, d, ak + (size_t)t * (kQ * 8 * 64) + L, tile, L, m);
             }
             __syncthreads();  // wave 0's share of acc1 is in its tile
@@ -2646,7 +2657,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_n2k
     __syncthreads();  // the partner has read this wave's tile
-    inv_2k_s<BIN>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
+    inv_2k_s<BIN, LIM>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
     if (c == 0) {
         uint64_t* oa = ext_a + (size_t)gate * g.N;
 #pragma unroll
@@ -2663,8 +2674,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 bool lmk2k_supported(const GateArgs& g, const BootTables& t, int nd) {
-    return t.Q < (1u << 27) && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 &&
-           (nd == 3 || nd == 4) && (uint32_t)(nd + 1) * g.gbits <= 32;
+    // 2 retained digits up to Q < 2^28 (the forward transform reduced once), 3 or 4 below 2^27
+    const bool qok = nd == 2 ? t.Q < (1u << 28) : t.Q < (1u << 27);
+    return qok && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && nd >= 2 && nd <= 4 &&
+           (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
 hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
@@ -2674,11 +2687,14 @@ hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, con
     if (!lmk2k_supported(g, t, nd)) return hipErrorInvalidValue;
     const uint4* e = static_cast<const uint4*>(ek);
     const uint4* a = static_cast<const uint4*>(ak);
-#define FHE_L2K(ND_, IO)                                                                                           \
-    hipLaunchKernelGGL((k_blind_rotate_lmk2k<ND_, IO>), dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, nops, \
-                       maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
-    if (nd == 3) { if (g.acc_io) FHE_L2K(3, true); else FHE_L2K(3, false); }
-    else { if (g.acc_io) FHE_L2K(4, true); else FHE_L2K(4, false); }
+#define FHE_L2K(ND_, IO, Q28_)                                                                                     \
+    hipLaunchKernelGGL((k_blind_rotate_lmk2k<ND_, IO, Q28_>), dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, \
+                       nops, maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
+    if (nd == 2) {  // STD256Q_LMKCDEY (28-bit Q)
+        if (t.Q >= (1u << 27)) { if (g.acc_io) FHE_L2K(2, true, true); else FHE_L2K(2, false, true); }
+        else { if (g.acc_io) FHE_L2K(2, true, false); else FHE_L2K(2, false, false); }
+    } else if (nd == 3) { if (g.acc_io) FHE_L2K(3, true, false); else FHE_L2K(3, false, false); }
+    else { if (g.acc_io) FHE_L2K(4, true, false); else FHE_L2K(4, false, false); }
 #undef FHE_L2K
     return hipGetLastError();
 }

@@ -41,13 +41,19 @@ bool Engine::g3_set(const Params& p) {
            p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.qKS <= 65536 && p.n < 1024;
 }
 
+constexpr bool kN2kExtended = false;
 bool Engine::n2k_set(const Params& p) {
     // GINX with even monomial exponents (q < 2N: the half-resolution table) and digitsG = 4; LMKCDEY at
     // any q with digitsG = 4 or 5 (3 or 4 retained digits); the digit fields of d + C in 32 bits
+    // (digitsG = 3, two retained digits: Q < 2^28, the forward transform reduced once -- STD256Q_LMKCDEY)
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
     const bool ginx = p.method == M_GINX && p.q < 2 * p.N && p.digitsG == 4;
-    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || p.digitsG == 5);
-    if (is_large(p.paramset) || p.timeopt || !(ginx || lmk) || p.N != 2048 || p.Q >= (1ull << 27) || g < 2 ||
+    // digitsG 3 (28-bit Q) and 5: FHE_HIP_N2K_EXT=1 until measured on the GPU (kN2kExtended)
+    const char* ext = std::getenv("FHE_HIP_N2K_EXT");
+    const bool wide_rows = ext ? std::string(ext) == "1" : kN2kExtended;
+    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || (wide_rows && (p.digitsG == 3 || p.digitsG == 5)));
+    const uint64_t qmax = p.digitsG == 3 ? (1ull << 28) : (1ull << 27);
+    if (is_large(p.paramset) || p.timeopt || !(ginx || lmk) || p.N != 2048 || p.Q >= qmax || g < 2 ||
         (uint64_t)p.digitsG * g > 32)
         return false;
     uint64_t C = 0;
