@@ -2477,7 +2477,7 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
 namespace {
 // |acc| between ops, units of Q/10: 2 (ND (11 Q + 2^(g-1)) Q 2^-32 + Q/2) for Q < 2^27; Q28 (ND = 2,
 // 2^27 <= Q < 2^28, the forward transform reduced once): 2 (2 (6.82 Q) Q 2^-32 + Q/2) < 2.8 Q
-template <int ND, bool Q28> constexpr int kL2AccBound = Q28 ? 28 : ND == 4 ? 38 : 33;
+template <int ND, bool Q28> constexpr int kL2AccBound = Q28 ? 28 : 33;
 constexpr size_t l2k_lds() { return (size_t)(2048 + 2048 + 2 * kW2Tile) * 4; }
 
 // EVAL automorphism X -> X^k on layout C through this wave's tile (as automorphism_c at N = 1024):
@@ -2674,9 +2674,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 bool lmk2k_supported(const GateArgs& g, const BootTables& t, int nd) {
-    // 2 retained digits up to Q < 2^28 (the forward transform reduced once), 3 or 4 below 2^27
+    // 2 retained digits up to Q < 2^28 (the forward transform reduced once), 3 below 2^27.  (4 digits,
+    // STD256Q_4_LMKCDEY, compiled to a kernel with 10,853 scalar instructions and ran at 1.07K gates/s
+    // against 10.6K on K5: profiles/r04_ext_bench.txt; not instantiated.)
     const bool qok = nd == 2 ? t.Q < (1u << 28) : t.Q < (1u << 27);
-    return qok && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && nd >= 2 && nd <= 4 &&
+    return qok && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && nd >= 2 && nd <= 3 &&
            (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
@@ -2693,8 +2695,7 @@ hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, con
     if (nd == 2) {  // STD256Q_LMKCDEY (28-bit Q)
         if (t.Q >= (1u << 27)) { if (g.acc_io) FHE_L2K(2, true, true); else FHE_L2K(2, false, true); }
         else { if (g.acc_io) FHE_L2K(2, true, false); else FHE_L2K(2, false, false); }
-    } else if (nd == 3) { if (g.acc_io) FHE_L2K(3, true, false); else FHE_L2K(3, false, false); }
-    else { if (g.acc_io) FHE_L2K(4, true, false); else FHE_L2K(4, false, false); }
+    } else { if (g.acc_io) FHE_L2K(3, true, false); else FHE_L2K(3, false, false); }
 #undef FHE_L2K
     return hipGetLastError();
 }

@@ -41,18 +41,19 @@ bool Engine::g3_set(const Params& p) {
            p.digitsG == 4 && g >= 2 && 4 * g <= 32 && C + p.Q < (1ull << 32) && p.qKS <= 65536 && p.n < 1024;
 }
 
-constexpr bool kN2kExtended = false;
+constexpr bool kN2kExtended = true;
 bool Engine::n2k_set(const Params& p) {
     // GINX with even monomial exponents (q < 2N: the half-resolution table) and digitsG = 4; LMKCDEY at
     // any q with digitsG = 4 or 5 (3 or 4 retained digits); the digit fields of d + C in 32 bits
     // (digitsG = 3, two retained digits: Q < 2^28, the forward transform reduced once -- STD256Q_LMKCDEY)
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
     const bool ginx = p.method == M_GINX && p.q < 2 * p.N && p.digitsG == 4;
-    // digitsG 3 (28-bit Q) and 5: FHE_HIP_N2K_EXT=1 until measured on the GPU (kN2kExtended)
+    // digitsG 3 with 2^27 <= Q < 2^28 (STD256Q_LMKCDEY) measured 24.0K -> 32.7K gates/s
+    // (profiles/r04_ext_bench.txt); FHE_HIP_N2K_EXT=0 keeps it on K5
     const char* ext = std::getenv("FHE_HIP_N2K_EXT");
     const bool wide_rows = ext ? std::string(ext) == "1" : kN2kExtended;
-    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || (wide_rows && (p.digitsG == 3 || p.digitsG == 5)));
-    const uint64_t qmax = p.digitsG == 3 ? (1ull << 28) : (1ull << 27);
+    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || (wide_rows && p.digitsG == 3));
+    const uint64_t qmax = p.digitsG == 3 ? (1ull << 28) : (1ull << 27);  // digitsG 3: 2 digits, 8Q plan
     if (is_large(p.paramset) || p.timeopt || !(ginx || lmk) || p.N != 2048 || p.Q >= qmax || g < 2 ||
         (uint64_t)p.digitsG * g > 32)
         return false;
@@ -275,9 +276,9 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
         } else if (ks32_set(p_)) {
             const char* e = std::getenv("FHE_HIP_KS32");
             ks32_ = !(e && std::string(e) == "0");
-        } else if (ks32w_set(p_)) {
-            const char* e = std::getenv("FHE_HIP_KS32W");
-            ks32w_ = e && std::string(e) == "1";
+        } else if (ks32w_set(p_)) {  // measured +5-15% (profiles/r04_ksw_bench.txt)
+            const char* e = std::getenv("FHE_HIP_KS32");
+            ks32w_ = !(e && std::string(e) == "0");
         }
         if (method == M_LMKCDEY) {  // op lists (k_prep_lmk_w) for k_blind_rotate_wide_ops
             if (p_.n > 2048 || (p_.numAutoKeys + 1) > 0x7fff) throw std::invalid_argument("device path: LMKCDEY n <= 2048");

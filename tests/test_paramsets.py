@@ -169,19 +169,17 @@ def test_gpu_digitsg4_multi_input_gates_vs_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["std256q", "std256q_lmkcdey", "std256q_3_lmkcdey", "std256q_4_lmkcdey"])
+@pytest.mark.parametrize("name", ["std256q", "std256q_lmkcdey", "std256q_3_lmkcdey"])
 def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
     """N = 2048, Q < 2^27, digitsG = 4: K1w, the register-resident two-waves-per-gate accumulators
-    (STD256Q, q = 1024: launch_blind_rotate_n2k; STD256Q_LMKCDEY (28-bit Q) / STD256Q_3_LMKCDEY /
-    STD256Q_4_LMKCDEY: launch_blind_rotate_lmk2k with 2 / 3 / 4 retained digits; the default),
+    (STD256Q, q = 1024: launch_blind_rotate_n2k; STD256Q_LMKCDEY (28-bit Q) / STD256Q_3_LMKCDEY:
+    launch_blind_rotate_lmk2k with 2 / 3 retained digits; the default),
     against the one-gate-per-workgroup accumulator the sets ran on before (FHE_HIP_N2K=0,
     bootstrap_wide.hip A32) on 333 gates of every 2-input type (final and extended outputs) and on the seam's
     BlindRotate (random accumulators, ciphertexts mod q for GINX and mod 2N for LMKCDEY, as EvalAcc reads
     them); the gates also decrypt to the truth table.  The reference goldens of the sets run in
     test_gpu_wider_paramset_gates_bit_exact_vs_reference on the default kernel."""
     from fhe_amd import binfhe as bf
-    if name in ("std256q_lmkcdey", "std256q_4_lmkcdey"):   # the digitsG = 3 / 5 rows (FHE_HIP_N2K_EXT)
-        monkeypatch.setenv("FHE_HIP_N2K_EXT", "1")
     ps, m = WIDER_SETS[name]
     assert bf.kernel_path(ps, m) == 4
     keys = bf.keygen(ps, m, 41)
