@@ -118,6 +118,9 @@ constexpr uint32_t kKsWideBatch = FHE_KS_WIDE_BATCH;  // from here: G 512, IPR 2
 constexpr int kKsSplitG = 512;
 #ifndef FHE_KS_XCD
 #define FHE_KS_XCD 0
+#endif
+#ifndef FHE_KS_GPT
+#define FHE_KS_GPT 1  // gates per thread of the 512-thread tiles (1: 512-gate tiles)
 #endif            // the row split's gate tile
 // LOGB = log2(baseKS): 5 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 6 (STD128_3/4,
 // LPF_STD128Q, STD256Q_3_LMKCDEY: 64 slices, 2 values of i per round so that the double buffer keeps the
@@ -141,7 +144,9 @@ template <int LOGB, int IPR, int KD = 3, bool W32 = false> struct KsShape {
 // (mod 2^16 per column, as the sums themselves) and applies the epilogue.  Below 4096 gates the
 // 256-gate tiles alone leave the chip idle; split S ways they fill it while every KSK slice is still
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
-template <int G, bool SPLIT, int LOGB, int IPR, int KD = 3, bool W32 = false>
+// GPT: gates per thread (u16 rows, no row split): a workgroup's tile is G GPT gates, so every staged KSK
+// slice serves GPT times as many gates (KSK traffic / GPT); thread t owns gates t, t + G, ...
+template <int G, bool SPLIT, int LOGB, int IPR, int KD = 3, bool W32 = false, int GPT = 1>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const void* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
@@ -151,6 +156,7 @@ __global__ void __launch_bounds__(G)
     constexpr int kKsParts = S_::parts, kKsStep = S_::step, kIPR = S_::ipr, kBase = S_::base;
     constexpr int kRowB = S_::rowb, kPps = S_::pps, kEB = S_::eb;
     constexpr int kAcc = W32 ? kKsCols : kKsCols / 2;  // u32 sums, or packed u16 pairs
+    static_assert(GPT == 1 || (!SPLIT && !W32 && FHE_KS_B64), "GPT > 1: the u16, single-pass form");
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
     __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][kBase * kRowB];
@@ -164,14 +170,20 @@ __global__ void __launch_bounds__(G)
         by = lin & 7u;
         bx = lin >> 3;
     }
-    const uint32_t gate = bx * G + t;
-    const bool valid = gate < g.count;
     const uint32_t col0 = by * kKsCols;
     const uint32_t rounds = SPLIT ? g.N / kIPR / gridDim.z : g.N / kIPR;  // this workgroup's share
     const uint32_t r0 = SPLIT ? blockIdx.z * rounds : 0;
     using AV = typename std::conditional<kIPR == 4, uint4, typename std::conditional<kIPR == 2, uint2, uint32_t>::type>::type;
     static_assert(kIPR == 4 || kIPR == 2 || kIPR == 1, "a_i vector width");
-    const AV* ga4 = reinterpret_cast<const AV*>(ms_a + (size_t)(valid ? gate : 0) * g.N) + r0;
+    uint32_t gates[GPT];
+    const AV* ga4[GPT];
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+        gates[u] = (bx * GPT + u) * G + t;
+        ga4[u]   = reinterpret_cast<const AV*>(ms_a + (size_t)(gates[u] < g.count ? gates[u] : 0) * g.N) + r0;
+    }
+    const uint32_t gate = gates[0];
+    const bool valid = gate < g.count;
 
     // staging role: part x = t + G*r -> slice x / kPps, 16-byte part x % kPps
     auto slice_src = [&](uint32_t round, int q, int r) -> const uint4* {
@@ -194,9 +206,12 @@ __global__ void __launch_bounds__(G)
         }
     };
 
-    uint32_t acc[kAcc];
+    uint32_t accs[GPT][kAcc];
 #pragma unroll
-    for (int k = 0; k < kAcc; ++k) acc[k] = 0;
+    for (int u = 0; u < GPT; ++u)
+#pragma unroll
+        for (int k = 0; k < kAcc; ++k) accs[u][k] = 0;
+    uint32_t (&acc)[kAcc] = accs[0];
 
     uint4 st[kKsStep][P];
     // threads past kKsParts (narrow column tiles) stage nothing: their slice index would run past
@@ -207,7 +222,13 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
         for (int r = 0; r < P; ++r)
             if (stager) st[q][r] = *slice_src(0, q, r);
-    AV a0 = ga4[0], a1 = ga4[rounds > 1 ? 1 : 0], a2 = ga4[rounds > 2 ? 2 : 0];
+    AV a0[GPT], a1[GPT], a2[GPT];
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+        a0[u] = ga4[u][0];
+        a1[u] = ga4[u][rounds > 1 ? 1 : 0];
+        a2[u] = ga4[u][rounds > 2 ? 2 : 0];
+    }
 
     // one barrier per round: buffer buf is rewritten two rounds later, after every thread
     // has passed the next round's barrier (and so finished consuming it)
@@ -225,11 +246,37 @@ __global__ void __launch_bounds__(G)
                 for (int r = 0; r < P; ++r)
                     if (stager) st[q][r] = *slice_src(rd + 1, q, r);
         }
-        const AV av = a0;
-        a0 = a1;
-        a1 = a2;
-        if (rd + 3 < rounds) a2 = ga4[rd + 3];
-        const uint32_t* as = reinterpret_cast<const uint32_t*>(&av);
+        AV avs[GPT];
+#pragma unroll
+        for (int u = 0; u < GPT; ++u) {
+            avs[u] = a0[u];
+            a0[u]  = a1[u];
+            a1[u]  = a2[u];
+            if (rd + 3 < rounds) a2[u] = ga4[u][rd + 3];
+        }
+        if (GPT > 1) {
+#pragma unroll
+            for (int q = 0; q < kKsStep; ++q)
+#pragma unroll
+                for (int u = 0; u < GPT; ++u) {
+                    const uint32_t* as = reinterpret_cast<const uint32_t*>(&avs[u]);
+                    const uint32_t dig = (as[q / kKsDigits] >> (LOGB * (q % kKsDigits))) & (kBase - 1);
+                    const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kRowB);
+                    uint2 w[kKsCols / 4];
+#pragma unroll
+                    for (int k = 0; k < kKsCols / 4; ++k) {
+                        w[k] = src[k];
+                        asm volatile("" ::: "memory");
+                    }
+#pragma unroll
+                    for (int k = 0; k < kKsCols / 4; ++k) {
+                        accs[u][2 * k + 0] = pk_sub_u16(accs[u][2 * k + 0], w[k].x);
+                        accs[u][2 * k + 1] = pk_sub_u16(accs[u][2 * k + 1], w[k].y);
+                    }
+                }
+            continue;
+        }
+        const uint32_t* as = reinterpret_cast<const uint32_t*>(&avs[0]);
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q) {
             const uint32_t dig = (as[q / kKsDigits] >> (LOGB * (q % kKsDigits))) & (kBase - 1);
@@ -273,6 +320,28 @@ __global__ void __launch_bounds__(G)
                 }
             }
         }
+    }
+    if (GPT > 1) {
+        const uint32_t qm = g.qKS - 1;
+#pragma unroll
+        for (int u = 0; u < GPT; ++u) {
+            if (gates[u] >= g.count) continue;
+            const uint32_t b = ms_b[gates[u]];
+            uint64_t* oa = a_out + (size_t)gates[u] * g.n;
+#pragma unroll
+            for (int k = 0; k < kKsCols / 2; ++k) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t c = col0 + 2 * k + h;
+                    const uint32_t neg = h ? (accs[u][k] >> 16) : (accs[u][k] & 0xffffu);
+                    uint64_t v = ((c == g.n ? b : 0u) + neg) & qm;
+                    if (q_out) v = mod_switch_up(v, g.qKS, q_out);
+                    if (c < g.n) oa[c] = v;
+                    else if (c == g.n) b_out[gates[u]] = v;
+                }
+            }
+        }
+        return;
     }
     if (!valid) return;
     if (SPLIT) {  // partial rows of ksk_width / 2 packed pairs, or ksk_width u32 sums (W32)
@@ -396,7 +465,11 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
             if (S > 1) FHE_KS_LAUNCH(256, true, 4, 2, 4); else FHE_KS_LAUNCH(256, false, 4, 2, 4);
         } else if (logBase == 5) {
             if (S > 1) FHE_KS_LAUNCH(kKsSplitG, true, 5, 4);
-            else if (G == 512) FHE_KS_LAUNCH(512, false, 5, 2);
+            else if (G == 512 && FHE_KS_GPT > 1) {  // GPT gates per thread: grid over G GPT-gate tiles
+                const dim3 gg((g.count + 512 * FHE_KS_GPT - 1) / (512 * FHE_KS_GPT), W / kKsCols, 1);
+                hipLaunchKernelGGL((k_keyswitch_tiled<512, false, 5, 2, 3, false, FHE_KS_GPT>), gg, dim3(512), 0, s, g,
+                                   ksk, ms_a, ms_b, q_out, a_out, b_out, nullptr);
+            } else if (G == 512) FHE_KS_LAUNCH(512, false, 5, 2);
             else FHE_KS_LAUNCH(256, false, 5, 4);
         } else {
             if (S > 1) FHE_KS_LAUNCH(256, true, 6, 2); else FHE_KS_LAUNCH(256, false, 6, 2);

@@ -3,6 +3,6 @@
 # context-owned seam scratch)
 set -o pipefail
 export FHE_SEGV_TRACE=1
-timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/r04_gpu_tests_a.txt 2>&1; rc=$?
-grep -E "FAILED|passed|failed|error" gpurun_out/r04_gpu_tests_a.txt | tail -5
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/r04_gpu_tests_b.txt 2>&1; rc=$?
+grep -E "FAILED|passed|failed|error" gpurun_out/r04_gpu_tests_b.txt | tail -5
 exit $rc
