@@ -2081,32 +2081,48 @@ FHE_DEV int wa2k(int L) { return L; }
 FHE_DEV int wb2k(int L) { return 66 * (L >> 1) + (L & 1); }
 FHE_DEV int wc2k(int L) { return 2 * L + 2 * (L >> 5); }
 
-// RED (2^27 <= Q < 2^28, 8Q of signed headroom): one signed Montgomery product by 2^32 mod Q after the
-// five A stages (|v| < 5Q + 2^(g-1) -> < 0.82 Q), so the six stages after it end below 6.82 Q
-template <int NP, bool RED = false>
+// QM, the modulus class: 0: Q < 2^27 (16Q of signed headroom), no reduction; 1: Q < 2^28 (8Q): one signed
+// Montgomery product by 2^32 mod Q after the five A stages (|v| < 5Q + 2^(g-1) -> < 0.82 Q), the six
+// stages after it end below 6.82 Q; 2: Q < 2^29 (4Q): one after stages 3, 6 and 9 (< 3Q + 2^(g-1) ->
+// < 0.875 Q, < 3.875 Q -> < 0.98 Q, < 3.98 Q -> < Q), the last two end below 3 Q
+template <int NP>
+FHE_DEV void red_2k(uint32_t (&v)[NP][32], const Mod& m) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[p][r] = smont_mul(v[p][r], m.oneR, m);
+}
+
+// one radix-2 stage over the 32 registers: A stages (b = 10..6) pair register bits b - 6 with the twiddles
+// of twA; B stages (b = 5..1) pair register bits b - 1 with s_tab's, indexed by the lane pair G
+template <int NP, bool B>
+FHE_DEV void fwd_2k_stage(uint32_t (&v)[NP][32], int b, int G, const uint32_t* __restrict__ tw, const Mod& m) {
+    const int rb = B ? b - 1 : b - 6;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        if (r & (1 << rb)) continue;
+        const uint32_t w = B ? tw[(1 << (10 - b)) + (G << (5 - b)) + (r >> b)] : tw[(1 << (10 - b)) + (r >> (rb + 1))];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
+    }
+}
+
+template <int NP, int QM = 0>
 FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t* __restrict__ twA,
                       const uint32_t* s_tab, const Mod& m) {
+    // the stages are written out: a loop over them with the reductions inside was left rolled for NP = 3,
+    // and a plain one for NP = 4 (the digit array in scratch)
     const int G = L >> 1;
     uint32_t* ta = t + wa2k(L);
     uint32_t* tb = t + wb2k(L);
     uint32_t* tc = t + wc2k(L);
-#pragma unroll
-    for (int b = 10; b >= 6; --b) {
-        const int rb = b - 6;
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            if (r & (1 << rb)) continue;
-            const uint32_t w = twA[(1 << (10 - b)) + (r >> (rb + 1))];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
-        }
-    }
-    if (RED) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-#pragma unroll
-            for (int r = 0; r < 32; ++r) v[p][r] = smont_mul(v[p][r], m.oneR, m);
-    }
+    fwd_2k_stage<NP, false>(v, 10, G, twA, m);
+    fwd_2k_stage<NP, false>(v, 9, G, twA, m);
+    fwd_2k_stage<NP, false>(v, 8, G, twA, m);
+    if (QM == 2) red_2k<NP>(v, m);  // after stage 3
+    fwd_2k_stage<NP, false>(v, 7, G, twA, m);
+    fwd_2k_stage<NP, false>(v, 6, G, twA, m);
+    if (QM == 1) red_2k<NP>(v, m);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {  // A -> B
 #pragma unroll
@@ -2116,17 +2132,13 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
         for (int r = 0; r < 32; ++r) v[p][r] = tb[2 * r];
         wave_lds_sync();
     }
-#pragma unroll
-    for (int b = 5; b >= 1; --b) {
-        const int rb = b - 1;
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            if (r & (1 << rb)) continue;
-            const uint32_t w = s_tab[(1 << (10 - b)) + (G << (5 - b)) + (r >> b)];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
-        }
-    }
+    fwd_2k_stage<NP, true>(v, 5, G, s_tab, m);
+    if (QM == 2) red_2k<NP>(v, m);  // after stage 6
+    fwd_2k_stage<NP, true>(v, 4, G, s_tab, m);
+    fwd_2k_stage<NP, true>(v, 3, G, s_tab, m);
+    fwd_2k_stage<NP, true>(v, 2, G, s_tab, m);
+    if (QM == 2) red_2k<NP>(v, m);  // after stage 9
+    fwd_2k_stage<NP, true>(v, 1, G, s_tab, m);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {  // B -> C
 #pragma unroll
@@ -2477,7 +2489,8 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
 namespace {
 // |acc| between ops, units of Q/10: 2 (ND (11 Q + 2^(g-1)) Q 2^-32 + Q/2) for Q < 2^27; Q28 (ND = 2,
 // 2^27 <= Q < 2^28, the forward transform reduced once): 2 (2 (6.82 Q) Q 2^-32 + Q/2) < 2.8 Q
-template <int ND, bool Q28> constexpr int kL2AccBound = Q28 ? 28 : 33;
+// QM 2 (Q < 2^29, digits below 3 Q after the forward transform): 2 (ND 3 Q Q 2^-32 + Q/2) -> 33 (ND 3)
+template <int ND, int QM> constexpr int kL2AccBound = QM == 1 ? (ND == 3 ? 36 : 28) : QM == 2 ? (ND == 3 ? 33 : 25) : 33;
 constexpr size_t l2k_lds() { return (size_t)(2048 + 2048 + 2 * kW2Tile) * 4; }
 
 // EVAL automorphism X -> X^k on layout C through this wave's tile (as automorphism_c at N = 1024):
@@ -2536,14 +2549,14 @@ FHE_DEV void mac_2k(uint32_t (&acc)[32], const uint32_t (&d)[ND][32], const uint
 }
 }  // namespace
 
-template <int ND, bool ACCIO, bool Q28 = false>
+template <int ND, bool ACCIO, int QM = 0>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_blind_rotate_lmk2k(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
                          const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
                          const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                          const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
     constexpr int kQ = 2 * ND;
-    constexpr int BIN = kL2AccBound<ND, Q28>, LIM = Q28 ? 80 : 160;
+    constexpr int BIN = kL2AccBound<ND, QM>, LIM = QM == 2 ? 40 : QM == 1 ? 80 : 160;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 2048;
@@ -2584,7 +2597,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             }
             tv[0][r] = v;
         }
-        fwd_2k_s<1, Q28>(tv, tile, L, twAf, s_tab, m);
+        fwd_2k_s<1, QM>(tv, tile, L, twAf, s_tab, m);
 #pragma unroll
         for (int r = 0; r < 32; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
         automorphism_2k(acc, tile, L, M - 5);
@@ -2603,45 +2616,41 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
         const uint32_t* twI = twAi;
         asm volatile("" : "+s"(twF), "+s"(twI));
         __syncthreads();  // the partner has read this wave's tile (previous op)
-        uint32_t d[ND][32];
-        if (!(op & 0x8000u)) {
-            // ---- AddToAccLMKCDEY: acc_c <- sum over both components' digits of D ek[op][row][c]
-#pragma unroll
-            for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-            inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
-#pragma unroll
-            for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
-            fwd_2k_s<ND, Q28>(d, tile, L, twF, s_tab, m);
-            mac_2k<ND>(acc, d, ek + ((size_t)op * 2 + c) * (kQ * 8 * 64) + L, tile, L, m);
-            __syncthreads();  // both waves' partner words are in LDS
-#pragma unroll
-            for (int r = 0; r < 32; ++r) acc[r] += partner[(r << 6) | L];
-        } else {
-            // ---- Automorphism(5^t or 2N - 5, ak[t])
-            const uint32_t t = op & 0x7fffu;
+        // ---- AddToAccLMKCDEY (op < 0x8000): acc_c <- sum over both components' digits of D ek[op][row][c];
+        // ---- Automorphism(5^t or 2N - 5, ak[t]) (op = 0x8000 | t): acc0' -> COEF -> digits -> EVAL,
+        // acc0 replaced, acc1's share to the tile.  One copy of the digit path serves both (the two copies
+        // put the digit array of the 3-digit, 29-bit form in scratch)
+        const bool isauto = op & 0x8000u;
+        const uint32_t t  = op & 0x7fffu;
+        if (isauto) {
             uint32_t kexp = M - 5;
             if (t) {
                 kexp = 1;
                 for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5u) & (M - 1);
             }
             automorphism_2k(acc, tile, L, kexp);
-            if (c == 0) {  // acc0' -> COEF -> 3 digits -> EVAL; acc0 replaced, acc1's share to the tile
+        }
+        if (!isauto || c == 0) {
+            uint32_t d[ND][32];
 #pragma unroll
-                for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-                inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+            for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
+            inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
-                for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
-                fwd_2k_s<ND, Q28>(d, tile, L, twF, s_tab, m);
-                mac_2k<ND>(acc, d, ak + (size_t)t * (kQ * 8 * 64) + L, tile, L, m);
-            }
-            __syncthreads();  // wave 0's share of acc1 is in its tile
-            if (c == 1) {
+            for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+            fwd_2k_s<ND, QM>(d, tile, L, twF, s_tab, m);
+            const uint4* key = isauto ? ak + (size_t)t * (kQ * 8 * 64) : ek + ((size_t)op * 2 + c) * (kQ * 8 * 64);
+            mac_2k<ND>(acc, d, key + L, tile, L, m);
+        }
+        __syncthreads();  // the partner words (AddToAcc: both waves'; Automorphism: wave 0's share of acc1)
+        if (!isauto) {
 #pragma unroll
-                for (int r = 0; r < 32; ++r) {
-                    const int64_t S = (int64_t)(int32_t)acc[r] * (int32_t)m.oneR +
-                                      (int64_t)(int32_t)partner[(r << 6) | L] * (int32_t)m.oneR;
-                    acc[r] = smont_red(S, m);
-                }
+            for (int r = 0; r < 32; ++r) acc[r] += partner[(r << 6) | L];
+        } else if (c == 1) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const int64_t S = (int64_t)(int32_t)acc[r] * (int32_t)m.oneR +
+                                  (int64_t)(int32_t)partner[(r << 6) | L] * (int32_t)m.oneR;
+                acc[r] = smont_red(S, m);
             }
         }
     }
@@ -2674,11 +2683,12 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 bool lmk2k_supported(const GateArgs& g, const BootTables& t, int nd) {
-    // 2 retained digits up to Q < 2^28 (the forward transform reduced once), 3 below 2^27.  (4 digits,
-    // STD256Q_4_LMKCDEY, compiled to a kernel with 10,853 scalar instructions and ran at 1.07K gates/s
-    // against 10.6K on K5: profiles/r04_ext_bench.txt; not instantiated.)
-    const bool qok = nd == 2 ? t.Q < (1u << 28) : t.Q < (1u << 27);
-    return qok && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && nd >= 2 && nd <= 3 &&
+    // 2 or 3 retained digits, Q < 2^29 (the forward transform reduced once at Q >= 2^27, three times at
+    // Q >= 2^28); 4 digits (STD256Q_4_LMKCDEY) at Q < 2^27.  (The 4-digit form first ran at 1.07K gates/s
+    // against 10.6K on K5, profiles/r04_ext_bench.txt: its digit array sat in scratch, the forward stage
+    // loop left rolled; the stages are now written out.)
+    const bool qok = nd == 4 ? t.Q < (1u << 27) : t.Q < (1u << 29);
+    return qok && g.N == 2048 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && nd >= 2 && nd <= 4 &&
            (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
@@ -2689,13 +2699,21 @@ hipError_t launch_blind_rotate_lmk2k(const GateArgs& g, const BootTables& t, con
     if (!lmk2k_supported(g, t, nd)) return hipErrorInvalidValue;
     const uint4* e = static_cast<const uint4*>(ek);
     const uint4* a = static_cast<const uint4*>(ak);
-#define FHE_L2K(ND_, IO, Q28_)                                                                                     \
-    hipLaunchKernelGGL((k_blind_rotate_lmk2k<ND_, IO, Q28_>), dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops, \
+#define FHE_L2K(ND_, IO, QM_)                                                                                      \
+    hipLaunchKernelGGL((k_blind_rotate_lmk2k<ND_, IO, QM_>), dim3(g.count), dim3(128), l2k_lds(), s, g, t, e, a, ops,  \
                        nops, maxops, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
+    const int qm = t.Q >= (1u << 28) ? 2 : t.Q >= (1u << 27) ? 1 : 0;  // the modulus class (fwd_2k_s)
     if (nd == 2) {  // STD256Q_LMKCDEY (28-bit Q)
-        if (t.Q >= (1u << 27)) { if (g.acc_io) FHE_L2K(2, true, true); else FHE_L2K(2, false, true); }
-        else { if (g.acc_io) FHE_L2K(2, true, false); else FHE_L2K(2, false, false); }
-    } else { if (g.acc_io) FHE_L2K(3, true, false); else FHE_L2K(3, false, false); }
+        if (qm == 1) { if (g.acc_io) FHE_L2K(2, true, 1); else FHE_L2K(2, false, 1); }
+        else if (qm == 2) { if (g.acc_io) FHE_L2K(2, true, 2); else FHE_L2K(2, false, 2); }
+        else { if (g.acc_io) FHE_L2K(2, true, 0); else FHE_L2K(2, false, 0); }
+    } else if (nd == 4) {  // STD256Q_4_LMKCDEY (digitsG 5)
+        if (g.acc_io) FHE_L2K(4, true, 0); else FHE_L2K(4, false, 0);
+    } else {  // STD256Q_3_LMKCDEY (26-bit); STD256_3 / _4_LMKCDEY (29-bit)
+        if (qm == 0) { if (g.acc_io) FHE_L2K(3, true, 0); else FHE_L2K(3, false, 0); }
+        else if (qm == 1) { if (g.acc_io) FHE_L2K(3, true, 1); else FHE_L2K(3, false, 1); }
+        else { if (g.acc_io) FHE_L2K(3, true, 2); else FHE_L2K(3, false, 2); }
+    }
 #undef FHE_L2K
     return hipGetLastError();
 }

@@ -52,8 +52,11 @@ bool Engine::n2k_set(const Params& p) {
     // (profiles/r04_ext_bench.txt); FHE_HIP_N2K_EXT=0 keeps it on K5
     const char* ext = std::getenv("FHE_HIP_N2K_EXT");
     const bool wide_rows = ext ? std::string(ext) == "1" : kN2kExtended;
-    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || (wide_rows && p.digitsG == 3));
-    const uint64_t qmax = p.digitsG == 3 ? (1ull << 28) : (1ull << 27);  // digitsG 3: 2 digits, 8Q plan
+    const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || (wide_rows && (p.digitsG == 3 || p.digitsG == 5)));
+    if (lmk && p.Q >= (1ull << 27) && (!wide_rows || p.digitsG == 5)) return false;  // reduced forward: 2-3 digits
+    // LMKCDEY: Q < 2^29 (the forward transform reduced once at Q >= 2^27, three times at Q >= 2^28: the
+    // 29-bit STD256_3 / STD256_4_LMKCDEY); GINX: Q < 2^27
+    const uint64_t qmax = p.method == M_LMKCDEY ? (1ull << 29) : (1ull << 27);
     if (is_large(p.paramset) || p.timeopt || !(ginx || lmk) || p.N != 2048 || p.Q >= qmax || g < 2 ||
         (uint64_t)p.digitsG * g > 32)
         return false;

@@ -169,11 +169,13 @@ def test_gpu_digitsg4_multi_input_gates_vs_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["std256q", "std256q_lmkcdey", "std256q_3_lmkcdey"])
+@pytest.mark.parametrize("name", ["std256q", "std256q_lmkcdey", "std256q_3_lmkcdey", "std256_3_lmkcdey",
+                                  "std256_4_lmkcdey", "std256q_4_lmkcdey"])
 def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
     """N = 2048, Q < 2^27, digitsG = 4: K1w, the register-resident two-waves-per-gate accumulators
     (STD256Q, q = 1024: launch_blind_rotate_n2k; STD256Q_LMKCDEY (28-bit Q) / STD256Q_3_LMKCDEY:
-    launch_blind_rotate_lmk2k with 2 / 3 retained digits; the default),
+    launch_blind_rotate_lmk2k with 2 / 3 retained digits; STD256_3 / STD256_4_LMKCDEY: 29-bit Q, the forward
+    transform reduced after stages 3, 6 and 9; the default),
     against the one-gate-per-workgroup accumulator the sets ran on before (FHE_HIP_N2K=0,
     bootstrap_wide.hip A32) on 333 gates of every 2-input type (final and extended outputs) and on the seam's
     BlindRotate (random accumulators, ciphertexts mod q for GINX and mod 2N for LMKCDEY, as EvalAcc reads
