@@ -135,8 +135,8 @@ __host__ __device__ constexpr uint32_t g2_key_word(uint32_t nd, uint32_t c, uint
 // with 2048-word tabF / tabI and the 2113-pair half monomial table), u64 ctExt into the 64-bit path's
 // workspace
 hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const void* keys, const uint16_t* idx,
-                                   const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
-bool n2k_supported(const GateArgs& g, const BootTables& t);
+                                   const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, int nd, hipStream_t s);
+bool n2k_supported(const GateArgs& g, const BootTables& t, int nd);
 // K1w for LMKCDEY (k_blind_rotate_lmk2k<nd>): N = 2048, Q < 2^27, digitsG = nd + 1 = 4 or 5
 // (STD256Q_3_LMKCDEY, STD256Q_4_LMKCDEY); op lists of launch_prep_lmk, keys in Engine::pack_n2k's
 // LMKCDEY layout (ek per index, then ak per automorphism key), tables as launch_blind_rotate_n2k

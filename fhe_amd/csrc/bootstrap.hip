@@ -2107,7 +2107,23 @@ FHE_DEV void fwd_2k_stage(uint32_t (&v)[NP][32], int b, int G, const uint32_t* _
     }
 }
 
-template <int NP, int QM = 0>
+// v - rint(v / Q) Q in 32-bit registers (|v| < 2^31): the float quotient is off by under 2^-20, so the
+// result is below 0.51 Q; no 64-bit temporaries (FRED: K1w GINX, whose 3-digit form spilled 104 VGPRs with
+// smont_mul's and 30 with this; K1w-LMKCDEY keeps red_2k, measured 6% faster there)
+template <int NP>
+FHE_DEV void red_2k_f(uint32_t (&v)[NP][32], const Mod& m) {
+    const float iq = 1.0f / (float)m.Q;
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const int32_t x = (int32_t)v[p][r];
+            const int32_t q = (int32_t)__builtin_rintf((float)x * iq);
+            v[p][r]         = (uint32_t)(x - q * (int32_t)m.Q);
+        }
+}
+
+template <int NP, int QM = 0, bool FRED = false>
 FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t* __restrict__ twA,
                       const uint32_t* s_tab, const Mod& m) {
     // the stages are written out: a loop over them with the reductions inside was left rolled for NP = 3,
@@ -2119,7 +2135,7 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
     fwd_2k_stage<NP, false>(v, 10, G, twA, m);
     fwd_2k_stage<NP, false>(v, 9, G, twA, m);
     fwd_2k_stage<NP, false>(v, 8, G, twA, m);
-    if (QM == 2) red_2k<NP>(v, m);  // after stage 3
+    if (QM == 2) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 3
     fwd_2k_stage<NP, false>(v, 7, G, twA, m);
     fwd_2k_stage<NP, false>(v, 6, G, twA, m);
     if (QM == 1) red_2k<NP>(v, m);
@@ -2133,11 +2149,11 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
         wave_lds_sync();
     }
     fwd_2k_stage<NP, true>(v, 5, G, s_tab, m);
-    if (QM == 2) red_2k<NP>(v, m);  // after stage 6
+    if (QM == 2) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 6
     fwd_2k_stage<NP, true>(v, 4, G, s_tab, m);
     fwd_2k_stage<NP, true>(v, 3, G, s_tab, m);
     fwd_2k_stage<NP, true>(v, 2, G, s_tab, m);
-    if (QM == 2) red_2k<NP>(v, m);  // after stage 9
+    if (QM == 2) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 9
     fwd_2k_stage<NP, true>(v, 1, G, s_tab, m);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {  // B -> C
@@ -2274,12 +2290,18 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
 }
 }  // namespace
 
-template <int ND, bool ACCIO>
+// QM 2 (2^27 <= Q < 2^29, STD256 / STD256_3 with q = 2048): the forward transform reduced three times
+// (fwd_2k_s), the monomial pairs centred to (-Q/2, Q/2] and the product's low word taken signed, so that
+// |acc| < 2.6 Q (own wave: |lo mp.x| 2^-32 < Q/4 per column, |hi mp.y| 2^-32 < 3 ND Q^3 2^-65 < 0.07 Q,
+// |acc oneR| 2^-32 < A/8, + Q/2; the partner's share without the acc term) fits the 4 Q plan
+template <int ND, int QM> constexpr int kW2Bound = QM == 2 ? 27 : kW2AccBound;
+template <int ND, bool ACCIO, int QM = 0>
 __global__ void __launch_bounds__(128 * kW2Gates, 2)
     k_blind_rotate_n2k(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                        const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
     constexpr int kQ = 2 * ND;  // key vectors per slot pair: ND digit rows x 2 columns
+    constexpr int BIN = kW2Bound<ND, QM>, LIM = QM == 2 ? 40 : 160;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 2048;
@@ -2289,7 +2311,14 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
         s_tab[i]  = T.tabF[i];
         s_tabI[i] = T.tabI[i];
     }
-    for (int i = threadIdx.x; i < kW2Mono; i += blockDim.x) s_mono2[i] = make_uint2(T.monoP[i], T.mono[i]);
+    for (int i = threadIdx.x; i < kW2Mono; i += blockDim.x) {
+        uint32_t mx = T.monoP[i], my = T.mono[i];
+        if (QM == 2) {  // centred: (-Q/2, Q/2]
+            mx = mx > T.Q / 2 ? mx - T.Q : mx;
+            my = my > T.Q / 2 ? my - T.Q : my;
+        }
+        s_mono2[i] = make_uint2(mx, my);
+    }
 
     const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
     const int c = wave & 1;  // RLWE component of this wave
@@ -2321,7 +2350,7 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
             }
             tv[0][r] = v;
         }
-        fwd_2k_s<1>(tv, tile, L, twAf, s_tab, m);
+        fwd_2k_s<1, QM, true>(tv, tile, L, twAf, s_tab, m);
 #pragma unroll
         for (int r = 0; r < 32; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
     } else {
@@ -2359,10 +2388,10 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
         uint32_t d[ND][32];
 #pragma unroll
         for (int r = 0; r < 32; ++r) d[0][r] = acc[r];
-        inv_2k_s<kW2AccBound>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
+        inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
         for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
-        fwd_2k_s<ND>(d, tile, L, twF, s_tab, m);
+        fwd_2k_s<ND, QM, true>(d, tile, L, twF, s_tab, m);
         const uint32_t fl = (as * lmul) & 2047u;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) kq[0][q] = kb[(q * 16 + 0) * 64];
@@ -2393,8 +2422,16 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
                         S1 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.y : kv.x);
                         S2 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.w : kv.z);
                     }
-                    int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
-                    S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
+                    int64_t S;
+                    if (QM == 2) {  // S1 = hi 2^32 + lo with lo signed
+                        const int32_t l1 = (int32_t)S1, l2 = (int32_t)S2;
+                        const int32_t h1 = (int32_t)((S1 - l1) >> 32), h2 = (int32_t)((S2 - l2) >> 32);
+                        S = (int64_t)l1 * (int32_t)mp.x + (int64_t)h1 * (int32_t)mp.y;
+                        S += (int64_t)l2 * (int32_t)mn.x + (int64_t)h2 * (int32_t)mn.y;
+                    } else {
+                        S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
+                        S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
+                    }
                     if (o == 0) {
                         S += (int64_t)(int32_t)acc[r] * (int32_t)T.oneR;
                         acc[r] = smont_red(S, m);
@@ -2423,7 +2460,7 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
     // extraction (binfhe-base-scheme.cpp:110-121): canonical COEF in layout A; wave 0 writes the
     // transposed acc0 (coefficient k -> position N - k, negated), wave 1 the b term from acc1[0]
     __syncthreads();  // the partner has read this wave's tile
-    inv_2k_s<kW2AccBound>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
+    inv_2k_s<BIN, LIM>(acc, tile, L, twAi, s_tabI, T.w1R, m.oneR, m);
     if (!live) return;
     if (c == 0) {
         uint64_t* oa = ext_a + (size_t)gate * g.N;
@@ -2440,30 +2477,40 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
     }
 }
 
-bool n2k_supported(const GateArgs& g, const BootTables& t) {
-    return t.Q < (1u << 27) && g.N == 2048 && g.ctmod < 2 * g.N && g.tv == nullptr && g.tv64 == nullptr &&
-           g.gbits >= 2 && 4 * g.gbits <= 32;
+bool n2k_supported(const GateArgs& g, const BootTables& t, int nd) {
+    // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29
+    return t.Q < (1u << 29) && (nd == 3 || (nd == 2 && t.Q >= (1u << 27))) && g.N == 2048 && g.ctmod < 2 * g.N &&
+           g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
 hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const void* keys, const uint16_t* idx,
-                                   const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, hipStream_t s) {
+                                   const uint32_t* tvb, uint64_t* ext_a, uint64_t* ext_b, int nd, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if (!n2k_supported(g, t)) return hipErrorInvalidValue;
+    if (!n2k_supported(g, t, nd)) return hipErrorInvalidValue;
     static const bool attr = [] {
         for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false>),
-                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true>)})
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false, 2>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true, 2>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, false, 2>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, true, 2>)})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)w2_lds());
         return true;
     }();
     (void)attr;
     const uint32_t blocks = (g.count + kW2Gates - 1) / kW2Gates;
     const uint4* k = static_cast<const uint4*>(keys);
-    if (g.acc_io)
-        hipLaunchKernelGGL((k_blind_rotate_n2k<3, true>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), s, g, t, k,
-                           idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
-    else
-        hipLaunchKernelGGL((k_blind_rotate_n2k<3, false>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), s, g, t, k,
-                           idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv);
+#define FHE_N2K(ND_, IO, QM_)                                                                                      \
+    hipLaunchKernelGGL((k_blind_rotate_n2k<ND_, IO, QM_>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), s, g, t, k, \
+                       idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
+    if (t.Q < (1u << 27)) {  // STD256Q
+        if (g.acc_io) FHE_N2K(3, true, 0); else FHE_N2K(3, false, 0);
+    } else if (nd == 3) {  // STD256_3 (29-bit Q)
+        if (g.acc_io) FHE_N2K(3, true, 2); else FHE_N2K(3, false, 2);
+    } else {  // STD256 (29-bit Q, digitsG 3)
+        if (g.acc_io) FHE_N2K(2, true, 2); else FHE_N2K(2, false, 2);
+    }
+#undef FHE_N2K
     return hipGetLastError();
 }
 

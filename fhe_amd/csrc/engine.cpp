@@ -47,7 +47,10 @@ bool Engine::n2k_set(const Params& p) {
     // any q with digitsG = 4 or 5 (3 or 4 retained digits); the digit fields of d + C in 32 bits
     // (digitsG = 3, two retained digits: Q < 2^28, the forward transform reduced once -- STD256Q_LMKCDEY)
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
-    const bool ginx = p.method == M_GINX && p.q < 2 * p.N && p.digitsG == 4;
+    // GINX: digitsG 4 at Q < 2^27 (STD256Q); digitsG 3 / 4 at 2^27 <= Q < 2^29 (STD256, STD256_3: the
+    // forward transform reduced three times, FHE_HIP_N2K_EXT)
+    const bool ginx = p.method == M_GINX && p.q < 2 * p.N &&
+                      (p.digitsG == 4 || (p.digitsG == 3 && p.Q >= (1ull << 27)));
     // digitsG 3 with 2^27 <= Q < 2^28 (STD256Q_LMKCDEY) measured 24.0K -> 32.7K gates/s
     // (profiles/r04_ext_bench.txt); FHE_HIP_N2K_EXT=0 keeps it on K5
     const char* ext = std::getenv("FHE_HIP_N2K_EXT");
@@ -56,7 +59,7 @@ bool Engine::n2k_set(const Params& p) {
     if (lmk && p.Q >= (1ull << 27) && (!wide_rows || p.digitsG == 5)) return false;  // reduced forward: 2-3 digits
     // LMKCDEY: Q < 2^29 (the forward transform reduced once at Q >= 2^27, three times at Q >= 2^28: the
     // 29-bit STD256_3 / STD256_4_LMKCDEY); GINX: Q < 2^27
-    const uint64_t qmax = p.method == M_LMKCDEY ? (1ull << 29) : (1ull << 27);
+    const uint64_t qmax = wide_rows ? (1ull << 29) : (1ull << 27);
     if (is_large(p.paramset) || p.timeopt || !(ginx || lmk) || p.N != 2048 || p.Q >= qmax || g < 2 ||
         (uint64_t)p.digitsG * g > 32)
         return false;
@@ -167,12 +170,13 @@ void Engine::pack_n2k(const uint64_t* bsk) {
         FHE_HIP_CHECK(hipMemcpy(d_bsk2_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
         return;
     }
-    const size_t per = (size_t)2 * 6 * 16 * 64 * 4;
+    const uint32_t kq = 2 * (p_.digitsG - 1);  // retained digits x 2 columns
+    const size_t per = (size_t)2 * kq * 16 * 64 * 4;
     std::vector<uint32_t> dev((size_t)n * per);
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < (int64_t)n; ++i)
         for (uint32_t c = 0; c < 2; ++c)
-            for (uint32_t q = 0; q < 6; ++q)
+            for (uint32_t q = 0; q < kq; ++q)
                 for (uint32_t k2 = 0; k2 < 16; ++k2)
                     for (uint32_t L = 0; L < 64; ++L)
                         for (uint32_t e4 = 0; e4 < 4; ++e4) {
@@ -180,7 +184,7 @@ void Engine::pack_n2k(const uint64_t* bsk) {
                             const uint32_t x = ((r >> 1) << 7) | (L << 1) | (r & 1);
                             const uint32_t row = 2 * (q >> 1) + c, col = (q & 1) ? 1 - c : c;
                             const size_t src = ((((size_t)i * 2 + ks) * dG2 + row) * 2 + col) * N + x;
-                            dev[(size_t)i * per + ((((c * 6 + q) * 16 + k2) * 64 + L) * 4 + e4)] =
+                            dev[(size_t)i * per + ((((c * kq + q) * 16 + k2) * 64 + L) * 4 + e4)] =
                                 to_mont(mulmod(bsk[src] % Q, ninv, Q), Q);
                         }
     FHE_HIP_CHECK(hipSetDevice(device_));
@@ -864,9 +868,10 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
                                                        d_ops_, d_nops_, maxops_, d_tvb_, d_wext_a_, d_wext_b_, dm, s));
             return;
         }
-        if (n2k_ && d_bsk2_ && n2k_supported(g, tabs2k_) && g.lv == g.lv64 && g.uv == g.uv64 &&
+        if (n2k_ && d_bsk2_ && n2k_supported(g, tabs2k_, (int)p_.digitsG - 1) && g.lv == g.lv64 && g.uv == g.uv64 &&
             g.b_const == g.b64) {
-            FHE_HIP_CHECK(launch_blind_rotate_n2k(g, tabs2k_, d_bsk2_, d_idx_, d_tvb_, d_wext_a_, d_wext_b_, s));
+            FHE_HIP_CHECK(launch_blind_rotate_n2k(g, tabs2k_, d_bsk2_, d_idx_, d_tvb_, d_wext_a_, d_wext_b_,
+                                                  (int)p_.digitsG - 1, s));
             return;
         }
         if (g3_ && d_bsk2_ && ginx3_supported(g, tabs_) && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64) {
