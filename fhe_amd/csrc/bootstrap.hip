@@ -2294,14 +2294,18 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
 // (fwd_2k_s), the monomial pairs centred to (-Q/2, Q/2] and the product's low word taken signed, so that
 // |acc| < 2.6 Q (own wave: |lo mp.x| 2^-32 < Q/4 per column, |hi mp.y| 2^-32 < 3 ND Q^3 2^-65 < 0.07 Q,
 // |acc oneR| 2^-32 < A/8, + Q/2; the partner's share without the acc term) fits the 4 Q plan
-template <int ND, int QM> constexpr int kW2Bound = QM == 2 ? 27 : kW2AccBound;
-template <int ND, bool ACCIO, int QM = 0>
+// FULL (q = 2N, STD256_4: odd monomial exponents): the table holds psi^g - 1 for g in [0, 2048] and
+// psi^(g + 2048) - 1 = -(psi^g - 1) - 2 is formed on the fly, (-x - 2, -y - 2R) with 2R centred (|y'| < Q:
+// |acc| < 2.93 Q, bound 30)
+template <int ND, int QM, bool FULL> constexpr int kW2Bound = QM == 2 ? (FULL ? 30 : 27) : kW2AccBound;
+template <int ND, bool ACCIO, int QM = 0, bool FULL = false>
 __global__ void __launch_bounds__(128 * kW2Gates, 2)
     k_blind_rotate_n2k(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                        const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
     constexpr int kQ = 2 * ND;  // key vectors per slot pair: ND digit rows x 2 columns
-    constexpr int BIN = kW2Bound<ND, QM>, LIM = QM == 2 ? 40 : 160;
+    static_assert(!FULL || QM == 2, "the full-resolution monomials need the centred (QM 2) products");
+    constexpr int BIN = kW2Bound<ND, QM, FULL>, LIM = QM == 2 ? 40 : 160;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 2048;
@@ -2362,11 +2366,22 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
     const DecN dec       = make_decn(m.Q, g.gbits, ND);
     // monomial of slot x(L, r): e = m (2 brv11(x) + 1) mod 2N, m = a 2N / ctmod even, in half units
     // f = e / 2 = as (32 brv6(L) + 1) + as 2 brv4(r >> 1) mod 2048 (bit 0 of x adds as 2048 = 0)
+    // FULL: e = a (32 brv6(L) + 1) + a 2 brv4(r >> 1) + a 2048 (r & 1) mod 4096
     const uint32_t lmul = 32 * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1;
     const uint4* kc     = keys + (size_t)c * (kQ * 16 * 64) + L;
+    uint32_t two_r = 0;
+    if (FULL) {
+        two_r = 2 * T.oneR;
+        two_r = two_r >= T.Q ? two_r - T.Q : two_r;
+        two_r = two_r > T.Q / 2 ? two_r - T.Q : two_r;
+    }
+    // u or -u - (2, 2R) by a mask (0 or ~0): no control flow around the MAC
+    auto negp = [&](uint2 u, uint32_t sm) {
+        return make_uint2(((u.x ^ sm) - sm) - (2u & sm), ((u.y ^ sm) - sm) - (two_r & sm));
+    };
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m       = fresh_nq(m0);
-        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> 1;
+        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> (FULL ? 0 : 1);
         const uint4* kb   = kc + (size_t)i * (2 * kQ * 16 * 64);
         // the uniform twiddles re-read per index (hoisted, the 62 of them would sit in VGPRs across the loop)
         const uint32_t* twF = twAf;
@@ -2392,7 +2407,8 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
 #pragma unroll
         for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
         fwd_2k_s<ND, QM, true>(d, tile, L, twF, s_tab, m);
-        const uint32_t fl = (as * lmul) & 2047u;
+        constexpr uint32_t EM = FULL ? 4095u : 2047u;
+        const uint32_t fl = (as * lmul) & EM;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) kq[0][q] = kb[(q * 16 + 0) * 64];
 #pragma unroll
@@ -2406,13 +2422,27 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
             }
             asm volatile("" ::: "memory");
             const uint32_t ur = __builtin_amdgcn_readfirstlane(
-                (as * 2u * (__builtin_bitreverse32((uint32_t)k2) >> 28)) & 2047u);
-            const uint32_t f = (fl + ur) & 2047u, fn = 2048u - f;
-            const uint2 mp = s_mono2[f + (f >> 5)], mn = s_mono2[fn + (fn >> 5)];
+                (as * 2u * (__builtin_bitreverse32((uint32_t)k2) >> 28)) & EM);
+            uint2 mp, mn;
+            if (FULL) {
+                const uint32_t e0 = (fl + ur) & 4095u, en = (4096u - e0) & 4095u;
+                const uint32_t g0 = e0 & 2047u, gn = en & 2047u;
+                const uint2 t0 = s_mono2[g0 + (g0 >> 5)], tn = s_mono2[gn + (gn >> 5)];
+                mp = negp(t0, 0u - ((e0 >> 11) & 1u));
+                mn = negp(tn, 0u - ((en >> 11) & 1u));
+            } else {
+                const uint32_t f = (fl + ur) & 2047u, fn = 2048u - f;
+                mp = s_mono2[f + (f >> 5)];
+                mn = s_mono2[fn + (fn >> 5)];
+            }
             const uint4* q4 = kq[k2 % KB];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * k2 + e;
+                if (FULL && e == 1) {  // odd a: slot r + 1 is 2048 a further
+                    mp = negp(mp, 0u - (as & 1u));
+                    mn = negp(mn, 0u - (as & 1u));
+                }
 #pragma unroll
                 for (int o = 0; o < 2; ++o) {  // o = 0: this wave's component, 1: the partner's
                     int64_t S1 = 0, S2 = 0;
@@ -2478,8 +2508,10 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
 }
 
 bool n2k_supported(const GateArgs& g, const BootTables& t, int nd) {
-    // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29
-    return t.Q < (1u << 29) && (nd == 3 || (nd == 2 && t.Q >= (1u << 27))) && g.N == 2048 && g.ctmod < 2 * g.N &&
+    // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29; q = 2N
+    // (the full-resolution monomials) at 2^27 <= Q < 2^29
+    const bool qok = g.ctmod < 2 * g.N || (g.ctmod == 2 * g.N && t.Q >= (1u << 27));
+    return t.Q < (1u << 29) && (nd == 3 || (nd == 2 && t.Q >= (1u << 27))) && g.N == 2048 && qok &&
            g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
@@ -2493,17 +2525,22 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false, 2>),
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true, 2>),
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, false, 2>),
-                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, true, 2>)})
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, true, 2>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false, 2, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true, 2, true>)})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)w2_lds());
         return true;
     }();
     (void)attr;
     const uint32_t blocks = (g.count + kW2Gates - 1) / kW2Gates;
     const uint4* k = static_cast<const uint4*>(keys);
-#define FHE_N2K(ND_, IO, QM_)                                                                                      \
-    hipLaunchKernelGGL((k_blind_rotate_n2k<ND_, IO, QM_>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), s, g, t, k, \
-                       idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
-    if (t.Q < (1u << 27)) {  // STD256Q
+#define FHE_N2K(ND_, IO, QM_, ...)                                                                                 \
+    hipLaunchKernelGGL((k_blind_rotate_n2k<ND_, IO, QM_, ##__VA_ARGS__>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), \
+                       s, g, t, k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
+    if (g.ctmod == 2 * g.N) {  // STD256_4 (29-bit Q, q = 2N)
+        if (nd != 3) return hipErrorInvalidValue;
+        if (g.acc_io) FHE_N2K(3, true, 2, true); else FHE_N2K(3, false, 2, true);
+    } else if (t.Q < (1u << 27)) {  // STD256Q
         if (g.acc_io) FHE_N2K(3, true, 0); else FHE_N2K(3, false, 0);
     } else if (nd == 3) {  // STD256_3 (29-bit Q)
         if (g.acc_io) FHE_N2K(3, true, 2); else FHE_N2K(3, false, 2);

@@ -49,8 +49,8 @@ bool Engine::n2k_set(const Params& p) {
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
     // GINX: digitsG 4 at Q < 2^27 (STD256Q); digitsG 3 / 4 at 2^27 <= Q < 2^29 (STD256, STD256_3: the
     // forward transform reduced three times, FHE_HIP_N2K_EXT)
-    const bool ginx = p.method == M_GINX && p.q < 2 * p.N &&
-                      (p.digitsG == 4 || (p.digitsG == 3 && p.Q >= (1ull << 27)));
+    const bool ginx = p.method == M_GINX && (p.q < 2 * p.N || (p.q == 2 * p.N && p.Q >= (1ull << 27))) &&
+                      (p.digitsG == 4 || (p.digitsG == 3 && p.Q >= (1ull << 27) && p.q < 2 * p.N));
     // digitsG 3 with 2^27 <= Q < 2^28 (STD256Q_LMKCDEY) measured 24.0K -> 32.7K gates/s
     // (profiles/r04_ext_bench.txt); FHE_HIP_N2K_EXT=0 keeps it on K5
     const char* ext = std::getenv("FHE_HIP_N2K_EXT");
@@ -98,7 +98,8 @@ void Engine::build_tables_n2k() {
         tabF[i] = to_mont(h.tab[i], Q);
         tabI[i] = to_mont(h.tabI[i], Q);
     }
-    const uint64_t psi2 = mulmod(p_.psi, p_.psi, Q);
+    // q = 2N (odd exponents): psi^g - 1 for g in [0, 2048], the kernel negating past 2048 (FULL)
+    const uint64_t psi2 = p_.q == 2 * p_.N ? p_.psi : mulmod(p_.psi, p_.psi, Q);
     uint64_t x = 1;
     for (uint32_t f = 0; f <= 2048; ++f) {
         mono[f + (f >> 5)]  = to_mont(submod(x, 1, Q), Q);

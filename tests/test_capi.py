@@ -45,7 +45,8 @@ def test_kernel_path_per_parameter_set():
     assert bf.kernel_path(STD128_3, bf.GINX) == 2
     assert bf.kernel_path(STD256, bf.GINX) == 4       # N = 2048, 29-bit Q, q = 2048: K1w, forward reduced 3x
     assert bf.kernel_path(16, bf.GINX) == 4           # STD256_3 (3 retained digits)
-    assert bf.kernel_path(17, bf.GINX) == 3           # STD256_4: q = 4096 = 2N (odd exponents): K5 A32
+    assert bf.kernel_path(17, bf.GINX) == 4           # STD256_4: q = 2N, the full-resolution monomials
+    assert bf.kernel_path(19, bf.GINX) == 3           # STD256Q_3: q = 2N, 4 retained digits: K5 A32
     assert bf.kernel_path(STD192, bf.GINX) == 0       # 37-bit Q: 64-bit residues
     assert bf.kernel_path(18, bf.GINX) == 4           # STD256Q: K1w (N = 2048, accumulator in registers)
     assert bf.kernel_path(37, bf.LMKCDEY) == 4        # STD256Q_3_LMKCDEY: K1w's LMKCDEY form
