@@ -2297,7 +2297,7 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
 // FULL (q = 2N, STD256_4: odd monomial exponents): the table holds psi^g - 1 for g in [0, 2048] and
 // psi^(g + 2048) - 1 = -(psi^g - 1) - 2 is formed on the fly, (-x - 2, -y - 2R) with 2R centred (|y'| < Q:
 // |acc| < 2.93 Q, bound 30)
-template <int ND, int QM, bool FULL> constexpr int kW2Bound = QM == 2 ? (FULL ? 30 : 27) : kW2AccBound;
+template <int ND, int QM, bool FULL> constexpr int kW2Bound = QM == 2 ? (FULL ? (ND == 4 ? 32 : 30) : 27) : kW2AccBound;
 template <int ND, bool ACCIO, int QM = 0, bool FULL = false>
 __global__ void __launch_bounds__(128 * kW2Gates, 2)
     k_blind_rotate_n2k(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
@@ -2397,7 +2397,7 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
         uint32_t* const tile    = tile_o;
         uint32_t* const partner = partner_o;
 #endif
-        constexpr int KB = FHE_N2K_KPF + 1;
+        constexpr int KB = ND == 4 ? 1 : FHE_N2K_KPF + 1;  // 4 digits: no registers for the key ring
         uint4 kq[KB][kQ];
         __syncthreads();  // the partner has read this wave's tile (previous index)
         uint32_t d[ND][32];
@@ -2510,8 +2510,9 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
 bool n2k_supported(const GateArgs& g, const BootTables& t, int nd) {
     // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29; q = 2N
     // (the full-resolution monomials) at 2^27 <= Q < 2^29
-    const bool qok = g.ctmod < 2 * g.N || (g.ctmod == 2 * g.N && t.Q >= (1u << 27));
-    return t.Q < (1u << 29) && (nd == 3 || (nd == 2 && t.Q >= (1u << 27))) && g.N == 2048 && qok &&
+    const bool qok = g.ctmod < 2 * g.N || (g.ctmod == 2 * g.N && (t.Q >= (1u << 27) || nd == 4));
+    const bool ndok = nd == 3 || (nd == 2 && t.Q >= (1u << 27)) || (nd == 4 && g.ctmod == 2 * g.N);
+    return t.Q < (1u << 29) && ndok && g.N == 2048 && qok &&
            g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
@@ -2527,7 +2528,9 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, false, 2>),
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<2, true, 2>),
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false, 2, true>),
-                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true, 2, true>)})
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true, 2, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, false, 2, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, true, 2, true>)})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)w2_lds());
         return true;
     }();
@@ -2537,9 +2540,9 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
 #define FHE_N2K(ND_, IO, QM_, ...)                                                                                 \
     hipLaunchKernelGGL((k_blind_rotate_n2k<ND_, IO, QM_, ##__VA_ARGS__>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), \
                        s, g, t, k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
-    if (g.ctmod == 2 * g.N) {  // STD256_4 (29-bit Q, q = 2N)
-        if (nd != 3) return hipErrorInvalidValue;
-        if (g.acc_io) FHE_N2K(3, true, 2, true); else FHE_N2K(3, false, 2, true);
+    if (g.ctmod == 2 * g.N) {  // STD256_4 (29-bit Q, q = 2N); STD256Q_3 / STD256Q_4 (4 retained digits)
+        if (nd == 4) { if (g.acc_io) FHE_N2K(4, true, 2, true); else FHE_N2K(4, false, 2, true); }
+        else if (g.acc_io) FHE_N2K(3, true, 2, true); else FHE_N2K(3, false, 2, true);
     } else if (t.Q < (1u << 27)) {  // STD256Q
         if (g.acc_io) FHE_N2K(3, true, 0); else FHE_N2K(3, false, 0);
     } else if (nd == 3) {  // STD256_3 (29-bit Q)

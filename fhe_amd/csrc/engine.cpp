@@ -43,18 +43,21 @@ bool Engine::g3_set(const Params& p) {
 
 constexpr bool kN2kExtended = true;
 bool Engine::n2k_set(const Params& p) {
-    // GINX with even monomial exponents (q < 2N: the half-resolution table) and digitsG = 4; LMKCDEY at
-    // any q with digitsG = 4 or 5 (3 or 4 retained digits); the digit fields of d + C in 32 bits
-    // (digitsG = 3, two retained digits: Q < 2^28, the forward transform reduced once -- STD256Q_LMKCDEY)
+    // K1w at N = 2048: GINX with digitsG = 4 (q < 2N: the half-resolution table), and under
+    // FHE_HIP_N2K_EXT (default on) digitsG 3 / 4 at 29-bit Q and q = 2N (the negated half-range table,
+    // digitsG 4 / 5); LMKCDEY with digitsG = 4, and under FHE_HIP_N2K_EXT digitsG 3 (Q < 2^29) and 5
+    // (Q < 2^27); the digit fields of d + C in 32 bits
     const uint64_t g = p.gBits, h = 1ull << (g - 1);
-    // GINX: digitsG 4 at Q < 2^27 (STD256Q); digitsG 3 / 4 at 2^27 <= Q < 2^29 (STD256, STD256_3: the
-    // forward transform reduced three times, FHE_HIP_N2K_EXT)
-    const bool ginx = p.method == M_GINX && (p.q < 2 * p.N || (p.q == 2 * p.N && p.Q >= (1ull << 27))) &&
-                      (p.digitsG == 4 || (p.digitsG == 3 && p.Q >= (1ull << 27) && p.q < 2 * p.N));
-    // digitsG 3 with 2^27 <= Q < 2^28 (STD256Q_LMKCDEY) measured 24.0K -> 32.7K gates/s
-    // (profiles/r04_ext_bench.txt); FHE_HIP_N2K_EXT=0 keeps it on K5
     const char* ext = std::getenv("FHE_HIP_N2K_EXT");
     const bool wide_rows = ext ? std::string(ext) == "1" : kN2kExtended;
+    // GINX: digitsG 4 at Q < 2^27 (STD256Q); digitsG 3 / 4 at 2^27 <= Q < 2^29 (STD256, STD256_3, STD256_4:
+    // the forward transform reduced three times); digitsG 5 at q = 2N (STD256Q_3, STD256Q_4)
+    const bool ginx = p.method == M_GINX &&
+                      (p.q < 2 * p.N || (p.q == 2 * p.N && (p.Q >= (1ull << 27) || p.digitsG == 5))) &&
+                      (p.digitsG == 4 || (p.digitsG == 3 && p.Q >= (1ull << 27) && p.q < 2 * p.N) ||
+                       (p.digitsG == 5 && p.q == 2 * p.N && wide_rows));
+    // digitsG 3 with 2^27 <= Q < 2^28 (STD256Q_LMKCDEY) measured 24.0K -> 32.7K gates/s
+    // (profiles/r04_ext_bench.txt); FHE_HIP_N2K_EXT=0 keeps it on K5
     const bool lmk = p.method == M_LMKCDEY && (p.digitsG == 4 || (wide_rows && (p.digitsG == 3 || p.digitsG == 5)));
     if (lmk && p.Q >= (1ull << 27) && (!wide_rows || p.digitsG == 5)) return false;  // reduced forward: 2-3 digits
     // LMKCDEY: Q < 2^29 (the forward transform reduced once at Q >= 2^27, three times at Q >= 2^28: the

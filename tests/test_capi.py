@@ -46,7 +46,8 @@ def test_kernel_path_per_parameter_set():
     assert bf.kernel_path(STD256, bf.GINX) == 4       # N = 2048, 29-bit Q, q = 2048: K1w, forward reduced 3x
     assert bf.kernel_path(16, bf.GINX) == 4           # STD256_3 (3 retained digits)
     assert bf.kernel_path(17, bf.GINX) == 4           # STD256_4: q = 2N, the full-resolution monomials
-    assert bf.kernel_path(19, bf.GINX) == 3           # STD256Q_3: q = 2N, 4 retained digits: K5 A32
+    assert bf.kernel_path(19, bf.GINX) == 4           # STD256Q_3: q = 2N, 4 retained digits
+    assert bf.kernel_path(20, bf.GINX) == 4           # STD256Q_4
     assert bf.kernel_path(STD192, bf.GINX) == 0       # 37-bit Q: 64-bit residues
     assert bf.kernel_path(18, bf.GINX) == 4           # STD256Q: K1w (N = 2048, accumulator in registers)
     assert bf.kernel_path(37, bf.LMKCDEY) == 4        # STD256Q_3_LMKCDEY: K1w's LMKCDEY form
@@ -55,5 +56,4 @@ def test_kernel_path_per_parameter_set():
     assert bf.kernel_path(33, bf.LMKCDEY) == 3        # STD256_LMKCDEY (30-bit Q): K5 A32
     assert bf.kernel_path(34, bf.LMKCDEY) == 4        # STD256_3_LMKCDEY (29-bit Q, 3 digits): K1w, forward reduced 3x
     assert bf.kernel_path(35, bf.LMKCDEY) == 4        # STD256_4_LMKCDEY (29-bit Q, 3 digits)
-    assert bf.kernel_path(19, bf.GINX) == 3           # STD256Q_3: q = 2N (odd exponents), digitsG = 5
     assert bf.uses_fast_kernels(bf.STD128, bf.GINX) and not bf.uses_fast_kernels(STD256, bf.GINX)

@@ -171,7 +171,7 @@ def test_gpu_digitsg4_multi_input_gates_vs_reference(name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["std256q", "std256q_lmkcdey", "std256q_3_lmkcdey", "std256_3_lmkcdey",
                                   "std256_4_lmkcdey", "std256q_4_lmkcdey", "std256", "std256_3",
-                                  "std256_4"])
+                                  "std256_4", "std256q_3", "std256q_4"])
 def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
     """N = 2048, Q < 2^27, digitsG = 4: K1w, the register-resident two-waves-per-gate accumulators
     (STD256Q, q = 1024: launch_blind_rotate_n2k; STD256Q_LMKCDEY (28-bit Q) / STD256Q_3_LMKCDEY:
