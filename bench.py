@@ -385,8 +385,11 @@ def pmc_summary(kernel, field):
             d = json.load(open(f))
         except Exception:
             continue
-        k = d.get("kernels", {}).get(kernel)
-        if k and k.get("batch") and k.get(field) is not None:
+        # tools/pmc_traffic.py writes {"round", "calibration", ..., "kernels": {name: {...}}}; a summary committed
+        # as that tool's stdout is the bare {name: {...}} map
+        ks = d.get("kernels") if isinstance(d.get("kernels"), dict) else d
+        k = ks.get(kernel) if isinstance(ks, dict) else None
+        if isinstance(k, dict) and k.get("batch") and k.get(field) is not None:
             best = (k[field], k["batch"])
     return best
 

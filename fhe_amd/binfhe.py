@@ -42,6 +42,8 @@ OR, AND, NOR, NAND, XOR, XNOR, MAJORITY, AND3, OR3, AND4, OR4, XOR_FAST, XNOR_FA
 GATE_NAMES = {"OR": OR, "AND": AND, "NOR": NOR, "NAND": NAND, "XOR": XOR, "XNOR": XNOR, "MAJORITY": MAJORITY,
               "AND3": AND3, "OR3": OR3, "AND4": AND4, "OR4": OR4, "CMUX": CMUX}
 MULTI_GATES = (MAJORITY, AND3, OR3, AND4, OR4)
+OP_BOOTSTRAP = -1      # fhe_hip_eval_mixed_batch: BinFHEScheme::Bootstrap
+LARGE_DIM, SMALL_DIM = 3, 4   # BINFHE_OUTPUT (binfhe-constants.h:103-109): Encrypt's output dimension
 
 
 class _Params(ctypes.Structure):
@@ -118,6 +120,14 @@ def _setup(L):
     L.fhe_hip_max_batch_size.argtypes = [vp, vp]
     L.fhe_hip_device_memory.argtypes = [ctypes.c_int, vp, vp]
     L.fhe_hip_unpack_keys.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, vp, sz, vp, sz, vp, sz, vp, sz]
+    L.fhe_hip_switch_to_qn_batch.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.fhe_hip_switch_to_qn_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp]
+    L.fhe_hip_eval_mixed_batch.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, sz, vp, vp, vp, vp, vp,
+                                           ctypes.c_int]
+    L.fhe_hip_eval_mixed_batch_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, sz, vp, vp, vp,
+                                                  vp, vp, ctypes.c_int, vp]
+    L.fhe_hip_keygen_ring_secret.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp]
+    L.fhe_hip_encrypt_large.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, ctypes.c_uint32, vp, vp]
     L._binfhe_ready = True
     return L
 
@@ -205,6 +215,24 @@ def encrypt(paramset, method, sk, bits, seed, p=4, mod=0):
     b = np.zeros(len(bits), np.uint64)
     check(L().fhe_hip_encrypt_mod(paramset, method, ptr(_u64(sk)), ptr(bits), len(bits), seed, p, mod, ptr(a),
                                   ptr(b)))
+    return a, b
+
+
+def keygen_ring_secret(paramset, method, seed):
+    """skN[N] of keygen(seed) (KeyGenN's key) stored mod qKS: the LWE secret of dimension-N ciphertexts
+    mod Q (decrypt(..., skN, a, b, mod=Q) with a of N columns)"""
+    skN = np.zeros(params(paramset, method).N, np.uint64)
+    check(L().fhe_hip_keygen_ring_secret(paramset, method, seed, ptr(skN)))
+    return skN
+
+
+def encrypt_large(paramset, method, skN, bits, seed, p=4):
+    """Encrypt(pk, m, LARGE_DIM, p) (binfhecontext.cpp:236-252): dimension N, modulus Q, under skN"""
+    P = params(paramset, method)
+    bits = np.ascontiguousarray(bits, dtype=np.int32)
+    a = np.zeros((len(bits), P.N), np.uint64)
+    b = np.zeros(len(bits), np.uint64)
+    check(L().fhe_hip_encrypt_large(paramset, method, ptr(_u64(skN)), ptr(bits), len(bits), seed, p, ptr(a), ptr(b)))
     return a, b
 
 
@@ -480,6 +508,36 @@ class GateEngine:
                                                        _ptrs(d_b_list), vp(d_ao), vp(d_bo),
                                                        vp(stream) if stream else None))
 
+    def switch_to_qn(self, a, b):
+        """SwitchCTtoqn (lwe-pke.cpp:170-178): a [count][N], b [count] mod Q -> (n, q)"""
+        a, b = _u64(a), _u64(b)
+        cnt = len(b)
+        ao = np.zeros((cnt, self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        check(L().fhe_hip_switch_to_qn_batch(self._h, cnt, ptr(a), ptr(b), ptr(ao), ptr(bo)))
+        return ao, bo
+
+    def eval_mixed(self, op, a_list, b_list, large=None, ptmod=4, extended=False):
+        """fhe_hip_eval_mixed_batch: op a gate or OP_BOOTSTRAP over k columns whose rows may be mod Q.
+        a_list[j]: [count][n] (column all mod q) or [count][N] with large[j][g] = 1 marking the rows mod Q
+        (large[j] None: the column is mod q)"""
+        a_list = [_u64(a) for a in a_list]
+        b_list = [_u64(b) for b in b_list]
+        k, cnt = len(a_list), len(b_list[0])
+        flags = [None if large is None or large[j] is None else np.ascontiguousarray(large[j], np.uint8)
+                 for j in range(k)]
+        for j in range(k):
+            want = self.params.N if flags[j] is not None else self.params.n
+            if a_list[j].shape != (cnt, want):
+                raise FheHipError(-2, f"column {j}: rows of {want} words expected")
+        wide = extended and op != CMUX
+        ao = np.zeros((cnt, self.params.N if wide else self.params.n), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        lp = (vp * k)(*[f.ctypes.data if f is not None else None for f in flags])
+        check(L().fhe_hip_eval_mixed_batch(self._h, op, k, ptmod, cnt, _ptrs(a_list), _ptrs(b_list), lp, ptr(ao),
+                                           ptr(bo), int(extended)))
+        return ao, bo
+
     def eval_cmux_device(self, count, d_a0, d_b0, d_a1, d_b1, d_a2, d_b2, d_ao, d_bo, stream=None):
         check(L().fhe_hip_eval_cmux_batch_device(self._h, count, vp(d_a0), vp(d_b0), vp(d_a1), vp(d_b1), vp(d_a2),
                                                  vp(d_b2), vp(d_ao), vp(d_bo), vp(stream) if stream else None))
@@ -694,7 +752,8 @@ class BinFHEContext:
 
     def BTKeyGen(self, sk):
         """keys generated on the device (fhe_hip_btkeygen_device); nothing crosses PCIe"""
-        self.engine.keygen_device(sk.s, self._next_seed())
+        self._key_seed = self._next_seed()
+        self.engine.keygen_device(sk.s, self._key_seed)
 
     def BTKeyLoad(self, bsk, kskA, kskB=None):
         """raw arrays (bsk, kskA, kskB), or the deserialized refresh / switching keys
@@ -705,7 +764,15 @@ class BinFHEContext:
             self.engine.load_keys(bsk, kskA, kskB)
 
     def Encrypt(self, sk, m, output=None, p=4, mod=0):
-        """Encrypt(sk, m, SMALL_DIM, p, mod) (binfhecontext.cpp:220-234)"""
+        """Encrypt(sk, m, SMALL_DIM, p, mod) (binfhecontext.cpp:220-234).  output = LARGE_DIM: the
+        dimension-N encryption mod Q that Encrypt(pk, m, LARGE_DIM, p) makes (:236-252), under the RLWE
+        secret of the keys BTKeyGen generated"""
+        if output == LARGE_DIM:
+            if getattr(self, "_key_seed", None) is None:
+                raise FheHipError(-11, "LARGE_DIM encryption needs the keys of BTKeyGen")
+            skN = keygen_ring_secret(self.paramset, self.method, self._key_seed)
+            a, b = encrypt_large(self.paramset, self.method, skN, [int(m)], self._next_seed(), p)
+            return LWECiphertext(a[0], int(b[0]), self.params.Q, p)
         a, b = encrypt(self.paramset, self.method, sk.s, [int(m)], self._next_seed(), p, mod)
         return LWECiphertext(a[0], int(b[0]), mod or self.params.q, p)
 
@@ -762,27 +829,64 @@ class BinFHEContext:
         a = np.where(ct.a == 0, 0, q - ct.a.astype(np.uint64)).astype(np.uint64)
         return LWECiphertext(a, int(((q >> 2) - ct.b) % q), q, ct.p)
 
-    def EvalBinGate(self, gate, ct1, ct2=None):
-        """EvalBinGate(gate, ct1, ct2) or EvalBinGate(gate, ctvector) (binfhecontext.h:305-315)"""
-        if ct2 is None:
-            return self._eval_vector(gate, list(ct1))
+    def EvalBinGate(self, gate, ct1, ct2=None, extended=False):
+        """EvalBinGate(gate, ct1, ct2, extended) or EvalBinGate(gate, ctvector, extended)
+        (binfhecontext.h:305-315).  Inputs mod q or mod Q (extended outputs, LARGE_DIM encryptions) are
+        switched to (n, q) on the GPU first, as the reference does (binfhe-base-scheme.cpp:92-93, 150-152)."""
+        if ct2 is None or isinstance(ct2, bool):
+            return self._eval_vector(gate, list(ct1), bool(ct2) if isinstance(ct2, bool) else extended)
         if ct1 is ct2:
             raise FheHipError(-8, "Input ciphertexts should be independant")
+        if extended or self._large(ct1) or self._large(ct2):
+            ao, bo = self._mixed(gate, [ct1, ct2], 4, extended)
+            return self._out(ao, bo, extended, 4)
         return self.EvalBinGateBatch(gate, [ct1], [ct2])[0]
 
-    def _eval_vector(self, gate, cts):
+    def Bootstrap(self, ct, extended=False):
+        """BinFHEContext::Bootstrap (binfhe-base-scheme.cpp:190-220): a ciphertext mod q or mod Q;
+        ctExt (dimension N, mod Q) when extended"""
+        ao, bo = self._mixed(OP_BOOTSTRAP, [ct], ct.p, extended)
+        return self._out(ao, bo, extended, ct.p)
+
+    def _large(self, ct):
+        return ct.modulus == self.params.Q
+
+    def _mixed(self, op, cts, p, extended):
+        cols_a, cols_b, large = [], [], []
+        P = self.params
+        for c in cts:
+            if self._large(c):
+                if len(c.a) != P.N:
+                    raise FheHipError(-2, "ciphertext mod Q of dimension N expected")
+                cols_a.append(c.a[None, :]); large.append(np.ones(1, np.uint8))
+            else:
+                cols_a.append(c.a[None, :]); large.append(None)
+            cols_b.append(np.array([c.b], np.uint64))
+        return self.engine.eval_mixed(op, cols_a, cols_b, large, p, extended)
+
+    def _out(self, ao, bo, extended, p):
+        mod = self.params.Q if extended else self.params.q
+        return LWECiphertext(ao[0], int(bo[0]), mod, p)
+
+    def _eval_vector(self, gate, cts, extended=False):
         for i in range(len(cts)):
             for j in range(i + 1, len(cts)):
                 if cts[i] is cts[j]:
                     raise FheHipError(-8, "Input ciphertexts should be independent")
         if gate in MULTI_GATES:
             p = cts[0].p
+            if extended or any(self._large(c) for c in cts):
+                ao, bo = self._mixed(gate, cts, p, extended)
+                return self._out(ao, bo, extended, p)
             ao, bo = self.engine.eval_gate_multi(gate, [c.a[None, :] for c in cts],
                                                  [np.array([c.b], np.uint64) for c in cts], p)
             return LWECiphertext(ao[0], int(bo[0]), self.params.q, p)
         if gate == CMUX:
             if len(cts) != 3:
                 raise FheHipError(-8, "CMUX gate implemented for ciphertext vectors of size 3")
+            if any(self._large(c) for c in cts):   # CMUX ignores extended (:180-182)
+                ao, bo = self._mixed(CMUX, cts, 4, False)
+                return self._out(ao, bo, False, 4)
             return self.EvalCMUXBatch([cts[0]], [cts[1]], [cts[2]])[0]
         raise FheHipError(-8, "This gate is not implemented for vector of ciphertexts at this time")
 

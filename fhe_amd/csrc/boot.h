@@ -194,6 +194,25 @@ hipError_t launch_lwe_addb(uint64_t* b, uint64_t c, uint64_t m, size_t count, hi
 // the 32-bit key switch's input, for the digitsG = 4 sets of launch_blind_rotate_ginx3)
 hipError_t launch_narrow_u32(const uint64_t* a, const uint64_t* b, uint32_t* ao, uint32_t* bo, uint32_t len, size_t count,
                              hipStream_t s);
+// u32 [count][len] / [count] -> u64 (the 32-bit path's ctExt out of the workspace)
+hipError_t launch_widen_u64(const uint32_t* a, const uint32_t* b, uint64_t* ao, uint64_t* bo, uint32_t len, size_t count,
+                            hipStream_t s);
+// Ciphertexts mod Q as gate / bootstrap inputs (binfhe-base-scheme.cpp:92-93, 150-152, 200): SwitchCTtoqn
+// (lwe-pke.cpp:170-178) of the rows of a column that are mod Q.  A column holds `count` ciphertexts as
+// rows of `stride` u64 words (a) and count words (b); large[g] != 0 marks a ciphertext mod Q of dimension N,
+// 0 one mod q of dimension n (its first n words); large == nullptr: every row is mod Q.
+//   switch_in:  ModSwitch(Q -> qKS) (RoundqQ in IEEE double, lwe-pke.cpp:41-46, 254-261) of the flagged rows
+//               into the key switch's input ext [count][N] (u32, or u64 when ext64) / [count]; other rows 0.
+//               negate: EvalNOT at modulus Q first (binfhe-base-scheme.cpp:223-236; CMUX's NOT ct2, :180)
+//   switch_out: after KeySwitch + ModSwitch(qKS -> q) of ext into (a_out, b_out) [count][n] / [count], the
+//               unflagged rows copied in from the input (negated at q when negate); set_b: b_out of the
+//               flagged rows = b_large instead (Bootstrap's test-vector offset, Engine::eval_mixed_device)
+hipError_t launch_switch_in(const uint64_t* a, const uint64_t* b, uint32_t stride, const uint8_t* large, uint64_t Q,
+                            uint64_t qKS, uint32_t N, size_t count, bool negate, void* ext_a, void* ext_b, bool ext64,
+                            hipStream_t s);
+hipError_t launch_switch_out(const uint64_t* a, const uint64_t* b, uint32_t stride, const uint8_t* large, uint32_t n,
+                             uint64_t q, size_t count, bool negate, bool set_b, uint64_t b_large, uint64_t* a_out,
+                             uint64_t* b_out, hipStream_t s);
 // ModSwitch on u64 vectors (lwe-pke.cpp:41-46, 254-261)
 hipError_t launch_modswitch(uint64_t q_from, uint64_t q_to, uint32_t len, uint32_t count, const uint64_t* a,
                             const uint64_t* b, uint64_t* a_out, uint64_t* b_out, hipStream_t s);

@@ -2509,8 +2509,9 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
 
 bool n2k_supported(const GateArgs& g, const BootTables& t, int nd) {
     // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29; q = 2N
-    // (the full-resolution monomials) at 2^27 <= Q < 2^29
-    const bool qok = g.ctmod < 2 * g.N || (g.ctmod == 2 * g.N && (t.Q >= (1u << 27) || nd == 4));
+    // (the full-resolution monomials) only in the instantiations launched below: 3 digits at
+    // 2^27 <= Q < 2^29 or 4 digits (no 2-digit form takes q = 2N: such calls stay on K5)
+    const bool qok = g.ctmod < 2 * g.N || (g.ctmod == 2 * g.N && ((nd == 3 && t.Q >= (1u << 27)) || nd == 4));
     const bool ndok = nd == 3 || (nd == 2 && t.Q >= (1u << 27)) || (nd == 4 && g.ctmod == 2 * g.N);
     return t.Q < (1u << 29) && ndok && g.N == 2048 && qok &&
            g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && (uint32_t)(nd + 1) * g.gbits <= 32;

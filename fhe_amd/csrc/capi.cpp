@@ -81,7 +81,7 @@ struct fhe_hip_ctx {
 
 static void fill_params(const Params& p, fhe_hip_params* o) {
     o->paramset = p.paramset; o->method = p.method; o->n = p.n; o->N = p.N; o->q = p.q; o->qKS = p.qKS;
-    o->kernel = Engine::fast_path(p) ? 1u : Engine::g3_set(p) ? 2u : Engine::n2k_set(p) ? 4u : Engine::narrow_set(p) ? 3u : 0u;
+    o->kernel = Engine::kernel_kind(p);
     o->baseKS = p.baseKS; o->digitsKS = p.digitsKS; o->baseG = p.baseG; o->digitsG = p.digitsG;
     o->numAutoKeys = p.numAutoKeys; o->keyDist = p.keyDist; o->Q = p.Q; o->psi = p.psi;
     o->bsk_words = p.bsk_words(); o->ksk_rows = p.ksk_rows_all();
@@ -604,6 +604,60 @@ int fhe_hip_bootstrap_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
     });
 }
 
+int fhe_hip_switch_to_qn_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
+                               uint64_t* b_out) {
+    if (!ctx || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
+        ctx->eng.switch_to_qn_host(count, a, b, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_switch_to_qn_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                      uint64_t* d_a_out, uint64_t* d_b_out, void* stream) {
+    if (!ctx || !io_ok(count, d_a, d_b, d_a_out, d_b_out, d_a, d_b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const CallOrder order(ctx, stream);
+        ctx->eng.switch_to_qn_device(count, d_a, d_b, d_a_out, d_b_out, order.s);
+        return FHE_HIP_OK;
+    });
+}
+
+static bool mixed_args_ok(uint32_t k, size_t count, const uint64_t* const* a_in, const uint64_t* const* b_in,
+                          const uint64_t* a_out, const uint64_t* b_out) {
+    if (!count) return true;
+    if (!a_in || !b_in || !a_out || !b_out || k < 1 || k > 4) return false;
+    for (uint32_t j = 0; j < k; ++j)
+        if (!a_in[j] || !b_in[j]) return false;
+    return true;
+}
+
+int fhe_hip_eval_mixed_batch(fhe_hip_ctx* ctx, int op, uint32_t k, uint32_t ptmod, size_t count,
+                             const uint64_t* const* a_in, const uint64_t* const* b_in, const uint8_t* const* large,
+                             uint64_t* a_out, uint64_t* b_out, int extended) {
+    if (!ctx || !mixed_args_ok(k, count, a_in, b_in, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
+        ctx->eng.eval_mixed_host(op, k, ptmod, count, a_in, b_in, large, a_out, b_out, extended != 0);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_mixed_batch_device(fhe_hip_ctx* ctx, int op, uint32_t k, uint32_t ptmod, size_t count,
+                                    const uint64_t* const* d_a_in, const uint64_t* const* d_b_in,
+                                    const uint8_t* const* d_large, uint64_t* d_a_out, uint64_t* d_b_out, int extended,
+                                    void* stream) {
+    if (!ctx || !mixed_args_ok(k, count, d_a_in, d_b_in, d_a_out, d_b_out))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        const CallOrder order(ctx, stream);
+        ctx->eng.eval_mixed_device(op, k, ptmod, count, d_a_in, d_b_in, d_large, d_a_out, d_b_out, extended != 0,
+                                   order.s);
+        return FHE_HIP_OK;
+    });
+}
+
 // ---- the Backend seam (backend.h:73-247) ----
 int fhe_hip_blind_rotate_acc_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, uint64_t ctmod, uint64_t* acc) {
     if (!ctx || (count && (!a || !acc))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
@@ -963,6 +1017,27 @@ int fhe_hip_decrypt_ptmod(int paramset, int method, const uint64_t* sk, const ui
         Params p = make_params(paramset, method);
         if (len != p.n && len != p.N) return fail(FHE_HIP_ERR_INVALID_PARAM, "len must be n or N");
         for (size_t i = 0; i < count; ++i) out[i] = decrypt(p, sk, a + i * len, b[i], len, mod, ptmod);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_keygen_ring_secret(int paramset, int method, uint64_t seed, uint64_t* skN) {
+    if (!skN) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        Params p = make_params(paramset, method);
+        std::vector<uint64_t> s;
+        keygen_ring_secret(p, seed, s);
+        for (uint32_t i = 0; i < p.N; ++i) skN[i] = s[i] > (p.Q >> 1) ? p.qKS - (p.Q - s[i]) % p.qKS : s[i] % p.qKS;
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_encrypt_large(int paramset, int method, const uint64_t* skN, const int* bits, size_t count, uint64_t seed,
+                          uint32_t ptmod, uint64_t* a, uint64_t* b) {
+    if (!skN || (count && (!bits || !a || !b))) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        Params p = make_params(paramset, method);
+        encrypt(p, skN, bits, count, seed, a, b, ptmod, p.Q, p.N);
         return FHE_HIP_OK;
     });
 }

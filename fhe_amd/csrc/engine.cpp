@@ -71,6 +71,21 @@ bool Engine::n2k_set(const Params& p) {
     return C + p.Q < (1ull << 32);
 }
 
+namespace {
+bool knob_off(const char* name) {
+    const char* e = std::getenv(name);
+    return e && std::string(e) == "0";
+}
+}  // namespace
+
+uint32_t Engine::kernel_kind(const Params& p) {
+    if (fast_path(p)) return 1;
+    if (g3_set(p) && !knob_off("FHE_HIP_GINX3")) return 2;
+    if (n2k_set(p) && !knob_off("FHE_HIP_N2K")) return 4;
+    if (narrow_set(p) && !knob_off("FHE_HIP_NARROW")) return 3;
+    return 0;
+}
+
 bool Engine::ks32_set(const Params& p) {
     const bool pow2ks = !(p.qKS & (p.qKS - 1)), pow2b = !(p.baseKS & (p.baseKS - 1));
     const bool shape = ((p.baseKS == 32 || p.baseKS == 64) && p.digitsKS == 3) || (p.baseKS == 16 && p.digitsKS == 4);
@@ -80,7 +95,8 @@ bool Engine::ks32_set(const Params& p) {
 
 bool Engine::ks32w_set(const Params& p) {
     const bool pow2ks = p.qKS && !(p.qKS & (p.qKS - 1));
-    return !is_large(p.paramset) && !p.timeopt && pow2ks && p.qKS > 65536 && p.qKS <= (1ull << 32) &&
+    // qKS < 2^32: GateArgs::qKS is a u32 word (launch_keyswitch_w32 reads it from there)
+    return !is_large(p.paramset) && !p.timeopt && pow2ks && p.qKS > 65536 && p.qKS < (1ull << 32) &&
            keyswitch_w32_shape(p.baseKS, p.digitsKS) && p.n < 2048 && p.N <= 2048;
 }
 
@@ -316,7 +332,7 @@ Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_mix_, (void*)d_mixio_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
                       d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
                       (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_, d_tables2k_,
                       (void*)d_ksk32_})
@@ -960,17 +976,6 @@ void Engine::blind_rotate_init_device(size_t count, const uint64_t* a, const uin
     prep_device(g, in, 0, s);
     rotate_device(g, s);
     rot_count_ = 0;
-    if (std::getenv("FHE_HIP_DEBUG")) {  // diagnostics: the op count and accumulator words of gate 0
-        uint32_t nops0 = 0;
-        uint64_t w[4] = {};
-        FHE_HIP_CHECK(hipStreamSynchronize(s));
-        if (d_nops_) FHE_HIP_CHECK(hipMemcpy(&nops0, d_nops_, 4, hipMemcpyDeviceToHost));
-        FHE_HIP_CHECK(hipMemcpy(w, acc, sizeof w, hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[fhe_hip] blind_rotate_init count=%zu cap=%zu maxops=%u nops0=%u wide=%d narrow=%d "
-                     "acc=%llu %llu %llu %llu err=%d\n", count, cap_, maxops_, nops0, (int)wide_, (int)narrow_,
-                     (unsigned long long)w[0], (unsigned long long)w[1], (unsigned long long)w[2],
-                     (unsigned long long)w[3], (int)hipGetLastError());
-    }
 }
 
 void Engine::external_product_device(size_t count, const uint64_t* rgsw, const uint64_t* rlwe, uint64_t* result,
@@ -1088,28 +1093,225 @@ void Engine::eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* 
     if (2 * count > 0x7fffffffull) throw std::invalid_argument("batch too large");
     ensure_work(2 * count);
     FHE_HIP_CHECK(hipSetDevice(device_));
-    if (count > ccap_) {
-        FHE_HIP_CHECK(hipStreamSynchronize(s));
-        if (d_l1_) FHE_HIP_CHECK(hipFree(d_l1_));
-        d_l1_ = nullptr;
-        ccap_ = 0;
-        FHE_HIP_CHECK(hipMalloc(&d_l1_, 2 * count * ((size_t)p_.n + 1) * 8));
-        ccap_ = count;
-    }
+    cmux_levels(count, a0, b0, a1, b1, a2, b2, nullptr, nullptr, a_out, b_out, s);
+}
+
+uint64_t* Engine::grow(uint64_t*& ptr, size_t& cap, size_t bytes) {
+    if (bytes <= cap) return ptr;
+    sync_streams();
+    if (ptr) FHE_HIP_CHECK(hipFree(ptr));
+    ptr = nullptr;
+    cap = 0;
+    FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&ptr), bytes));
+    cap = bytes;
+    return ptr;
+}
+
+void Engine::cmux_levels(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
+                         const uint64_t* a2, const uint64_t* b2, const uint64_t* a2n, const uint64_t* b2n,
+                         uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
     const size_t n = p_.n;
-    uint64_t* l1a = d_l1_;                 // [2 count][n]: NAND(ct0, NOT ct2) | NAND(ct1, ct2)
-    uint64_t* l1b = d_l1_ + 2 * count * n; // [2 count]
+    uint64_t* l1 = grow(d_l1_, ccap_, 2 * count * (n + 1) * 8);
+    uint64_t* l1a = l1;                 // [2 count][n]: NAND(ct0, NOT ct2) | NAND(ct1, ct2)
+    uint64_t* l1b = l1 + 2 * count * n; // [2 count]
     const GateArgs gh = gate_args(G_NAND, count);
-    GateInputs lo{{a0, a2, nullptr, nullptr}, {b0, b2, nullptr, nullptr}, 2, 2u, p_.q >> 2};  // ct0 + NOT ct2
-    GateInputs hi{{a1, a2, nullptr, nullptr}, {b1, b2, nullptr, nullptr}, 2, 0u, 0u};
+    // ct0 + NOT ct2: EvalNOT (:223-236) folded into the input combination (ct0 - ct2, b offset q/4; exact
+    // mod the power-of-two q), or the explicit NOT column when ct2 was switched from Q
+    const GateInputs lo = a2n ? GateInputs{{a0, a2n, nullptr, nullptr}, {b0, b2n, nullptr, nullptr}, 2, 0u, 0u}
+                              : GateInputs{{a0, a2, nullptr, nullptr}, {b0, b2, nullptr, nullptr}, 2, 2u, p_.q >> 2};
+    const GateInputs hi{{a1, a2, nullptr, nullptr}, {b1, b2, nullptr, nullptr}, 2, 0u, 0u};
     prep_device(gh, lo, 0, s);
     prep_device(gh, hi, count, s);
     rotate_device(gate_args(G_NAND, 2 * count), s);
     keyswitch_workspace_device(2 * count, l1a, l1b, s);
-    GateInputs top{{l1a, l1a + count * n, nullptr, nullptr}, {l1b, l1b + count, nullptr, nullptr}, 2, 0u, 0u};
+    const GateInputs top{{l1a, l1a + count * n, nullptr, nullptr}, {l1b, l1b + count, nullptr, nullptr}, 2, 0u, 0u};
     prep_device(gh, top, 0, s);
     rotate_device(gh, s);
     keyswitch_workspace_device(count, a_out, b_out, s);
+}
+
+void Engine::ext_to_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    if (count > rot_count_) throw std::logic_error("ctExt of more ciphertexts than the last blind rotation produced");
+    if (wide_) {
+        FHE_HIP_CHECK(hipMemcpyAsync(a_out, d_wext_a_, count * p_.N * 8, hipMemcpyDeviceToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(b_out, d_wext_b_, count * 8, hipMemcpyDeviceToDevice, s));
+        return;
+    }
+    FHE_HIP_CHECK(launch_widen_u64(d_ext_a_, d_ext_b_, a_out, b_out, p_.N, count, s));
+}
+
+void Engine::switch_column_device(size_t count, const uint64_t* a, const uint64_t* b, uint32_t stride,
+                                  const uint8_t* large, bool negate, bool set_b, uint64_t b_large, uint64_t* a_out,
+                                  uint64_t* b_out, hipStream_t s) {
+    // ModSwitch(Q -> qKS) into the key switch's input, KeySwitch + ModSwitch(qKS -> q) (K2's epilogue) into
+    // the output column, then the rows that were mod q already copied in (lwe-pke.cpp:170-178)
+    FHE_HIP_CHECK(launch_switch_in(a, b, stride, large, p_.Q, p_.qKS, p_.N, count, negate,
+                                   wide_ ? (void*)d_wext_a_ : (void*)d_ext_a_, wide_ ? (void*)d_wext_b_ : (void*)d_ext_b_,
+                                   wide_, s));
+    keyswitch_ext(count, p_.q, a_out, b_out, s);
+    FHE_HIP_CHECK(launch_switch_out(a, b, stride, large, p_.n, p_.q, count, negate, set_b, b_large, a_out, b_out, s));
+    rot_count_ = 0;  // the workspace no longer holds a blind rotation's ctExt
+}
+
+void Engine::switch_to_qn_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out,
+                                 hipStream_t s) {
+    if (!d_ksk_ && !d_wksk_) throw std::logic_error("key-switching key not loaded");
+    if (count == 0) return;
+    if (!a || !b || !a_out || !b_out) throw std::invalid_argument("null argument");
+    if (count > 0x7fffffffull) throw std::invalid_argument("batch too large");
+    ensure_work(count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    switch_column_device(count, a, b, p_.N, nullptr, false, false, 0, a_out, b_out, s);
+}
+
+void Engine::eval_mixed_device(int op, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a,
+                               const uint64_t* const* b, const uint8_t* const* large, uint64_t* a_out, uint64_t* b_out,
+                               bool extended, hipStream_t s) {
+    if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
+    const bool multi = op == G_MAJORITY || op == G_AND3 || op == G_OR3 || op == G_AND4 || op == G_OR4;
+    if (op == kOpBootstrap) {
+        if (k != 1) throw std::invalid_argument("Bootstrap takes one ciphertext");
+        if (ptmod < 1) throw std::invalid_argument("plaintext modulus out of range");
+    } else if (op == G_CMUX) {
+        if (k != 3) throw std::invalid_argument("CMUX gate implemented for ciphertext vectors of size 3");
+    } else if (multi) {
+        if (k < 2 || k > 4) throw std::invalid_argument("EvalBinGate(ctvector): 2 to 4 ciphertexts");
+        gate_args(op, count, ptmod, true);
+    } else {
+        if (k != 2) throw std::invalid_argument("EvalBinGate: two ciphertexts");
+        gate_args(op, count);
+    }
+    if (count == 0) return;
+    if (!a || !b || !a_out || !b_out) throw std::invalid_argument("null argument");
+    for (uint32_t j = 0; j < k; ++j)
+        if (!a[j] || !b[j]) throw std::invalid_argument("null ciphertext array");
+    if ((op == G_CMUX ? 2 : 1) * count > 0x7fffffffull) throw std::invalid_argument("batch too large");
+    ensure_work(op == G_CMUX ? 2 * count : count);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    const size_t n = p_.n, col = count * (n + 1);
+    bool any = false;
+    for (uint32_t j = 0; j < k; ++j) any |= large && large[j];
+    const bool cmux_not = op == G_CMUX && large && large[2];
+    uint64_t* mix = any ? grow(d_mix_, mixcap_, (k + (cmux_not ? 1 : 0)) * col * 8) : nullptr;
+    // Bootstrap (:199-201): ct + (ct->GetModulus() >> 2) by ModAddFast at the switched ciphertext's modulus q.
+    // For an input mod Q that sum is b_sw + Q/4 - q >= 1.5 q, and BootstrapGateCore's window walk
+    // (:562-567, ModSubFast by 1 from there) never wraps and never enters [lb, ub < q): every test-vector
+    // slot is uv.  The device prep adds q/4 mod q to b; the b its window test then sees, (lb - 1) mod q,
+    // walks exactly the complement of [lb, ub), so the same all-uv test vector results.
+    const GateArgs gand = gate_args(G_AND, count);
+    if (op == kOpBootstrap && any && (p_.Q >> 2) < 2 * (uint64_t)p_.q + (p_.q >> 1))
+        throw std::invalid_argument("Bootstrap of a ciphertext mod Q needs Q/4 >= 2.5 q");
+    const uint64_t q = p_.q, b_large = ((uint64_t)gand.lb + 2 * q - 1 - (q >> 2)) % q;
+    const uint64_t* ia[4] = {};
+    const uint64_t* ib[4] = {};
+    for (uint32_t j = 0; j < k; ++j) {
+        if (large && large[j]) {
+            uint64_t* ca = mix + j * col;
+            uint64_t* cb = ca + count * n;
+            switch_column_device(count, a[j], b[j], p_.N, large[j], false, op == kOpBootstrap, b_large, ca, cb, s);
+            ia[j] = ca;
+            ib[j] = cb;
+        } else {
+            ia[j] = a[j];
+            ib[j] = b[j];
+        }
+    }
+    if (op == G_CMUX) {
+        const uint64_t *a2n = nullptr, *b2n = nullptr;
+        if (cmux_not) {  // EvalNOT at ct2's own modulus (:180, :223-236), then the NAND's SwitchCTtoqn
+            uint64_t* ca = mix + k * col;
+            uint64_t* cb = ca + count * n;
+            switch_column_device(count, a[2], b[2], p_.N, large[2], true, false, 0, ca, cb, s);
+            a2n = ca;
+            b2n = cb;
+        }
+        cmux_levels(count, ia[0], ib[0], ia[1], ib[1], ia[2], ib[2], a2n, b2n, a_out, b_out, s);
+        return;
+    }
+    if (op == kOpBootstrap) {
+        // the window and its values are p = 4's (the switched / copied ciphertext's default plaintext
+        // modulus, lwe-ciphertext.h:161); the extraction's b uses the input's own (:210-211)
+        GateArgs g = gand;
+        g.b_const = (uint32_t)(p_.Q / (2 * (uint64_t)ptmod) + 1);
+        g.b64 = p_.Q / (2 * (uint64_t)ptmod) + 1;
+        g.msb_out = extended ? 0 : 1;
+        const GateInputs in{{ia[0], nullptr, nullptr, nullptr}, {ib[0], nullptr, nullptr, nullptr}, 1, 0, p_.q >> 2};
+        prep_device(g, in, 0, s);
+        rotate_device(g, s);
+    } else if (multi) {
+        GateArgs g = gate_args(op, count, ptmod, true);
+        g.msb_out = extended ? 0 : 1;
+        GateInputs in{};
+        for (uint32_t j = 0; j < k; ++j) {
+            in.a[j] = ia[j];
+            in.b[j] = ib[j];
+        }
+        in.k = k;
+        prep_device(g, in, 0, s);
+        rotate_device(g, s);
+    } else {
+        bootstrap_device(op, count, ia[0], ib[0], ia[1], ib[1], !extended, s);
+    }
+    if (extended)
+        ext_to_device(count, a_out, b_out, s);
+    else
+        keyswitch_workspace_device(count, a_out, b_out, s);
+}
+
+void Engine::eval_mixed_host(int op, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a,
+                             const uint64_t* const* b, const uint8_t* const* large, uint64_t* a_out, uint64_t* b_out,
+                             bool extended) {
+    if (k < 1 || k > 4) throw std::invalid_argument("1 to 4 ciphertext columns");
+    if (count == 0) return;
+    const size_t n = p_.n, N = p_.N;
+    // staged columns (rows of N words where flagged), flags, and the output
+    size_t words = 0;
+    for (uint32_t j = 0; j < k; ++j) words += count * ((large && large[j] ? N : n) + 1) + (count + 7) / 8;
+    const size_t outw = count * ((extended && op != G_CMUX ? N : n) + 1);
+    uint64_t* d = grow(d_mixio_, mixiocap_, (words + outw) * 8);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    const uint64_t* da[4] = {};
+    const uint64_t* db[4] = {};
+    const uint8_t* dl[4] = {};
+    uint64_t* cur = d;
+    for (uint32_t j = 0; j < k; ++j) {
+        if (!a[j] || !b[j]) throw std::invalid_argument("null ciphertext array");
+        const bool lg = large && large[j];
+        const size_t len = lg ? N : n;
+        FHE_HIP_CHECK(hipMemcpyAsync(cur, a[j], count * len * 8, hipMemcpyHostToDevice, stream_));
+        da[j] = cur;
+        cur += count * len;
+        FHE_HIP_CHECK(hipMemcpyAsync(cur, b[j], count * 8, hipMemcpyHostToDevice, stream_));
+        db[j] = cur;
+        cur += count;
+        if (lg) {
+            FHE_HIP_CHECK(hipMemcpyAsync(cur, large[j], count, hipMemcpyHostToDevice, stream_));
+            dl[j] = reinterpret_cast<const uint8_t*>(cur);
+        }
+        cur += (count + 7) / 8;
+    }
+    uint64_t* dao = cur;
+    uint64_t* dbo = dao + (outw - count);
+    eval_mixed_device(op, k, ptmod, count, da, db, dl, dao, dbo, extended, stream_);
+    FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, (outw - count) * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void Engine::switch_to_qn_host(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out) {
+    if (count == 0) return;
+    const size_t n = p_.n, N = p_.N;
+    uint64_t* d = grow(d_mixio_, mixiocap_, count * (N + 1 + n + 1) * 8);
+    FHE_HIP_CHECK(hipSetDevice(device_));
+    uint64_t* dbi = d + count * N;
+    uint64_t* dao = dbi + count;
+    uint64_t* dbo = dao + count * n;
+    FHE_HIP_CHECK(hipMemcpyAsync(d, a, count * N * 8, hipMemcpyHostToDevice, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(dbi, b, count * 8, hipMemcpyHostToDevice, stream_));
+    switch_to_qn_device(count, d, dbi, dao, dbo, stream_);
+    FHE_HIP_CHECK(hipMemcpyAsync(a_out, dao, count * n * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipMemcpyAsync(b_out, dbo, count * 8, hipMemcpyDeviceToHost, stream_));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 void Engine::keyswitch_workspace_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {

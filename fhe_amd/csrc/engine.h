@@ -64,6 +64,9 @@ public:
     static bool ks32_set(const Params& p);
     // the u32-sum form for power-of-two qKS above 2^16 (launch_keyswitch_w32 shapes)
     static bool ks32w_set(const Params& p);
+    // the accumulator kernels a context of this set runs on (fhe_hip_params::kernel), with the A/B
+    // environment knobs a context reads at creation (FHE_HIP_GINX3, FHE_HIP_N2K, FHE_HIP_NARROW)
+    static uint32_t kernel_kind(const Params& p);
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -114,6 +117,28 @@ public:
                         hipStream_t s);
     void eval_cmux_device(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
                           const uint64_t* a2, const uint64_t* b2, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+
+    // ---- ciphertexts mod Q as inputs (binfhe-base-scheme.cpp:92-93, 150-152, 200-201) ----
+    // SwitchCTtoqn (lwe-pke.cpp:170-178) of `count` ciphertexts a [count][N], b [count] mod Q into
+    // [count][n] / [count] mod q: ModSwitch(Q -> qKS), KeySwitch, ModSwitch(qKS -> q)
+    void switch_to_qn_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out,
+                             hipStream_t s);
+    // The reference's gate entry points on inputs of either modulus.  op: a 2-input gate (k = 2),
+    // MAJORITY / AND3 / OR3 / AND4 / OR4 (k = 2..4, plaintext modulus ptmod), CMUX (k = 3) or kOpBootstrap
+    // (BinFHEScheme::Bootstrap, k = 1, the input's plaintext modulus ptmod).  Column j: count ciphertexts,
+    // large[j] == nullptr: rows of n words mod q; otherwise rows of N words, large[j][g] != 0 marking a
+    // ciphertext mod Q (dimension N), 0 one mod q (its first n words).  Outputs [count][n] mod q, or
+    // ctExt [count][N] mod Q when extended (CMUX ignores extended, as the reference does: :180-182).
+    // Device pointers (large[j] too), asynchronous on s.
+    static constexpr int kOpBootstrap = -1;
+    void eval_mixed_device(int op, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a,
+                           const uint64_t* const* b, const uint8_t* const* large, uint64_t* a_out, uint64_t* b_out,
+                           bool extended, hipStream_t s);
+    // the same on host buffers (synchronous)
+    void eval_mixed_host(int op, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a,
+                         const uint64_t* const* b, const uint8_t* const* large, uint64_t* a_out, uint64_t* b_out,
+                         bool extended);
+    void switch_to_qn_host(size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out, uint64_t* b_out);
 
     // ---- functional bootstrapping (binfhe-base-scheme.cpp:241-521, 589-648); fb.cpp ----
     // BootstrapFunc: a [count][n] mod ctmod (power of two <= 2N), f[x] = f(x) < fmod for x < ctmod;
@@ -169,6 +194,20 @@ private:
     void build_tables();
     void build_tables_wide();
     void build_loggen();
+    // one ciphertext column switched to mod q (see eval_mixed_device): the flagged rows through
+    // SwitchCTtoqn (negated at Q first when negate; b replaced by b_large when set_b), the others copied
+    // (negated at q when negate); a_out [count][n] must not overlap the input
+    void switch_column_device(size_t count, const uint64_t* a, const uint64_t* b, uint32_t stride, const uint8_t* large,
+                              bool negate, bool set_b, uint64_t b_large, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // ctExt of workspace slots [0, count) as u64 [count][N] / [count] into device buffers
+    void ext_to_device(size_t count, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // CMUX's two NAND levels (binfhe-base-scheme.cpp:176-182); a2n / b2n: NOT ct2 given explicitly
+    // (nullptr: folded into the first NAND's input combination)
+    void cmux_levels(size_t count, const uint64_t* a0, const uint64_t* b0, const uint64_t* a1, const uint64_t* b1,
+                     const uint64_t* a2, const uint64_t* b2, const uint64_t* a2n, const uint64_t* b2n, uint64_t* a_out,
+                     uint64_t* b_out, hipStream_t s);
+    // grow-only device scratch (synchronises the context's streams before it grows)
+    uint64_t* grow(uint64_t*& ptr, size_t& cap, size_t bytes);
     // KeySwitch + ModSwitch(qKS -> q_out) of workspace slots [0, count) (q_out = 0: none)
     void keyswitch_ext(size_t count, uint64_t q_out, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
     // ctExt of workspace slots [0, count) to host u64 arrays
@@ -227,9 +266,13 @@ private:
     uint32_t* d_tvb_ = nullptr;
     uint32_t* d_ext_a_ = nullptr;
     uint32_t* d_ext_b_ = nullptr;
-    // CMUX: first-level NAND outputs [2 count][n] + [2 count]
+    // CMUX: first-level NAND outputs [2 count][n] + [2 count] (ccap_: bytes)
     size_t ccap_ = 0;
     uint64_t* d_l1_ = nullptr;
+    // mixed-modulus inputs: switched columns (eval_mixed_device) and the host entry point's staging
+    size_t mixcap_ = 0, mixiocap_ = 0;
+    uint64_t* d_mix_ = nullptr;
+    uint64_t* d_mixio_ = nullptr;
     // functional bootstrapping: test-vector table [2N] u32 and ciphertext temporaries
     uint32_t* d_tv_ = nullptr;
     size_t fbcap_ = 0;

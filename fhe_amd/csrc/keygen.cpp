@@ -261,15 +261,16 @@ void keygen_one(const Params& p, const std::vector<uint64_t>& sk, uint64_t seed,
 }  // namespace
 
 void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
-             uint64_t* b, uint32_t ptmod, uint64_t mod) {
+             uint64_t* b, uint32_t ptmod, uint64_t mod, uint32_t len) {
     const uint64_t q = mod ? mod : p.q;
+    const uint32_t n = len ? len : p.n;
     if (ptmod < 2 || ptmod > q) throw std::invalid_argument("plaintext modulus out of range");
 #pragma omp parallel for schedule(static) if (count > 64)
     for (int64_t g = 0; g < (int64_t)count; ++g) {
         Rng r(seed, T_ENC, (uint64_t)g);
-        uint64_t* ag = a + (size_t)g * p.n;
+        uint64_t* ag = a + (size_t)g * n;
         u128 acc = 0;
-        for (uint32_t i = 0; i < p.n; ++i) {
+        for (uint32_t i = 0; i < n; ++i) {
             ag[i] = r.uniform(q);
             acc += (u128)ag[i] * lift(signed_of(sk[i], p.qKS), q);
         }

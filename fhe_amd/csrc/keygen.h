@@ -96,9 +96,9 @@ void keygen_bootstrap_device(const Params& p, const std::vector<uint64_t>& sk, u
                              uint32_t* d_bsk, uint16_t* d_ksk, uint64_t* raw_bsk, uint64_t* raw_kskA,
                              uint64_t* raw_kskB, void* stream);
 // LWEEncryptionScheme::Encrypt / Decrypt (lwe-pke.cpp:103-128, 181-226) with plaintext modulus
-// ptmod and ciphertext modulus mod (0: q)
+// ptmod and ciphertext modulus mod (0: q); len: the dimension (0: n; N with skN for EncryptN's LARGE_DIM)
 void encrypt(const Params& p, const uint64_t* sk, const int* bits, size_t count, uint64_t seed, uint64_t* a,
-             uint64_t* b, uint32_t ptmod = 4, uint64_t mod = 0);
+             uint64_t* b, uint32_t ptmod = 4, uint64_t mod = 0, uint32_t len = 0);
 int64_t decrypt(const Params& p, const uint64_t* sk, const uint64_t* a, uint64_t b, uint32_t len, uint64_t mod,
                 uint32_t ptmod = 4);
 

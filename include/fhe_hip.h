@@ -218,6 +218,35 @@ int fhe_hip_eval_cmux_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a0, 
 int fhe_hip_eval_cmux_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a0, const uint64_t* d_b0,
                                    const uint64_t* d_a1, const uint64_t* d_b1, const uint64_t* d_a2,
                                    const uint64_t* d_b2, uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* ---- ciphertexts mod Q (extended outputs, LARGE_DIM encryptions) as inputs ----
+ * BinFHEScheme::EvalBinGate / EvalBinGate(ctvector) / Bootstrap switch every input whose modulus is Q
+ * to (n, q) first (binfhe-base-scheme.cpp:92-93, 150-152, 200: SwitchCTtoqn), and inputs of either
+ * modulus may be mixed within one call.
+ * SwitchCTtoqn (lwe-pke.cpp:170-178; BinFHEContext::SwitchCTtoqn, binfhecontext.cpp:254-264):
+ *   a[count][N], b[count] mod Q -> a_out[count][n], b_out[count] mod q. */
+int fhe_hip_switch_to_qn_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t* a_out,
+                               uint64_t* b_out);
+int fhe_hip_switch_to_qn_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                      uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
+/* op: OR..XNOR / XOR_FAST / XNOR_FAST (k = 2; EvalBinGate(gate, ct1, ct2, extended), :76-126),
+ * MAJORITY / AND3 / OR3 / AND4 / OR4 (k = 2..4, inputs' plaintext modulus ptmod; :129-175), CMUX (k = 3,
+ * {ct0, ct1, ct2} -> ct2 ? ct1 : ct0, extended ignored as the reference ignores it, :176-182), or
+ * FHE_HIP_OP_BOOTSTRAP (k = 1, Bootstrap(ct, extended), :190-220, the input's plaintext modulus ptmod).
+ * Column j: count ciphertexts a_in[j], b_in[j]; large == NULL or large[j] == NULL: rows of n words, all mod q;
+ * otherwise rows of N words, large[j][g] = 1 marking a ciphertext mod Q (dimension N), 0 one mod q (its first
+ * n words used).  Outputs [count][n] mod q, or ctExt [count][N] mod Q when extended.
+ * Bootstrap of an input mod Q keeps the reference's constant ct->GetModulus() >> 2 (:201), added at q by
+ * ModAddFast, so its test vector is the window's constant uv. */
+#define FHE_HIP_OP_BOOTSTRAP (-1)
+int fhe_hip_eval_mixed_batch(fhe_hip_ctx* ctx, int op, uint32_t k, uint32_t ptmod, size_t count,
+                             const uint64_t* const* a_in, const uint64_t* const* b_in, const uint8_t* const* large,
+                             uint64_t* a_out, uint64_t* b_out, int extended);
+/* device buffers (large[j] device arrays too), asynchronous on stream */
+int fhe_hip_eval_mixed_batch_device(fhe_hip_ctx* ctx, int op, uint32_t k, uint32_t ptmod, size_t count,
+                                    const uint64_t* const* d_a_in, const uint64_t* const* d_b_in,
+                                    const uint8_t* const* d_large, uint64_t* d_a_out, uint64_t* d_b_out, int extended,
+                                    void* stream);
+
 /* ---- functional bootstrapping (binfhe-base-scheme.cpp:241-521, 589-648) ----
  * Batches of `count` LWE ciphertexts a[count][n], b[count] under the context's keys; beta = 128
  * (BinFHEContext::GetBeta).  Moduli are powers of two.
@@ -322,6 +351,14 @@ int fhe_hip_encrypt_mod(int paramset, int method, const uint64_t* sk, const int*
                         uint32_t ptmod, uint64_t mod, uint64_t* a, uint64_t* b);
 int fhe_hip_decrypt_ptmod(int paramset, int method, const uint64_t* sk, const uint64_t* a, const uint64_t* b,
                           size_t count, uint32_t len, uint64_t mod, uint32_t ptmod, int64_t* out);
+/* The RLWE secret skN[N] of fhe_hip_keygen(..., seed, ...) (KeyGenN's key, binfhecontext.cpp:203-208), stored
+ * mod qKS as the key switch holds it (lwe-pke.cpp:285-286): the LWE secret of dimension-N ciphertexts mod Q.
+ * fhe_hip_decrypt_ptmod with len = N, mod = Q decrypts them under it. */
+int fhe_hip_keygen_ring_secret(int paramset, int method, uint64_t seed, uint64_t* skN);
+/* Encrypt(pk, m, LARGE_DIM, p) (binfhecontext.cpp:236-252, EncryptN): a[count][N], b[count] mod Q under skN
+ * (a symmetric encryption under the key the public key belongs to; uniform a, the reference's Gaussian) */
+int fhe_hip_encrypt_large(int paramset, int method, const uint64_t* skN, const int* bits, size_t count, uint64_t seed,
+                          uint32_t ptmod, uint64_t* a, uint64_t* b);
 
 /* ------------------------------------------------------------------------ */
 /* Device memory (Backend::Allocate/Free/CopyToDevice/CopyToHost/Synchronize, */

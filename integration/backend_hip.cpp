@@ -504,6 +504,72 @@ void BackendHIP::UnpackCiphertexts(const DeviceBuffer& packed, std::vector<LWECi
 }
 
 // ---- the fused gate path ---------------------------------------------------------------------------------
+namespace {
+// One input column in the C-ABI's mixed form (fhe_hip_eval_mixed_batch): the reference takes ciphertexts mod
+// q (dimension n) or mod Q (dimension N: extended outputs, LARGE_DIM encryptions) and switches the latter
+// first (binfhe-base-scheme.cpp:92-93, 150-152, 200).  Without any ciphertext mod Q the rows are n words;
+// with one, every row is N words and large[g] marks the ciphertexts mod Q.
+struct MixedColumn {
+    std::vector<uint64_t> a, b;
+    std::vector<uint8_t> large;
+    bool any = false;
+};
+MixedColumn mixed_column(const std::vector<LWECiphertext>& v, const std::vector<size_t>& rows, uint32_t n, uint32_t N,
+                         const NativeInteger& q, const NativeInteger& Q) {
+    MixedColumn c;
+    const size_t B = rows.size();
+    c.large.assign(B, 0);
+    for (size_t g = 0; g < B; ++g) {
+        const auto& ct = v[rows[g]];
+        if (!ct)
+            throw std::invalid_argument("BackendHIP: null ciphertext");
+        const bool lg = ct->GetModulus() == Q;
+        if (lg ? ct->GetLength() != N : (ct->GetModulus() != q || ct->GetLength() != n))
+            throw std::invalid_argument("BackendHIP: ciphertexts mod q of dimension n or mod Q of dimension N");
+        c.large[g] = lg ? 1 : 0;
+        c.any |= lg;
+    }
+    const uint32_t len = c.any ? N : n;
+    c.a.assign(B * len, 0);
+    c.b.resize(B);
+    for (size_t g = 0; g < B; ++g) {
+        const auto& ct = v[rows[g]];
+        const auto& x  = ct->GetA();
+        for (uint32_t i = 0; i < x.GetLength(); ++i)
+            c.a[g * len + i] = x[i].ConvertToInt();
+        c.b[g] = ct->GetB().ConvertToInt();
+    }
+    return c;
+}
+std::vector<size_t> all_rows(size_t B) {
+    std::vector<size_t> r(B);
+    for (size_t g = 0; g < B; ++g)
+        r[g] = g;
+    return r;
+}
+// fhe_hip_eval_mixed_batch over columns; outputs [B][n] mod q
+void eval_mixed(fhe_hip_ctx* ctx, int op, uint32_t ptmod, std::vector<MixedColumn>& cols, size_t B, uint32_t n,
+                std::vector<uint64_t>& ao, std::vector<uint64_t>& bo) {
+    std::vector<const uint64_t*> pa, pb;
+    std::vector<const uint8_t*> pl;
+    for (auto& c : cols) {
+        pa.push_back(c.a.data());
+        pb.push_back(c.b.data());
+        pl.push_back(c.any ? c.large.data() : nullptr);
+    }
+    ao.assign(B * n, 0);
+    bo.assign(B, 0);
+    const int rc = fhe_hip_eval_mixed_batch(ctx, op, (uint32_t)cols.size(), ptmod, B, pa.data(), pb.data(),
+                                            pl.data(), ao.data(), bo.data(), 0);
+    if (rc != FHE_HIP_OK) {  // BackendHIP::Check's mapping
+        const std::string msg = std::string("BackendHIP: EvalBinGate (inputs mod Q): ") + fhe_hip_last_error();
+        if (rc == FHE_HIP_ERR_INVALID_PARAM || rc == FHE_HIP_ERR_NULL_PTR)
+            throw std::invalid_argument(msg);
+        throw std::runtime_error(msg);
+    }
+}
+}  // namespace
+
 void BackendHIP::EvalBinGateBatch(BINGATE gate, const RingGSWBTKey& keys, const std::vector<LWECiphertext>& ct1,
                                   const std::vector<LWECiphertext>& ct2, std::vector<LWECiphertext>& out) {
     std::lock_guard<std::mutex> lock(mu_);
@@ -513,28 +579,25 @@ void BackendHIP::EvalBinGateBatch(BINGATE gate, const RingGSWBTKey& keys, const 
     out.resize(B);
     if (B == 0)
         return;
+    for (size_t g = 0; g < B; ++g)
+        if (ct1[g] == ct2[g])  // binfhe-base-scheme.cpp:85-86
+            throw std::invalid_argument("Input ciphertexts should be independant");
     EnsureBSK(keys.BSkey);
     EnsureKSK(keys.KSkey);
     const uint32_t n = p_.n;
-    std::vector<uint64_t> a1(B * n), b1(B), a2(B * n), b2(B), ao(B * n), bo(B);
-    for (size_t g = 0; g < B; ++g) {
-        if (ct1[g] == ct2[g])  // binfhe-base-scheme.cpp:85-86
-            throw std::invalid_argument("Input ciphertexts should be independant");
-        const auto& x = ct1[g]->GetA();
-        const auto& y = ct2[g]->GetA();
-        if (x.GetLength() != n || y.GetLength() != n)
-            throw std::invalid_argument("BackendHIP::EvalBinGateBatch: ciphertexts of dimension n");
-        for (uint32_t i = 0; i < n; ++i) {
-            a1[g * n + i] = x[i].ConvertToInt();
-            a2[g * n + i] = y[i].ConvertToInt();
-        }
-        b1[g] = ct1[g]->GetB().ConvertToInt();
-        b2[g] = ct2[g]->GetB().ConvertToInt();
+    const NativeInteger q(p_.q), Q(p_.Q);
+    const auto rows = all_rows(B);
+    std::vector<MixedColumn> cols{mixed_column(ct1, rows, n, p_.N, q, Q), mixed_column(ct2, rows, n, p_.N, q, Q)};
+    std::vector<uint64_t> ao, bo;
+    if (cols[0].any || cols[1].any) {  // SwitchCTtoqn of the inputs mod Q on the device first (:92-93)
+        eval_mixed(ctx_, static_cast<int>(gate), 4, cols, B, n, ao, bo);
+    } else {
+        ao.assign(B * n, 0);
+        bo.assign(B, 0);
+        Check(fhe_hip_eval_bingate_batch(ctx_, static_cast<int>(gate), B, cols[0].a.data(), cols[0].b.data(),
+                                         cols[1].a.data(), cols[1].b.data(), ao.data(), bo.data()),
+              "EvalBinGateBatch");
     }
-    Check(fhe_hip_eval_bingate_batch(ctx_, static_cast<int>(gate), B, a1.data(), b1.data(), a2.data(), b2.data(),
-                                     ao.data(), bo.data()),
-          "EvalBinGateBatch");
-    const NativeInteger q(p_.q);
     for (size_t g = 0; g < B; ++g)
         out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
 }
@@ -554,12 +617,6 @@ void flatten(const std::vector<LWECiphertext>& v, const std::vector<size_t>& row
             a[g * n + i] = x[i].ConvertToInt();
         b[g] = ct->GetB().ConvertToInt();
     }
-}
-std::vector<size_t> all_rows(size_t B) {
-    std::vector<size_t> r(B);
-    for (size_t g = 0; g < B; ++g)
-        r[g] = g;
-    return r;
 }
 }  // namespace
 
@@ -608,24 +665,34 @@ void BackendHIP::RefreshBatch(const RingGSWBTKey& keys, const std::vector<LWECip
     out.resize(B);
     if (B == 0)
         return;
-    const NativeInteger q(p_.q);
-    for (const auto& ct : cts) {
-        if (!ct)
+    const NativeInteger q(p_.q), Q(p_.Q);
+    // BinFHEScheme::Bootstrap (binfhe-base-scheme.cpp:190-220) per ciphertext of modulus q or Q (switched first,
+    // :200, its constant Q >> 2 kept, :201); the extraction's b is Q/(2p) + 1 for the input's own plaintext
+    // modulus p (:210), so one device call per distinct p
+    std::vector<std::pair<uint64_t, size_t>> order(B);
+    for (size_t g = 0; g < B; ++g) {
+        if (!cts[g])
             throw std::invalid_argument("Ciphertext is empty");
-        if (ct->GetModulus() != q)  // the Q-modulus input of :199 (SwitchCTtoqn first) is not taken here
-            throw std::invalid_argument("BackendHIP::RefreshBatch: ciphertexts mod q");
-        if (ct->GetptModulus() != 4)  // the window and b constant of the device path are p = 4's (:205, :211)
-            throw std::invalid_argument("BackendHIP::RefreshBatch: plaintext modulus 4");
+        order[g] = {cts[g]->GetptModulus().ConvertToInt(), g};
     }
+    std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
     EnsureBSK(keys.BSkey);
     EnsureKSK(keys.KSkey);
     const uint32_t n = p_.n;
-    std::vector<uint64_t> a(B * n), b(B), ao(B * n), bo(B);
-    flatten(cts, all_rows(B), n, a.data(), b.data());
-    Check(fhe_hip_bootstrap_batch(ctx_, B, a.data(), b.data(), ao.data(), bo.data()), "RefreshBatch");
-    for (size_t g = 0; g < B; ++g) {
-        out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
-        out[g]->SetptModulus(cts[g]->GetptModulus());
+    for (size_t s0 = 0; s0 < B;) {
+        const uint64_t p = order[s0].first;
+        std::vector<size_t> rows;
+        for (; s0 < B && order[s0].first == p; ++s0)
+            rows.push_back(order[s0].second);
+        if (p == 0 || p > 0xffffffffull)
+            throw std::invalid_argument("BackendHIP::RefreshBatch: plaintext modulus");
+        std::vector<MixedColumn> cols{mixed_column(cts, rows, n, p_.N, q, Q)};
+        std::vector<uint64_t> ao, bo;
+        eval_mixed(ctx_, FHE_HIP_OP_BOOTSTRAP, (uint32_t)p, cols, rows.size(), n, ao, bo);
+        for (size_t g = 0; g < rows.size(); ++g) {
+            out[rows[g]] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
+            out[rows[g]]->SetptModulus(NativeInteger(p));
+        }
     }
 }
 
@@ -646,14 +713,16 @@ void BackendHIP::EvalCMUXBatch(const RingGSWBTKey& keys, const std::vector<LWECi
     EnsureKSK(keys.KSkey);
     const uint32_t n = p_.n;
     const auto rows  = all_rows(B);
-    std::vector<uint64_t> a0(B * n), b0(B), a1(B * n), b1(B), a2(B * n), b2(B), ao(B * n), bo(B);
-    flatten(ct0, rows, n, a0.data(), b0.data());
-    flatten(ct1, rows, n, a1.data(), b1.data());
-    flatten(ct2, rows, n, a2.data(), b2.data());
-    Check(fhe_hip_eval_cmux_batch(ctx_, B, a0.data(), b0.data(), a1.data(), b1.data(), a2.data(), b2.data(),
-                                  ao.data(), bo.data()),
-          "EvalCMUXBatch");
-    const NativeInteger q(p_.q);
+    const NativeInteger q(p_.q), Q(p_.Q);
+    std::vector<MixedColumn> cols{mixed_column(ct0, rows, n, p_.N, q, Q), mixed_column(ct1, rows, n, p_.N, q, Q),
+                                  mixed_column(ct2, rows, n, p_.N, q, Q)};
+    std::vector<uint64_t> ao(B * n), bo(B);
+    if (cols[0].any || cols[1].any || cols[2].any)  // NAND's SwitchCTtoqn of inputs mod Q (:180-182, :92-93)
+        eval_mixed(ctx_, static_cast<int>(CMUX), 4, cols, B, n, ao, bo);
+    else
+        Check(fhe_hip_eval_cmux_batch(ctx_, B, cols[0].a.data(), cols[0].b.data(), cols[1].a.data(), cols[1].b.data(),
+                                      cols[2].a.data(), cols[2].b.data(), ao.data(), bo.data()),
+              "EvalCMUXBatch");
     for (size_t g = 0; g < B; ++g)
         out[g] = std::make_shared<LWECiphertextImpl>(vec_from(ao.data() + g * n, n, q), NativeInteger(bo[g]));
 }

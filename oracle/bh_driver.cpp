@@ -515,6 +515,65 @@ int bh_eval_gates_routed(void* h, int gate, size_t count, const uint64_t* a1, co
     });
 }
 
+// Ciphertexts mod Q through the routed callers (binfhe-base-scheme.cpp:92-93, 180-182, 200-201): k columns of
+// count ciphertexts, rows of N words, large[j][g] != 0 marking a ciphertext mod Q (dimension N), 0 one mod q
+// (its first n words), every input of plaintext modulus ptmod.  op < 6: EvalBinGateBatchHIP vs the reference's
+// EvalBinGateBatch; op = 13 (CMUX, k = 3): EvalCMUXBatchHIP vs EvalCMUXBatch; op = -1 (k = 1):
+// BackendHIP::RefreshBatch vs BinFHEContext::Bootstrap.  Outputs [count][n]; *ok = the routed call succeeded
+int bh_eval_mixed_routed(void* h, int op, uint32_t k, uint32_t ptmod, size_t count, const uint64_t* const* a,
+                         const uint64_t* const* b, const uint8_t* const* large, uint64_t* ga, uint64_t* gb,
+                         uint64_t* ra, uint64_t* rb, int* ok) {
+    return guarded([&] {
+        BinFHEContext& cc = CC(h);
+        auto lp           = cc.GetParams()->GetLWEParams();
+        const uint32_t n = lp->Getn(), N = lp->GetN();
+        const NativeInteger q = lp->Getq(), Q = lp->GetQ();
+        std::vector<std::vector<LWECiphertext>> cols(k);
+        for (uint32_t j = 0; j < k; ++j)
+            for (size_t g = 0; g < count; ++g) {
+                const bool lg = large[j][g] != 0;
+                auto ct = std::make_shared<LWECiphertextImpl>(vec_from(a[j] + g * N, lg ? N : n, lg ? Q : q),
+                                                              NativeInteger(b[j][g]));
+                ct->SetptModulus(ptmod);
+                cols[j].push_back(ct);
+            }
+        std::vector<LWECiphertext> out, ref(count);
+        *ok = 0;
+        if (op == -1) {
+            RingGSWBTKey keys;
+            keys.BSkey = cc.GetRefreshKey();
+            keys.KSkey = cc.GetSwitchKey();
+            g_be->RefreshBatch(keys, cols[0], out);
+            *ok = out.size() == count;
+            for (size_t g = 0; g < count; ++g)
+                *ok = *ok && out[g]->GetptModulus() == ptmod;
+#pragma omp parallel for
+            for (size_t g = 0; g < count; ++g)
+                ref[g] = cc.Bootstrap(cols[0][g]);
+        }
+        else if (op == CMUX) {
+            const BatchResult r = EvalCMUXBatchHIP(cc, cols[0], cols[1], cols[2], out, 0);
+            *ok = r.success && r.processed == count;
+            if (!r.success)
+                throw std::runtime_error("EvalCMUXBatchHIP: " + r.error);
+            const BatchResult rr = EvalCMUXBatch(cc, cols[0], cols[1], cols[2], ref, 0);
+            if (!rr.success)
+                throw std::runtime_error("reference EvalCMUXBatch: " + rr.error);
+        }
+        else {
+            const BatchResult r = EvalBinGateBatchHIP(cc, static_cast<BINGATE>(op), cols[0], cols[1], out, 0);
+            *ok = r.success && r.processed == count;
+            if (!r.success)
+                throw std::runtime_error("EvalBinGateBatchHIP: " + r.error);
+            const BatchResult rr = EvalBinGateBatch(cc, static_cast<BINGATE>(op), cols[0], cols[1], ref, 0);
+            if (!rr.success)
+                throw std::runtime_error("reference EvalBinGateBatch: " + rr.error);
+        }
+        lwe_out(out, ga, gb);
+        lwe_out(ref, ra, rb);
+    });
+}
+
 // PackCiphertexts -> UnpackCiphertexts and PackBootstrappingKey -> UnpackBootstrappingKey round trips
 // through device memory; *ok bit 0: ciphertexts equal, bit 1: key equal to the context's refresh key
 int bh_pack_roundtrip(void* h, size_t count, const uint64_t* a, const uint64_t* b, int* ok) {

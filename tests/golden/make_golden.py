@@ -414,6 +414,112 @@ def make_config3(nthreads=8):
     print("config3 ok", C3_GATES, flush=True)
 
 
+# Ciphertexts mod Q as inputs (binfhe-base-scheme.cpp:92-93, 150-152, 200-201): the flows of the
+# reference's UnitTestFHEWExtended.cpp:37-153 (extended = true outputs chained into the next gate, SMALL_DIM
+# and LARGE_DIM encryptions mixed within one call) as batches, plus every 2-input gate, MAJORITY and CMUX on
+# mixed inputs.  LARGE_DIM ciphertexts are encryptions under the keys' RLWE secret skN (dimension N, mod Q),
+# what Encrypt(pk, m, LARGE_DIM, p) makes (binfhecontext.cpp:236-252).
+MIXED_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "std192": (9, GINX),
+              "std256q": (18, GINX)}
+MIXED_COUNT = 8
+OP_BOOTSTRAP = -1
+
+
+def mixed_column(ps, m, sk, skN, bits, flags, seed, p):
+    """one input column: rows of N words; flagged rows are LARGE_DIM encryptions (mod Q), the others
+    SMALL_DIM ones (mod q, first n words)"""
+    from fhe_amd import binfhe as bf
+    P = bf.params(ps, m)
+    sa, sb = bf.encrypt(ps, m, sk, bits, seed, p)
+    la, lb = bf.encrypt_large(ps, m, skN, bits, seed + 0x1000, p)
+    a = np.zeros((len(bits), P.N), np.uint64)
+    a[:, :P.n] = sa
+    a[flags == 1] = la[flags == 1]
+    b = np.where(flags == 1, lb, sb).astype(np.uint64)
+    return a, b
+
+
+def mixed_cases(ps, m, key_seed, count=MIXED_COUNT):
+    """keys, skN and the input-only cases: name -> (op, ptmod, bits [k][count], columns [(a, b, flags)])"""
+    from fhe_amd import binfhe as bf
+    keys = bf.keygen(ps, m, key_seed)
+    skN = bf.keygen_ring_secret(ps, m, key_seed)
+    rng = np.random.default_rng(key_seed ^ 0x3D)
+    cases = {}
+
+    def cols(name, op, k, p, pattern=None):
+        bits = rng.integers(0, 2, size=(k, count))
+        fl = rng.integers(0, 2, size=(k, count)).astype(np.uint8) if pattern is None else np.array(pattern, np.uint8)
+        fl[:, 0] = 1   # every column has a ciphertext mod Q and (below) one mod q
+        fl[:, 1] = 0
+        base = key_seed + 0x500 + 16 * len(cases)
+        c = [mixed_column(ps, m, keys.sk, skN, bits[j], fl[j], base + j, p) + (fl[j],) for j in range(k)]
+        cases[name] = (op, p, bits, c)
+
+    for gname, g in GATES.items():
+        cols(f"gate_{gname}", g, 2, 4)
+    cols("majority", 6, 3, 4)
+    cols("cmux", 13, 3, 4)
+    cols("boot", OP_BOOTSTRAP, 1, 4)
+    cols("boot_p8", OP_BOOTSTRAP, 1, 8)
+    # UnitTestFHEWExtended flows: EvalBinGate2 (p = 4: small, large), EvalBinGate3 (p = 6: small, large, small),
+    # EvalBinGate4 (p = 8: small, large, small, large); the BootStrap test is "boot" with its large rows
+    cols("flow2", None, 2, 4, [[0] * count, [1] * count])
+    cols("flow3", None, 3, 6, [[0] * count, [1] * count, [0] * count])
+    cols("flow4", None, 4, 8, [[0] * count, [1] * count, [0] * count, [1] * count])
+    return keys, skN, cases
+
+
+FLOW_GATES = {"flow2": (0, 1), "flow3": (8, 7), "flow4": (10, 9)}   # (OR, AND), (OR3, AND3), (OR4, AND4)
+
+
+def make_mixed(names=("std128", "lmkcdey")):
+    for name in names:
+        ps, m = MIXED_SETS[name]
+        key_seed = 0xB00E0000 + ps + (m << 8)
+        keys, skN, cases = mixed_cases(ps, m, key_seed)
+        ref = Ref(ps, m)
+        ref.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        out = {"paramset": ps, "method": m, "key_seed": np.uint64(key_seed),
+               "keys_sha": np.array(sha(keys.bsk) + sha(keys.kskA) + sha(keys.kskB)), "skN_sha": np.array(sha(skN))}
+        for cname, (op, p, bits, c) in cases.items():
+            A = [x[0] for x in c]
+            B = [x[1] for x in c]
+            F = [x[2] for x in c]
+            out[f"{cname}_in_sha"] = np.array("".join(sha(x) for x in A + B))
+            out[f"{cname}_bits"] = bits
+            out[f"{cname}_flags"] = np.array(F)
+            if cname in FLOW_GATES:
+                # UnitTestFHEWExtended.cpp:53-59: ct11 = G1(v, extended), ct12 = G2(v, extended) with the
+                # 2-input form taking (small, large) then (large, small), then NAND(ct11, ct12, false)
+                g1, g2 = FLOW_GATES[cname]
+                if cname == "flow2":
+                    e1 = ref.eval_mixed(g1, A, B, F, p, extended=True)
+                    e2 = ref.eval_mixed(g2, A[::-1], B[::-1], F[::-1], p, extended=True)
+                else:
+                    e1 = ref.eval_mixed(g1, A, B, F, p, extended=True)
+                    e2 = ref.eval_mixed(g2, A, B, F, p, extended=True)
+                ones = np.ones(len(B[0]), np.uint8)
+                fo = ref.eval_mixed(3, [e1[0], e2[0]], [e1[1], e2[1]], [ones, ones], 4)
+                out[f"{cname}_ext1_sha"] = np.array(sha(e1[0]) + sha(e1[1]))
+                out[f"{cname}_ext2_sha"] = np.array(sha(e2[0]) + sha(e2[1]))
+                out[f"{cname}_out_a"], out[f"{cname}_out_b"] = fo
+                out[f"{cname}_dec"] = np.array([ref.decrypt(keys.sk, fo[0][i], fo[1][i], ref.q) for i in range(len(fo[1]))])
+                print(name, cname, "NAND of the chained outputs decrypts:", list(out[f"{cname}_dec"]), flush=True)
+                continue
+            ao, bo = ref.eval_mixed(op, A, B, F, p)
+            out[f"{cname}_out_a"], out[f"{cname}_out_b"] = ao, bo
+            out[f"{cname}_dec"] = np.array([ref.decrypt(keys.sk, ao[i], bo[i], ref.q, p if op == OP_BOOTSTRAP else 4)
+                                            for i in range(len(bo))])
+            if op != 13:   # CMUX ignores extended
+                ea, eb = ref.eval_mixed(op, A, B, F, p, extended=True)
+                out[f"{cname}_ext_sha"] = np.array(sha(ea) + sha(eb))
+                out[f"{cname}_ext_a0"] = ea[0]
+            print(name, cname, "decrypts:", list(out[f"{cname}_dec"]), flush=True)
+        np.savez_compressed(os.path.join(HERE, f"mixed_{name}.npz"), **out)
+        print(name, "mixed ok", flush=True)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "config3":
         make_config3()
@@ -436,5 +542,7 @@ if __name__ == "__main__":
         make_fb(sys.argv[2:] or ("std128",))
     if what == "large":
         make_large(sys.argv[2:] or tuple(LARGE_SETS))
+    if what == "mixed":
+        make_mixed(sys.argv[2:] or tuple(MIXED_SETS))
     sys.stdout.flush()
     os._exit(0)   # skip interpreter teardown: two OpenMP runtimes (reference + fhe_amd) in one process

@@ -214,6 +214,23 @@ class Ref:
                                              ctypes.c_int(nthreads)))
         return ao, bo
 
+    def eval_mixed(self, op, a_list, b_list, large, ptmod=4, extended=False, nthreads=0):
+        """ref_eval_mixed: EvalBinGate / EvalBinGate(ctvector) / Bootstrap (op = -1) on columns whose rows may
+        be mod Q (large[j][g] = 1; such a column has rows of N words, large[j] None: rows of n words mod q)"""
+        cnt = len(b_list[0])
+        L = self.N if (extended and op != 13) else self.n
+        ao = np.zeros((cnt, L), np.uint64)
+        bo = np.zeros(cnt, np.uint64)
+        a_list = [np.ascontiguousarray(x, np.uint64) for x in a_list]
+        b_list = [np.ascontiguousarray(x, np.uint64) for x in b_list]
+        flags = [None if large is None or large[j] is None else np.ascontiguousarray(large[j], np.uint8)
+                 for j in range(len(a_list))]
+        lp = (vp * len(flags))(*[f.ctypes.data if f is not None else None for f in flags])
+        self._chk(self.L.ref_eval_mixed(self.h, ctypes.c_int(op), ctypes.c_uint32(len(a_list)), ctypes.c_uint32(ptmod),
+                                        ctypes.c_size_t(cnt), _ptrs(a_list), _ptrs(b_list), lp, _p(ao), _p(bo),
+                                        ctypes.c_int(int(extended)), ctypes.c_int(nthreads)))
+        return ao, bo
+
     def decrypt(self, sk, a, b, mod, ptmod=4):
         r = ctypes.c_int64()
         self._chk(self.L.ref_decrypt_p(self.h, _p(np.ascontiguousarray(sk, np.uint64)),

@@ -35,12 +35,15 @@ u64 = ctypes.c_uint64
 STD128, STD128_LMKCDEY, GINX, LMKCDEY = 3, 21, 2, 3
 BH = ["bh_register", "bh_unregister", "bh_info", "bh_memory_roundtrip", "bh_blind_rotate", "bh_external_product",
       "bh_keyswitch", "bh_modswitch", "bh_eval_gates", "bh_pack_roundtrip", "bh_last_error", "bh_bootstrap_init",
-      "bh_batch_callers", "bh_eval_gates_routed"]
+      "bh_batch_callers", "bh_eval_gates_routed", "bh_eval_mixed_routed"]
 STD128_AP, AP = 2, 1
 # name -> (paramset, method) (binfhe-constants.h:49-95); "_refkeys": keys from the reference's BTKeyGen
 BACKEND_SETS = {"std128": (STD128, GINX), "lmkcdey": (STD128_LMKCDEY, LMKCDEY), "std128_refkeys": (STD128, GINX),
                 "ap": (STD128_AP, AP), "std128_3": (4, GINX), "std128_4_lmkcdey": (23, LMKCDEY),
-                "std192": (9, GINX), "std192_lmkcdey": (27, LMKCDEY)}
+                "std192": (9, GINX), "std192_lmkcdey": (27, LMKCDEY),
+                # K1w (N = 2048, accumulator in registers, accumulator-I/O instantiations): seam parity with the
+                # reference's EvalAcc directly, not only with the K5 GPU path
+                "std256q": (18, GINX), "std256q_3_lmkcdey": (37, LMKCDEY)}
 
 needs_backend = pytest.mark.skipif(not backend_available(), reason="oracle/_ref/libbackend_hip.so not built")
 
@@ -463,6 +466,53 @@ def test_gpu_backend_routed_cmux_and_refresh(bset):
     b.chk(b.L.bh_refresh(b.h, sz(count), P(cts[0][0]), P(cts[0][1]), P(ga), P(gb), P(ra), P(rb)))
     assert np.array_equal(ga, ra) and np.array_equal(gb, rb), name
     assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), bits[:, 0]), name
+
+
+@pytest.mark.gpu
+@needs_backend
+@pytest.mark.parametrize("bset", ROUTED, indirect=True)
+def test_gpu_backend_routed_inputs_mod_Q(bset):
+    """Ciphertexts mod Q (dimension N: extended outputs, LARGE_DIM encryptions) mixed with ones mod q in one
+    batch through the routed callers: EvalBinGateBatchHIP (every 2-input gate), EvalCMUXBatchHIP and
+    BackendHIP::RefreshBatch (plaintext moduli 4 and 8) == the reference's EvalBinGateBatch / EvalCMUXBatch /
+    Bootstrap, which switch those inputs first (binfhe-base-scheme.cpp:92-93, 180-182, 200-201)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import mixed_column
+    from fhe_amd import binfhe as bf
+    name = bset
+    b = backend(name)
+    r = b.ref
+    skN = bf.keygen_ring_secret(b.ps, b.m, 0xB0070000 + b.ps)
+    rng = np.random.default_rng(47)
+    count = 12
+
+    def run(op, k, p):
+        bits = rng.integers(0, 2, (k, count))
+        fl = rng.integers(0, 2, (k, count)).astype(np.uint8)
+        fl[:, 0], fl[:, 1] = 1, 0
+        cols = [mixed_column(b.ps, b.m, b.sk, skN, bits[j], fl[j], 900 + 10 * k + j, p) for j in range(k)]
+        A = [c[0] for c in cols]
+        B = [c[1] for c in cols]
+        ptr = lambda xs: (vp * k)(*[x.ctypes.data for x in xs])   # noqa: E731
+        ga, gb = np.zeros((count, r.n), np.uint64), np.zeros(count, np.uint64)
+        ra, rb = np.zeros_like(ga), np.zeros_like(gb)
+        ok = ctypes.c_int()
+        b.chk(b.L.bh_eval_mixed_routed(b.h, op, k, p, sz(count), ptr(A), ptr(B), ptr(list(fl)), P(ga), P(gb), P(ra),
+                                       P(rb), ctypes.byref(ok)))
+        assert ok.value == 1, (name, op)
+        assert np.array_equal(ga, ra) and np.array_equal(gb, rb), (name, op, p)
+        return bits, fl, ga, gb
+
+    for gate in range(6):
+        run(gate, 2, 4)
+    bits, fl, ga, gb = run(13, 3, 4)
+    assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb), np.where(bits[2] == 1, bits[1], bits[0])), name
+    for p in (4, 8):   # p = 8: the reference's window stays p = 4's (:205), only b uses p (:210): parity only
+        bits, fl, ga, gb = run(-1, 1, p)
+        small = fl[0] == 0
+        if p == 4:
+            assert np.array_equal(bf.decrypt(b.ps, b.m, b.sk, ga, gb)[small], bits[0][small]), name
 
 
 @pytest.mark.gpu

@@ -57,3 +57,68 @@ def test_kernel_path_per_parameter_set():
     assert bf.kernel_path(34, bf.LMKCDEY) == 4        # STD256_3_LMKCDEY (29-bit Q, 3 digits): K1w, forward reduced 3x
     assert bf.kernel_path(35, bf.LMKCDEY) == 4        # STD256_4_LMKCDEY (29-bit Q, 3 digits)
     assert bf.uses_fast_kernels(bf.STD128, bf.GINX) and not bf.uses_fast_kernels(STD256, bf.GINX)
+
+
+def test_no_stream_ordered_pool_allocations():
+    """Round 4's zero read-back ("A block read back as zeros"): a seam call's device scratch came
+    from the stream-ordered pool (hipMallocAsync / hipFreeAsync per call), whose default release threshold
+    of 0 lets a stream / event synchronize hand pool memory back to the driver.  No product code uses that
+    allocator now: every device buffer is a hipMalloc'd, context-owned, grow-only allocation freed only after
+    the context's streams are synchronised (Engine::grow / ensure_work, fhe_hip_ctx::scratch)."""
+    import subprocess
+    from fhe_amd import lib_path
+    und = subprocess.run(["nm", "-D", "--undefined-only", lib_path], capture_output=True, text=True,
+                         check=True).stdout
+    assert "hipMallocAsync" not in und and "hipFreeAsync" not in und and "hipMallocFromPoolAsync" not in und
+    for d in ("fhe_amd/csrc", "integration"):
+        for f in os.listdir(os.path.join(ROOT, d)):
+            if f.endswith((".cpp", ".hip", ".h")):
+                txt = re.sub(r"//.*", "", open(os.path.join(ROOT, d, f)).read())
+                assert "hipMallocAsync" not in txt and "hipFreeAsync" not in txt, f
+
+
+import numpy as np  # noqa: E402
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ps,m", [(27, 3), (3, 2)])   # STD192_LMKCDEY (where r04 saw the zeros), STD128 GINX
+def test_gpu_seam_call_sequence_repeats_on_one_context(ps, m):
+    """the host-buffer seam calls (ExternalProduct, BlindRotate, BlindRotate with null accumulators, gates,
+    SwitchCTtoqn) interleaved three times on ONE context, each call's output equal to its first run: the
+    sequence that read a block back as zeros in round 4 (test_backend's std192_lmkcdey null accumulators)"""
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import check, ptr
+    L = bf.L()
+    L.fhe_hip_blind_rotate_init_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_void_p] * 3
+    keys = bf.keygen(ps, m, 0xB0070000 + ps)
+    P = bf.params(ps, m)
+    e = bf.GateEngine(ps, m, 0)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    rng = np.random.default_rng(5)
+    bits = rng.integers(0, 2, 5)
+    a, b = bf.encrypt(ps, m, keys.sk, bits, 3)
+    amod = 2 * P.N if m == 3 else P.q
+    acc_a = rng.integers(0, amod, (5, P.n), dtype=np.uint64)
+    acc = rng.integers(0, P.Q, (5, 2, P.N), dtype=np.uint64)
+    rgsw = rng.integers(0, P.Q, (3, 2 * (P.digitsG - 1), 2, P.N), dtype=np.uint64)
+    rlwe = rng.integers(0, P.Q, (3, 2, P.N), dtype=np.uint64)
+    skN = bf.keygen_ring_secret(ps, m, 0xB0070000 + ps)
+    la, lb = bf.encrypt_large(ps, m, skN, bits, 4)
+
+    def init(cnt):
+        out = np.zeros((cnt, 2, P.N), np.uint64)
+        check(L.fhe_hip_blind_rotate_init_batch(e._h, cnt, ptr(a[:cnt].copy()), ptr(b[:cnt].copy()), ptr(out)))
+        return out
+
+    def round_():
+        return [e.external_product(rgsw, rlwe), e.blind_rotate_acc(acc_a, amod, acc), init(1), init(5),
+                e.eval_gate(bf.AND, a, b, a[::-1].copy(), b[::-1].copy()), init(1), e.switch_to_qn(la, lb)]
+
+    first = round_()
+    assert np.any(first[2] != 0) and np.any(first[3] != 0)
+    for _ in range(2):
+        for x, y in zip(round_(), first):
+            for u, v in zip(x if isinstance(x, tuple) else (x,), y if isinstance(y, tuple) else (y,)):
+                assert np.array_equal(u, v)
+    e.close()

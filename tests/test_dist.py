@@ -127,3 +127,34 @@ def test_gpu_gloo_world2_engine_shards_bit_exact(tmp_path):
         p = np.load(tmp_path / f"e{r}.npz")
         assert float(p["t"]) == float(world)
         assert sha(p["ao"]) + sha(p["bo"]) == str(g["shard_sha"][r]), r
+
+
+def test_bench_reads_the_newest_pmc_summary_in_either_shape(tmp_path, monkeypatch):
+    """bench.py's roofline.traffic / valu_busy_pmc come from the newest round's PMC summary, whether it was
+    committed in tools/pmc_traffic.py's full form ({"kernels": {...}}) or as its bare kernel map"""
+    import glob
+    import json
+    import bench
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                                          "*pmc_traffic*.json")))
+    newest = None
+    for f in files:
+        d = json.load(open(f))
+        ks = d.get("kernels") if isinstance(d.get("kernels"), dict) else d
+        if isinstance(ks.get("k_blind_rotate_ginx"), dict):
+            newest = ks["k_blind_rotate_ginx"]
+    assert newest is not None
+    v, b = bench.pmc_summary("k_blind_rotate_ginx", "hbm_bytes_per_launch")
+    assert (v, b) == (newest["hbm_bytes_per_launch"], newest["batch"])
+    assert bench.pmc_traffic("k_blind_rotate_ginx", b) == newest["hbm_bytes_per_launch"]
+    assert bench.pmc_valu_busy("k_blind_rotate_ginx") == newest["valu_busy"]
+    # both shapes, the later round winning
+    (tmp_path / "profiles").mkdir()
+    full = {"round": "r98", "kernels": {"kx": {"batch": 10, "hbm_bytes_per_launch": 100, "valu_busy": 0.5}}}
+    bare = {"kx": {"batch": 20, "hbm_bytes_per_launch": 400, "valu_busy": 0.7}}
+    json.dump(full, open(tmp_path / "profiles" / "r98_pmc_traffic.json", "w"))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_summary("kx", "hbm_bytes_per_launch") == (100, 10)
+    json.dump(bare, open(tmp_path / "profiles" / "r99_pmc_traffic.json", "w"))
+    assert bench.pmc_summary("kx", "hbm_bytes_per_launch") == (400, 20)
+    assert bench.pmc_traffic("kx", 40) == 800

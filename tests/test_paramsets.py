@@ -195,6 +195,9 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
     amod = 2 * P.N if m == 3 else P.q
     acc_a = rng.integers(0, amod, (5, P.n), dtype=np.uint64)
     acc = rng.integers(0, P.Q, (5, 2, P.N), dtype=np.uint64)
+    # GINX seam calls with ciphertexts mod 2N as well (EvalAcc reads a_i with the ciphertext's modulus): the
+    # rows whose K1w has no q = 2N instantiation (2 retained digits) must fall back, not read past their keys
+    acc_a2 = rng.integers(0, 2 * P.N, (5, P.n), dtype=np.uint64)
     res = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("FHE_HIP_N2K", flag)
@@ -203,6 +206,8 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
         res[flag] = [(e.eval_gate(gate, a1, b1, a2, b2), e.eval_gate_extended(gate, a1, b1, a2, b2))
                      for gate in GATES.values()]
         res[flag].append(((e.blind_rotate_acc(acc_a, amod, acc),), ))
+        if m == 2 and amod != 2 * P.N:
+            res[flag].append(((e.blind_rotate_acc(acc_a2, 2 * P.N, acc),), ))
         e.close()
     for (gname, gate), (fast, ref) in zip(GATES.items(), zip(res["1"], res["0"])):
         for u, v in zip(fast, ref):
@@ -210,4 +215,5 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
                 assert np.array_equal(s, t), gname
         dec = bf.decrypt(ps, m, keys.sk, fast[0][0], fast[0][1])
         assert np.array_equal(dec, TRUTH[gate](x1, x2)), gname
-    assert np.array_equal(res["1"][-1][0][0], res["0"][-1][0][0])
+    for u, v in zip(res["1"][len(GATES):], res["0"][len(GATES):]):
+        assert np.array_equal(u[0][0], v[0][0])
