@@ -126,6 +126,8 @@ def _setup(L):
                                            ctypes.c_int]
     L.fhe_hip_eval_mixed_batch_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, sz, vp, vp, vp,
                                                   vp, vp, ctypes.c_int, vp]
+    L.fhe_hip_eval_func_multi_batch.argtypes = [vp, sz, vp, vp, u64, vp, sz, ctypes.c_uint32, vp, vp]
+    L.fhe_hip_eval_func_multi_batch_device.argtypes = [vp, sz, vp, vp, u64, vp, sz, ctypes.c_uint32, vp, vp, vp]
     L.fhe_hip_keygen_ring_secret.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp]
     L.fhe_hip_encrypt_large.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, ctypes.c_uint32, vp, vp]
     L._binfhe_ready = True
@@ -552,6 +554,16 @@ class GateEngine:
         ao, bo = self._fb_out(b)
         check(L().fhe_hip_eval_func_batch(self._h, len(b), ptr(a), ptr(b), q_in, ptr(lut), len(lut), ptr(ao), ptr(bo)))
         return ao[0], bo[0]
+
+    def eval_func_multi(self, a, b, q_in, luts):
+        """EvalFuncMultiOutputBatch: every LUT of luts [L][q_in] on every input; rows i L + j"""
+        a, b = _u64(a), _u64(b)
+        luts = _u64(np.atleast_2d(luts))
+        L_, cnt = luts.shape[0], len(b)
+        ao, bo = np.zeros((cnt * L_, self.params.n), np.uint64), np.zeros(cnt * L_, np.uint64)
+        check(L().fhe_hip_eval_func_multi_batch(self._h, cnt, ptr(a), ptr(b), q_in, ptr(luts), luts.shape[1], L_,
+                                                 ptr(ao), ptr(bo)))
+        return ao, bo
 
     def eval_floor(self, a, b, mod, roundbits=0):
         a, b = _u64(a), _u64(b)

@@ -83,6 +83,9 @@ struct GateArgs {
     // contents -- the seam's null accumulators (BootstrapBatch, batch.cpp:77-86); the final
     // accumulator still goes to acc_io
     uint32_t acc_tv;
+    // BootstrapFunc with several tables (EvalFuncMultiOutputBatch, batch.cpp:141-174): tv_mod > 1 cycles
+    // gate g through table g % tv_mod, at tv + (g % tv_mod) ctmod (tv64 likewise); 0 / 1: the one table
+    uint32_t tv_mod;
 };
 
 // The LWE ciphertext a gate bootstraps: ct = sum_j (-1)^{neg_j} ct_j + (0, boff) mod q, then
@@ -190,6 +193,9 @@ hipError_t launch_lwe_reduce(const uint64_t* a, const uint64_t* b, uint64_t* ao,
 hipError_t launch_lwe_sub(const uint64_t* xa, const uint64_t* xb, const uint64_t* ya, const uint64_t* yb, uint64_t* oa,
                           uint64_t* ob, uint64_t m, uint32_t len, size_t count, hipStream_t s);
 hipError_t launch_lwe_addb(uint64_t* b, uint64_t c, uint64_t m, size_t count, hipStream_t s);
+//   repeat: row i of [count][n] to rows i L .. i L + L - 1 of [count L][n] (EvalFuncMultiOutput's copies)
+hipError_t launch_lwe_repeat(const uint64_t* a, const uint64_t* b, uint32_t n, size_t count, uint32_t L, uint64_t* ao,
+                             uint64_t* bo, hipStream_t s);
 // u64 [count][len] / [count] values below 2^32 -> u32 (the 64-bit path's ctExt mod qKS <= 2^16 into
 // the 32-bit key switch's input, for the digitsG = 4 sets of launch_blind_rotate_ginx3)
 hipError_t launch_narrow_u32(const uint64_t* a, const uint64_t* b, uint32_t* ao, uint32_t* bo, uint32_t len, size_t count,

@@ -49,6 +49,7 @@ struct WideArgs {
     // initial one is read from there too unless acc_tv (then the test vector above, as for a gate)
     uint64_t* acc_io;
     uint32_t acc_tv;
+    uint32_t tv_mod;             // GateArgs::tv_mod: gate g reads table tv + (g % tv_mod) ctmod
 };
 
 // bsk: [n][2][dG2][2][N] Montgomery keys, u64 words (u32 with t.narrow)

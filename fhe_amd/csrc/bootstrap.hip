@@ -589,13 +589,15 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
         acc_load(acc, g, gate, h, l, T.ninvR, m);
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        // EvalFuncMultiOutput: table gate % tv_mod (GateArgs::tv_mod)
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             const uint32_t x = (uint32_t)(r << 5) | l;
             uint32_t v       = 0;
             if (h == 1 && x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
-                v                 = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                v                 = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             acc[r] = v;
         }
@@ -998,13 +1000,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         if (!DM) automorphism_eval(acc, tile, l, h ? M - 5 : 1u);
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        // EvalFuncMultiOutput: table gate % tv_mod (GateArgs::tv_mod)
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             const uint32_t x = (uint32_t)(r << 5) | l;
             uint32_t v       = 0;
             if (h == 1 && x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
-                v                 = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                v                 = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             acc[r] = v;
         }
@@ -2508,12 +2512,15 @@ __global__ void __launch_bounds__(128 * kW2Gates, 2)
 }
 
 bool n2k_supported(const GateArgs& g, const BootTables& t, int nd) {
-    // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29; q = 2N
-    // (the full-resolution monomials) only in the instantiations launched below: 3 digits at
-    // 2^27 <= Q < 2^29 or 4 digits (no 2-digit form takes q = 2N: such calls stay on K5)
-    const bool qok = g.ctmod < 2 * g.N || (g.ctmod == 2 * g.N && ((nd == 3 && t.Q >= (1u << 27)) || nd == 4));
-    const bool ndok = nd == 3 || (nd == 2 && t.Q >= (1u << 27)) || (nd == 4 && g.ctmod == 2 * g.N);
-    return t.Q < (1u << 29) && ndok && g.N == 2048 && qok &&
+    // The monomial table is full-resolution (psi^g - 1, the kernel negating past psi^2048) exactly when the set's
+    // q = 2N, half-resolution (psi^(2f) - 1) otherwise (Engine::build_tables_n2k).  The full-resolution
+    // instantiations (3 retained digits at 2^27 <= Q < 2^29, 4 digits) take any ciphertext modulus <= 2N; the
+    // half-resolution ones need even exponents, ciphertext moduli below 2N (a seam call at 2N stays on K5).
+    // 3 retained digits at Q < 2^29 (Q >= 2^27: QM 2), 2 retained digits at 2^27 <= Q < 2^29.
+    const bool full = g.q == 2 * g.N;
+    const bool qok = full ? (nd == 4 || (nd == 3 && t.Q >= (1u << 27))) : g.ctmod < 2 * g.N;
+    const bool ndok = nd == 3 || (nd == 2 && t.Q >= (1u << 27)) || (nd == 4 && full);
+    return t.Q < (1u << 29) && ndok && g.N == 2048 && qok && g.ctmod <= 2 * g.N &&
            g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 && (uint32_t)(nd + 1) * g.gbits <= 32;
 }
 
@@ -2541,7 +2548,7 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
 #define FHE_N2K(ND_, IO, QM_, ...)                                                                                 \
     hipLaunchKernelGGL((k_blind_rotate_n2k<ND_, IO, QM_, ##__VA_ARGS__>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), \
                        s, g, t, k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
-    if (g.ctmod == 2 * g.N) {  // STD256_4 (29-bit Q, q = 2N); STD256Q_3 / STD256Q_4 (4 retained digits)
+    if (g.q == 2 * g.N) {  // full-resolution table: STD256_4 (29-bit Q, q = 2N); STD256Q_3 / STD256Q_4 (4 digits)
         if (nd == 4) { if (g.acc_io) FHE_N2K(4, true, 2, true); else FHE_N2K(4, false, 2, true); }
         else if (g.acc_io) FHE_N2K(3, true, 2, true); else FHE_N2K(3, false, 2, true);
     } else if (t.Q < (1u << 27)) {  // STD256Q

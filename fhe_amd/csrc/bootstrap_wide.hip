@@ -391,13 +391,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
         }
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        // EvalFuncMultiOutput: table gate % tv_mod (GateArgs::tv_mod)
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
             const uint32_t x = t + TH * r;
             uint64_t v = 0;
             if (x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
-                v = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                v = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             buf[x] = (T)v;
         }
@@ -590,13 +592,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kOpsWaves)
         }
     } else {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        // EvalFuncMultiOutput: table gate % tv_mod (GateArgs::tv_mod)
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
 #pragma unroll
         for (int r = 0; r < S; ++r) {
             const uint32_t x = t + TH * r;
             uint64_t v = 0;
             if (x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
-                v = g.tv ? g.tv[bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                v = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             buf[x] = (T)v;
         }

@@ -375,6 +375,15 @@ static int emit_bytes(const std::string& v, uint8_t* out, size_t cap, size_t* si
     return FHE_HIP_OK;
 }
 
+int fhe_hip_copy_keys(fhe_hip_ctx* dst, const fhe_hip_ctx* src) {
+    if (!dst || !src) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (dst == src) return FHE_HIP_OK;
+    return guarded([&]() -> int {
+        dst->eng.copy_keys_from(src->eng);
+        return FHE_HIP_OK;
+    });
+}
+
 int fhe_hip_load_keys_cereal(fhe_hip_ctx* ctx, const uint8_t* refresh, size_t refresh_size, const uint8_t* sw,
                              size_t sw_size) {
     if (!ctx || !refresh || !sw) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
@@ -823,6 +832,33 @@ int fhe_hip_eval_func_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_
         const hipStream_t s = order.s;
         ctx->eng.eval_func_device(count, d_a, d_b, q_in, lut, d_a_out, d_b_out,
                                   s);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_func_multi_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in,
+                                  const uint64_t* luts, size_t lut_len, uint32_t num_luts, uint64_t* a_out,
+                                  uint64_t* b_out) {
+    if (!ctx || !luts || !io_ok(count, a, b, a_out, b_out, a, b)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
+    if (num_luts == 0) return fail(FHE_HIP_ERR_INVALID_PARAM, "no LUTs");
+    return guarded([&]() -> int {
+        ctx_stream(ctx, nullptr);
+        ctx->eng.fb_host(5, count, a, b, q_in, 0, num_luts, luts, a_out, b_out);
+        return FHE_HIP_OK;
+    });
+}
+
+int fhe_hip_eval_func_multi_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                         uint64_t q_in, const uint64_t* luts, size_t lut_len, uint32_t num_luts,
+                                         uint64_t* d_a_out, uint64_t* d_b_out, void* stream) {
+    if (!ctx || !luts || !io_ok(count, d_a, d_b, d_a_out, d_b_out, d_a, d_b))
+        return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    if (lut_len != q_in) return fail(FHE_HIP_ERR_INVALID_PARAM, "LUT length must equal the ciphertext modulus");
+    if (num_luts == 0) return fail(FHE_HIP_ERR_INVALID_PARAM, "no LUTs");
+    return guarded([&]() -> int {
+        const CallOrder order(ctx, stream);
+        ctx->eng.eval_func_multi_device(count, d_a, d_b, q_in, luts, num_luts, d_a_out, d_b_out, order.s);
         return FHE_HIP_OK;
     });
 }

@@ -332,8 +332,8 @@ Engine::~Engine() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (void* ptr : {(void*)d_tables_, d_bsk_, (void*)d_ksk_, (void*)d_idx_, (void*)d_tvb_, (void*)d_ext_a_,
-                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_mix_, (void*)d_mixio_, (void*)d_tv_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
-                      d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_, (void*)d_wtv_,
+                      (void*)d_ext_b_, (void*)d_io_, (void*)d_l1_, (void*)d_mix_, (void*)d_mixio_, (void*)d_tvbuf_, (void*)d_fb_, (void*)d_logGen_, (void*)d_ops_, (void*)d_nops_,
+                      d_wtables_, (void*)d_wksk_, (void*)d_wext_a_, (void*)d_wext_b_,
                       (void*)d_epk_, (void*)d_epops_, (void*)d_epn_, d_bsk2_, (void*)d_kspart_, d_tables2k_,
                       (void*)d_ksk32_})
         if (ptr) (void)hipFree(ptr);
@@ -698,6 +698,56 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
     FHE_HIP_CHECK(hipMemcpy(d_ksk_, dev.data(), dev.size() * 2, hipMemcpyHostToDevice));
 }
 
+void Engine::copy_keys_from(const Engine& src) {
+    if (src.p_.paramset != p_.paramset || src.p_.method != p_.method)
+        throw std::invalid_argument("copy_keys_from: another parameter set");
+    if (!src.ready()) throw std::logic_error("copy_keys_from: the source context has no keys");
+    if (src.device_ != device_) {
+        int can = 0;
+        FHE_HIP_CHECK(hipDeviceCanAccessPeer(&can, device_, src.device_));
+        if (can) {
+            FHE_HIP_CHECK(hipSetDevice(device_));
+            const hipError_t e = hipDeviceEnablePeerAccess(src.device_, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) throw HipError(e, "hipDeviceEnablePeerAccess");
+            (void)hipGetLastError();
+        }
+    }
+    auto dup = [&](void*& dst, const void* from) {
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        if (dst) FHE_HIP_CHECK(hipFree(dst));
+        dst = nullptr;
+        if (!from) return;
+        hipDeviceptr_t base = nullptr;
+        size_t bytes = 0;
+        FHE_HIP_CHECK(hipSetDevice(src.device_));
+        FHE_HIP_CHECK(hipMemGetAddressRange(&base, &bytes, const_cast<void*>(from)));
+        if (base != from) throw std::logic_error("copy_keys_from: not an allocation base");
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        FHE_HIP_CHECK(hipMalloc(&dst, bytes));
+        if (src.device_ == device_)
+            FHE_HIP_CHECK(hipMemcpyAsync(dst, from, bytes, hipMemcpyDeviceToDevice, stream_));
+        else
+            FHE_HIP_CHECK(hipMemcpyPeerAsync(dst, device_, from, src.device_, bytes, stream_));
+    };
+    sync_streams();
+    const_cast<Engine&>(src).sync_streams();
+    dup(d_bsk_, src.d_bsk_);
+    d_autok_ = src.d_autok_ ? static_cast<char*>(d_bsk_) + (static_cast<const char*>(src.d_autok_) -
+                                                            static_cast<const char*>(src.d_bsk_))
+                            : nullptr;
+    dup(d_bsk2_, src.d_bsk2_);
+    void* k = d_ksk_;
+    dup(k, src.d_ksk_);
+    d_ksk_ = static_cast<uint16_t*>(k);
+    k = d_ksk32_;
+    dup(k, src.d_ksk32_);
+    d_ksk32_ = static_cast<uint32_t*>(k);
+    k = d_wksk_;
+    dup(k, src.d_wksk_);
+    d_wksk_ = static_cast<uint64_t*>(k);
+    FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
 void Engine::keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t* bsk_out, uint64_t* kskA_out,
                            uint64_t* kskB_out) {
     if (!sk) throw std::invalid_argument("secret key is null");
@@ -866,6 +916,7 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         w.tv = g.tv64;
         w.acc_io = g.acc_io;
         w.acc_tv = g.acc_tv;
+        w.tv_mod = g.tv_mod;
         if (g3_ && p_.method == M_LMKCDEY && d_bsk2_ && g.lv == g.lv64 && g.uv == g.uv64 && g.b_const == g.b64 &&
             !g.tv && !g.tv64) {
             const uint32_t* ek = static_cast<const uint32_t*>(d_bsk2_);

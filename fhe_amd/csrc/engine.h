@@ -75,6 +75,9 @@ public:
     // generated in place in the resident layouts; non-null host pointers receive the raw layouts
     void keygen_device(const uint64_t* sk, size_t n, uint64_t seed, uint64_t* bsk_out, uint64_t* kskA_out,
                        uint64_t* kskB_out);
+    // the resident keys of another context of the same parameter set (any device): every packed key buffer
+    // copied device to device (hipMemcpyPeerAsync over xGMI between GPUs), no host repacking
+    void copy_keys_from(const Engine& src);
 
     // EvalBinGate on `count` pairs; device pointers, asynchronous on `s`
     void eval_gate_device(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,
@@ -145,9 +148,18 @@ public:
     // output [count][n] mod fmod
     void bootstrap_func_device(size_t count, const uint64_t* a, const uint64_t* b, uint32_t ctmod,
                                const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // the same with nt tables f[nt][ctmod]: ciphertext g bootstraps with table g % nt
+    void bootstrap_func_tables(size_t count, const uint64_t* a, const uint64_t* b, uint32_t ctmod, const uint64_t* f,
+                               uint32_t nt, uint64_t fmod, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
     // EvalFunc: inputs / outputs mod q_in (= lut length, power of two)
     void eval_func_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in, const uint64_t* lut,
                           uint64_t* a_out, uint64_t* b_out, hipStream_t s);
+    // EvalFuncMultiOutputBatch (batch.cpp:141-174): nl LUTs luts[nl][q_in] on every input; output j of input
+    // i at row i nl + j of a_out [count nl][n] / b_out [count nl].  The LUTs of one class (negacyclic /
+    // periodic / arbitrary) share the class's LUT-independent first bootstrap, and their last bootstraps run
+    // as one launch over count x nl ciphertexts
+    void eval_func_multi_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in, const uint64_t* luts,
+                                uint32_t nl, uint64_t* a_out, uint64_t* b_out, hipStream_t s);
     // EvalFloor: inputs / outputs mod `mod`
     void eval_floor_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod, uint32_t roundbits,
                            uint64_t* a_out, uint64_t* b_out, hipStream_t s);
@@ -160,7 +172,8 @@ public:
                             uint64_t* b_out, hipStream_t s);
     // host-buffer versions (synchronous); op: 0 func (arg = q_in, lut), 1 floor (arg = mod, iarg =
     // roundbits), 2 sign (arg = mod, iarg = scheme_switch), 3 decomp (arg = mod), 4 bootstrap_func
-    // (arg = ctmod, lut = f table, arg2 = fmod)
+    // (arg = ctmod, lut = f table, arg2 = fmod), 5 multi-output EvalFunc (arg = q_in, lut = luts[iarg][q_in];
+    // outputs [count iarg] rows)
     void fb_host(int op, size_t count, const uint64_t* a, const uint64_t* b, uint64_t arg, uint64_t arg2,
                  uint32_t iarg, const uint64_t* lut, uint64_t* a_out, uint64_t* b_out);
 
@@ -274,7 +287,8 @@ private:
     uint64_t* d_mix_ = nullptr;
     uint64_t* d_mixio_ = nullptr;
     // functional bootstrapping: test-vector table [2N] u32 and ciphertext temporaries
-    uint32_t* d_tv_ = nullptr;
+    uint64_t* d_tvbuf_ = nullptr;   // BootstrapFunc tables: u32 words (u64 on the wide path), grown with their count
+    size_t tvcap_ = 0;
     size_t fbcap_ = 0;
     uint64_t* d_fb_ = nullptr;
     // ExternalProduct: packed per-item keys and one-op lists (grown on demand)
@@ -311,7 +325,6 @@ private:
         Engine* e;
         ~BaseGuard() { e->set_base(e->p_.baseG); }
     };
-    uint64_t* d_wtv_ = nullptr;
 };
 
 }  // namespace fhe_amd

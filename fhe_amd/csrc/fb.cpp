@@ -5,6 +5,7 @@
 // as the gates (bootstrap.hip, keyswitch.hip) with a test-vector table instead of the gate
 // window; the LWE additions between bootstraps are element-wise kernels (lwe.hip).  The host
 // code here only sequences launches and builds test-vector tables.
+#include <algorithm>
 #include <vector>
 
 #include "engine.h"
@@ -71,31 +72,39 @@ uint64_t* Engine::fb_work(size_t count, int cts) {
 
 void Engine::bootstrap_func_device(size_t count, const uint64_t* a, const uint64_t* b, uint32_t ctmod,
                                    const uint64_t* f, uint64_t fmod, uint64_t* a_out, uint64_t* b_out, hipStream_t s) {
+    bootstrap_func_tables(count, a, b, ctmod, f, 1, fmod, a_out, b_out, s);
+}
+
+// BootstrapFunc (:617-642) with nt tables f[nt][ctmod]: ciphertext g bootstraps with table g % nt
+// (GateArgs::tv_mod); outputs mod fmod
+void Engine::bootstrap_func_tables(size_t count, const uint64_t* a, const uint64_t* b, uint32_t ctmod,
+                                   const uint64_t* f, uint32_t nt, uint64_t fmod, uint64_t* a_out, uint64_t* b_out,
+                                   hipStream_t s) {
     if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
     if (!pow2(ctmod) || ctmod < 4 || ctmod > 2 * p_.N) throw std::invalid_argument("ctmod must be a power of two <= 2N");
     if (fmod < 2 || fmod > (1ull << 40)) throw std::invalid_argument("fmod out of range");
+    if (nt < 1 || nt > 4096) throw std::invalid_argument("BootstrapFunc: 1 to 4096 tables");
     if (count == 0) return;
     if (count > 0x7fffffffull) throw std::invalid_argument("batch too large");
     ensure_work(count);
     FHE_HIP_CHECK(hipSetDevice(device_));
-    if (wide_) {
-        if (!d_wtv_) FHE_HIP_CHECK(hipMalloc(&d_wtv_, 2 * (size_t)p_.N * 8));
-    } else if (!d_tv_) {
-        FHE_HIP_CHECK(hipMalloc(&d_tv_, 2 * (size_t)p_.N * 4));
-    }
     // BootstrapFuncCore (:596-608): m[j * 2N/ctmod] = (Q / fmod) f((b - j) mod ctmod)
-    std::vector<uint64_t> tv(ctmod);
+    const size_t words = (size_t)nt * ctmod;
+    std::vector<uint64_t> tv(words);
     const uint64_t scale = p_.Q / fmod;
-    for (uint32_t x = 0; x < ctmod; ++x) {
+    for (size_t x = 0; x < words; ++x) {
         if (f[x] > fmod) throw std::invalid_argument("BootstrapFunc: f(x) exceeds fmod");
         tv[x] = scale * f[x];  // <= Q
     }
+    // the table region grows with the number of tables (grow: after the streams' earlier work that reads it)
+    const size_t need = std::max<size_t>(words, 2 * (size_t)p_.N);
     // stream-ordered: the copy runs after every earlier launch on s that reads the table
+    uint64_t* t = grow(d_tvbuf_, tvcap_, need * (wide_ ? 8 : 4));
     if (wide_) {
-        FHE_HIP_CHECK(hipMemcpyAsync(d_wtv_, tv.data(), ctmod * 8, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(t, tv.data(), words * 8, hipMemcpyHostToDevice, s));
     } else {
         std::vector<uint32_t> tv32(tv.begin(), tv.end());
-        FHE_HIP_CHECK(hipMemcpyAsync(d_tv_, tv32.data(), ctmod * 4, hipMemcpyHostToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(t, tv32.data(), words * 4, hipMemcpyHostToDevice, s));
     }
     GateArgs g{};
     g.count = (uint32_t)count;
@@ -105,8 +114,9 @@ void Engine::bootstrap_func_device(size_t count, const uint64_t* a, const uint64
     g.qKS = p_.qKS;
     g.ctmod = ctmod;
     g.factor = 2 * p_.N / ctmod;
-    g.tv = d_tv_;
-    g.tv64 = d_wtv_;
+    g.tv = wide_ ? nullptr : reinterpret_cast<const uint32_t*>(t);
+    g.tv64 = wide_ ? t : nullptr;
+    g.tv_mod = nt;
     g.b_const = 0;  // ctExt = (acc0, acc1[0]) (:624-626)
     g.msb_out = 1;
     g.gbits = p_.gBits;
@@ -158,6 +168,94 @@ void Engine::eval_func_device(size_t count, const uint64_t* a, const uint64_t* b
         FHE_HIP_CHECK(launch_lwe_addb(ub, q_in - (q_in >> 2), q_in, count, s));            // - q/4
         auto f1 = tv_values(TV_LUT_ANTI, lut, q_in, q_in, q_in);
         bootstrap_func_device(count, ua, ub, (uint32_t)q_in, f1.data(), q_in, a_out, b_out, s);
+    }
+}
+
+// EvalFuncMultiOutputBatch (batch.cpp:141-174): the reference runs EvalFunc(ct_i, lut_j) for every pair.
+// EvalFunc's first bootstrap (periodic / arbitrary classes, :283-297, :315-323) does not depend on the LUT,
+// so it runs once per input and class; the LUT-dependent last bootstrap of a class runs as one launch over
+// count x (its LUTs) ciphertexts with a test-vector table per LUT (bootstrap_func_tables).  Every output is
+// the value EvalFunc(ct_i, lut_j) computes: the same bootstraps on the same inputs.
+void Engine::eval_func_multi_device(size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in,
+                                    const uint64_t* luts, uint32_t nl, uint64_t* a_out, uint64_t* b_out,
+                                    hipStream_t s) {
+    if (!pow2(q_in) || q_in < 4 || q_in > 2 * p_.N) throw std::invalid_argument("EvalFunc: modulus must be a power of two <= 2N");
+    if (nl == 0 || nl > 4096) throw std::invalid_argument("EvalFuncMultiOutput: 1 to 4096 LUTs");
+    if (count == 0) return;
+    if (count * nl > 0x7fffffffull) throw std::invalid_argument("batch too large");
+    const size_t n = p_.n;
+    std::vector<int> cls(nl);
+    for (uint32_t j = 0; j < nl; ++j) cls[j] = lut_property(luts + (size_t)j * q_in, q_in, q_in);
+    for (uint32_t j = 0; j < nl; ++j)
+        if (cls[j] == 2 && q_in > p_.N)
+            throw std::invalid_argument("ERROR: ciphertext modulus q needs to be <= ring dimension for arbitrary function evaluation");
+    size_t maxg = 0;
+    for (int c = 0; c < 3; ++c) maxg = std::max<size_t>(maxg, (size_t)std::count(cls.begin(), cls.end(), c));
+    // temporaries (ciphertext slots of n + 1 words): t, u (count each), the repeated inputs and, when the
+    // LUTs split into classes, the class's outputs (count x maxg each)
+    const bool split = maxg < nl;
+    uint64_t* w = fb_work(count, (int)(2 + maxg * (split ? 2 : 1)));
+    uint64_t *ta = w, *tb = ta + count * n, *ua = tb + count, *ub = ua + count * n;
+    uint64_t *ra = ub + count, *rb = ra + count * maxg * n;
+    uint64_t *oa = rb + count * maxg, *ob = oa + count * maxg * n;
+    for (int c = 0; c < 3; ++c) {
+        std::vector<uint32_t> js;
+        for (uint32_t j = 0; j < nl; ++j)
+            if (cls[j] == c) js.push_back(j);
+        if (js.empty()) continue;
+        const uint32_t lg = (uint32_t)js.size();
+        const uint64_t cm = c == 2 ? q_in << 1 : q_in;   // the last bootstrap's ciphertext modulus (:299-310)
+        uint64_t* xa = split ? oa : a_out;
+        uint64_t* xb = split ? ob : b_out;
+        FHE_HIP_CHECK(hipMemcpyAsync(ta, a, count * n * 8, hipMemcpyDeviceToDevice, s));
+        FHE_HIP_CHECK(hipMemcpyAsync(tb, b, count * 8, hipMemcpyDeviceToDevice, s));
+        std::vector<uint64_t> f((size_t)lg * cm);
+        if (c == 0) {  // negacyclic (:253-259): ct + beta, one bootstrap with the LUT itself
+            FHE_HIP_CHECK(launch_lwe_addb(tb, kBeta % q_in, q_in, count, s));
+            for (uint32_t k = 0; k < lg; ++k) {
+                auto t = tv_values(TV_LUT, luts + (size_t)js[k] * q_in, q_in, q_in, q_in);
+                std::copy(t.begin(), t.end(), f.begin() + (size_t)k * cm);
+            }
+            FHE_HIP_CHECK(launch_lwe_repeat(ta, tb, (uint32_t)n, count, lg, ra, rb, s));
+            bootstrap_func_tables(count * lg, ra, rb, (uint32_t)q_in, f.data(), lg, q_in, xa, xb, s);
+        } else if (c == 1) {  // periodic (:315-337)
+            FHE_HIP_CHECK(launch_lwe_addb(tb, kBeta % q_in, q_in, count, s));
+            auto f0 = tv_values(TV_HALF, nullptr, 0, q_in, q_in);
+            bootstrap_func_device(count, ta, tb, (uint32_t)q_in, f0.data(), q_in, ua, ub, s);  // ct2, shared
+            FHE_HIP_CHECK(launch_lwe_sub(a, b, ua, ub, ua, ub, q_in, (uint32_t)n, count, s));   // EvalSubEq2(ct, ct2)
+            FHE_HIP_CHECK(launch_lwe_addb(ub, kBeta % q_in, q_in, count, s));
+            FHE_HIP_CHECK(launch_lwe_addb(ub, q_in - (q_in >> 2), q_in, count, s));            // - q/4
+            for (uint32_t k = 0; k < lg; ++k) {
+                auto t = tv_values(TV_LUT_ANTI, luts + (size_t)js[k] * q_in, q_in, q_in, q_in);
+                std::copy(t.begin(), t.end(), f.begin() + (size_t)k * cm);
+            }
+            FHE_HIP_CHECK(launch_lwe_repeat(ua, ub, (uint32_t)n, count, lg, ra, rb, s));
+            bootstrap_func_tables(count * lg, ra, rb, (uint32_t)q_in, f.data(), lg, q_in, xa, xb, s);
+        } else {  // arbitrary (:261-312)
+            const uint64_t dq = cm;
+            FHE_HIP_CHECK(hipMemcpyAsync(ua, ta, count * n * 8, hipMemcpyDeviceToDevice, s));
+            FHE_HIP_CHECK(hipMemcpyAsync(ub, tb, count * 8, hipMemcpyDeviceToDevice, s));
+            FHE_HIP_CHECK(launch_lwe_addb(ub, kBeta % dq, dq, count, s));
+            auto f0 = tv_values(TV_HALF, nullptr, 0, dq, dq);
+            bootstrap_func_device(count, ua, ub, (uint32_t)dq, f0.data(), dq, ua, ub, s);     // ct3, shared
+            FHE_HIP_CHECK(launch_lwe_sub(ta, tb, ua, ub, ua, ub, dq, (uint32_t)n, count, s));  // EvalSubEq2(ct1, ct3)
+            FHE_HIP_CHECK(launch_lwe_addb(ub, kBeta % dq, dq, count, s));
+            FHE_HIP_CHECK(launch_lwe_addb(ub, dq - (q_in >> 1), dq, count, s));              // - q/2
+            for (uint32_t k = 0; k < lg; ++k) {
+                auto t = tv_values(TV_LUT_ANTI, luts + (size_t)js[k] * q_in, q_in, dq, dq);
+                std::copy(t.begin(), t.end(), f.begin() + (size_t)k * cm);
+            }
+            FHE_HIP_CHECK(launch_lwe_repeat(ua, ub, (uint32_t)n, count, lg, ra, rb, s));
+            bootstrap_func_tables(count * lg, ra, rb, (uint32_t)dq, f.data(), lg, dq, ra, rb, s);  // ct4
+            FHE_HIP_CHECK(launch_lwe_reduce(ra, rb, xa, xb, q_in, (uint32_t)n, count * lg, s));   // SetModulus(q)
+        }
+        if (split)  // row i lg + k of the class -> row i nl + js[k]
+            for (uint32_t k = 0; k < lg; ++k) {
+                FHE_HIP_CHECK(hipMemcpy2DAsync(a_out + (size_t)js[k] * n, (size_t)nl * n * 8, oa + (size_t)k * n,
+                                               (size_t)lg * n * 8, n * 8, count, hipMemcpyDeviceToDevice, s));
+                FHE_HIP_CHECK(hipMemcpy2DAsync(b_out + js[k], (size_t)nl * 8, ob + k, (size_t)lg * 8, 8, count,
+                                               hipMemcpyDeviceToDevice, s));
+            }
     }
 }
 
@@ -266,7 +364,7 @@ void Engine::fb_host(int op, size_t count, const uint64_t* a, const uint64_t* b,
     if (!ready()) throw std::logic_error("keys not loaded (load_bsk / load_ksk)");
     if (count == 0) return;
     const size_t n = p_.n;
-    const size_t parts = op == 3 ? eval_decomp_parts(arg) : 1;
+    const size_t parts = op == 3 ? eval_decomp_parts(arg) : op == 5 ? iarg : 1;
     FHE_HIP_CHECK(hipSetDevice(device_));
     uint64_t* d = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d, count * (n + 1) * (1 + parts) * 8));
@@ -280,6 +378,7 @@ void Engine::fb_host(int op, size_t count, const uint64_t* a, const uint64_t* b,
             case 2: eval_sign_device(count, da, db, arg, iarg != 0, oa, ob, stream_); break;
             case 3: eval_decomp_device(count, da, db, arg, oa, ob, stream_); break;
             case 4: bootstrap_func_device(count, da, db, (uint32_t)arg, lut, arg2, oa, ob, stream_); break;
+            case 5: eval_func_multi_device(count, da, db, arg, lut, iarg, oa, ob, stream_); break;
             default: throw std::invalid_argument("unknown functional-bootstrapping op");
         }
         FHE_HIP_CHECK(hipMemcpyAsync(a_out, oa, parts * count * n * 8, hipMemcpyDeviceToHost, stream_));

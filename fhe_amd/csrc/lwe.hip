@@ -108,6 +108,17 @@ __global__ void k_switch_out(const uint64_t* __restrict__ a, const uint64_t* __r
     }
 }
 
+__global__ void k_lwe_repeat(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint32_t n, size_t count,
+                             uint32_t L, uint64_t* __restrict__ ao, uint64_t* __restrict__ bo) {
+    const uint64_t total = (uint64_t)count * L * n;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t row = i / n, x = i - row * n;
+        ao[i] = a[(row / L) * n + x];
+    }
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < (uint64_t)count * L; r += (uint64_t)gridDim.x * blockDim.x)
+        bo[r] = b[r / L];
+}
+
 uint32_t grid_for(uint64_t work) { return (uint32_t)std::min<uint64_t>((work + 255) / 256, 8192); }
 }  // namespace
 
@@ -140,6 +151,13 @@ hipError_t launch_narrow_u32(const uint64_t* a, const uint64_t* b, uint32_t* ao,
     if (count == 0) return hipSuccess;
     const uint64_t total = (uint64_t)count * len;
     hipLaunchKernelGGL(k_narrow_u32, dim3(grid_for(total)), dim3(256), 0, s, a, b, ao, bo, total, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_lwe_repeat(const uint64_t* a, const uint64_t* b, uint32_t n, size_t count, uint32_t L, uint64_t* ao,
+                             uint64_t* bo, hipStream_t s) {
+    if (count == 0 || L == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_lwe_repeat, dim3(grid_for((uint64_t)count * L * n)), dim3(256), 0, s, a, b, n, count, L, ao, bo);
     return hipGetLastError();
 }
 

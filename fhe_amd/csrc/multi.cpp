@@ -33,10 +33,11 @@ static void for_each_parallel(size_t n, F&& f) {
 
 void MultiEngine::load_keys(const uint64_t* bsk, size_t nbsk, const uint64_t* A, size_t nA, const uint64_t* B,
                             size_t nB) {
-    for_each_parallel(engines_.size(), [&](size_t i) {
-        engines_[i]->load_bsk(bsk, nbsk);
-        engines_[i]->load_ksk(A, nA, B, nB);
-    });
+    // packed once on the host into device 0's layouts, then fanned out device to device (xGMI peer copies
+    // between GPUs) instead of every device repacking the host keys
+    engines_[0]->load_bsk(bsk, nbsk);
+    engines_[0]->load_ksk(A, nA, B, nB);
+    for_each_parallel(engines_.size() - 1, [&](size_t i) { engines_[i + 1]->copy_keys_from(*engines_[0]); });
 }
 
 void MultiEngine::eval_gate_host(int gate, size_t count, const uint64_t* a1, const uint64_t* b1, const uint64_t* a2,

@@ -119,6 +119,10 @@ void* fhe_hip_stream(fhe_hip_ctx* ctx);
 /* upload keys (BTKeyLoad, binfhecontext.h:273-275; Backend::PackBootstrappingKey) */
 int fhe_hip_load_bsk(fhe_hip_ctx* ctx, const uint64_t* bsk, size_t n_words);
 int fhe_hip_load_ksk(fhe_hip_ctx* ctx, const uint64_t* A, size_t nA, const uint64_t* B, size_t nB);
+/* The resident keys of src (same parameter set and method, any device) into dst: device-to-device copies of
+ * the packed key buffers (xGMI peer copies between GPUs), no host repacking -- the per-device key fan-out of
+ * fhe_hip_multi_load_keys */
+int fhe_hip_copy_keys(fhe_hip_ctx* dst, const fhe_hip_ctx* src);
 /* BTKeyGen on the context's device (BinFHEContext::BTKeyGen binfhecontext.cpp:185-200 -> KeyGenAcc
  * rgsw-acc-cggi.cpp:39-96 / rgsw-acc-dm.cpp:39-114 / rgsw-acc-lmkcdey.cpp:39-226, KeySwitchGen
  * lwe-pke.cpp:264-344): generates and loads the keys for sk[n] (mod qKS); bit-identical to
@@ -258,6 +262,16 @@ int fhe_hip_eval_func_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, c
 int fhe_hip_eval_func_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
                                    uint64_t q_in, const uint64_t* lut, size_t lut_len, uint64_t* d_a_out,
                                    uint64_t* d_b_out, void* stream);
+/* EvalFuncMultiOutputBatch (batch.cpp:141-174): EvalFunc(ct_i, luts[j]) for every input i and each of num_luts
+ * LUTs luts[num_luts][lut_len = q_in]; output j of input i at row i * num_luts + j of a_out [count * num_luts][n],
+ * b_out [count * num_luts].  The LUT-independent first bootstrap of EvalFunc's periodic / arbitrary forms runs
+ * once per input and class; the LUT-dependent last bootstraps of a class run as one launch. */
+int fhe_hip_eval_func_multi_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t q_in,
+                                  const uint64_t* luts, size_t lut_len, uint32_t num_luts, uint64_t* a_out,
+                                  uint64_t* b_out);
+int fhe_hip_eval_func_multi_batch_device(fhe_hip_ctx* ctx, size_t count, const uint64_t* d_a, const uint64_t* d_b,
+                                         uint64_t q_in, const uint64_t* luts, size_t lut_len, uint32_t num_luts,
+                                         uint64_t* d_a_out, uint64_t* d_b_out, void* stream);
 /* EvalFloor (binfhecontext.cpp:346-357): inputs/outputs mod `mod` (<= 2^31) */
 int fhe_hip_eval_floor_batch(fhe_hip_ctx* ctx, size_t count, const uint64_t* a, const uint64_t* b, uint64_t mod,
                              uint32_t roundbits, uint64_t* a_out, uint64_t* b_out);

@@ -658,6 +658,53 @@ void BackendHIP::EvalFuncBatch(const RingGSWBTKey& keys, const std::vector<LWECi
     }
 }
 
+void BackendHIP::EvalFuncMultiOutputBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
+                                          const std::vector<std::vector<NativeInteger>>& luts,
+                                          std::vector<LWECiphertext>& out) {
+    std::lock_guard<std::mutex> lock(mu_);
+    const size_t B = cts.size(), L = luts.size();
+    out.resize(B * L);
+    if (B == 0 || L == 0)
+        return;
+    EnsureBSK(keys.BSkey);
+    EnsureKSK(keys.KSkey);
+    const size_t len = luts[0].size();
+    std::vector<uint64_t> tab(L * len);
+    for (size_t j = 0; j < L; ++j) {
+        if (luts[j].size() != len)
+            throw std::invalid_argument("EvalFuncMultiOutputBatch: LUTs of one length");
+        for (size_t i = 0; i < len; ++i)
+            tab[j * len + i] = luts[j][i].ConvertToInt();
+    }
+    // EvalFunc runs at each ciphertext's own modulus (binfhe-base-scheme.cpp:250): one call per modulus, all L
+    // LUTs in it (output j of input i at i * L + j, batch.cpp:160-164)
+    std::vector<std::pair<uint64_t, size_t>> order(B);
+    for (size_t g = 0; g < B; ++g) {
+        if (!cts[g])
+            throw std::invalid_argument("Ciphertext is empty");
+        order[g] = {cts[g]->GetModulus().ConvertToInt(), g};
+    }
+    std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    const uint32_t n = p_.n;
+    for (size_t s0 = 0; s0 < B;) {
+        const uint64_t q = order[s0].first;
+        std::vector<size_t> rows;
+        for (; s0 < B && order[s0].first == q; ++s0)
+            rows.push_back(order[s0].second);
+        const size_t c = rows.size();
+        std::vector<uint64_t> a(c * n), b(c), ao(c * L * n), bo(c * L);
+        flatten(cts, rows, n, a.data(), b.data());
+        Check(fhe_hip_eval_func_multi_batch(ctx_, c, a.data(), b.data(), q, tab.data(), len, (uint32_t)L, ao.data(),
+                                            bo.data()),
+              "EvalFuncMultiOutputBatch");
+        const NativeInteger qn(q);
+        for (size_t g = 0; g < c; ++g)
+            for (size_t j = 0; j < L; ++j)
+                out[rows[g] * L + j] = std::make_shared<LWECiphertextImpl>(
+                    vec_from(ao.data() + (g * L + j) * n, n, qn), NativeInteger(bo[g * L + j]));
+    }
+}
+
 void BackendHIP::RefreshBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
                               std::vector<LWECiphertext>& out) {
     std::lock_guard<std::mutex> lock(mu_);
@@ -769,17 +816,7 @@ BatchResult EvalFuncMultiOutputBatchHIP(BinFHEContext& cc, const std::vector<LWE
         return lux::fhe::EvalFuncMultiOutputBatch(cc, ct_in, luts, ct_out, flags);
     if (ct_in.empty() || luts.empty())
         return BatchResult{true, 0, 0, ""};
-    return batch_result(ct_in.size(), [&] {
-        const size_t L = luts.size(), B = ct_in.size();
-        ct_out.resize(B * L);
-        const RingGSWBTKey keys = context_keys(cc);
-        std::vector<LWECiphertext> part;
-        for (size_t j = 0; j < L; ++j) {  // output j of input i at i * L + j (batch.cpp:160-164)
-            hip->EvalFuncBatch(keys, ct_in, luts[j], part);
-            for (size_t i = 0; i < B; ++i)
-                ct_out[i * L + j] = part[i];
-        }
-    });
+    return batch_result(ct_in.size(), [&] { hip->EvalFuncMultiOutputBatch(context_keys(cc), ct_in, luts, ct_out); });
 }
 
 BatchResult EvalCMUXBatchHIP(BinFHEContext& cc, const std::vector<LWECiphertext>& ct_sel,

@@ -95,8 +95,13 @@ public:
     //                  NAND bootstraps in two dependent launches
     void EvalFuncBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
                        const std::vector<NativeInteger>& lut, std::vector<LWECiphertext>& out);
-    //   RefreshBatch:  BinFHEContext::Bootstrap (BinFHEScheme::Bootstrap, binfhe-base-scheme.cpp:190-218) per
-    //                  ciphertext (mod q, plaintext modulus 4)
+    //   EvalFuncMultiOutputBatch: EvalFunc(ct_i, luts[j]) for every pair (batch.cpp:141-174), output j of input
+    //                  i at i * L + j; one device call per ciphertext modulus (fhe_hip_eval_func_multi_batch)
+    void EvalFuncMultiOutputBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts,
+                                  const std::vector<std::vector<NativeInteger>>& luts, std::vector<LWECiphertext>& out);
+    //   RefreshBatch:  BinFHEContext::Bootstrap (BinFHEScheme::Bootstrap, binfhe-base-scheme.cpp:190-220) per
+    //                  ciphertext, mod q or mod Q (switched first, :200-201), any plaintext modulus
+    //   EvalBinGateBatch / EvalCMUXBatch take ciphertexts mod Q (dimension N) as well (:92-93, :180-182)
     void RefreshBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& cts, std::vector<LWECiphertext>& out);
     void EvalCMUXBatch(const RingGSWBTKey& keys, const std::vector<LWECiphertext>& ct0,
                        const std::vector<LWECiphertext>& ct1, const std::vector<LWECiphertext>& ct2,

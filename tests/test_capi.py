@@ -122,3 +122,30 @@ def test_gpu_seam_call_sequence_repeats_on_one_context(ps, m):
             for u, v in zip(x if isinstance(x, tuple) else (x,), y if isinstance(y, tuple) else (y,)):
                 assert np.array_equal(u, v)
     e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ps,m", [(3, 2), (21, 3), (9, 2), (18, 2), (37, 3)])
+def test_gpu_copy_keys_fan_out_matches_host_load(ps, m):
+    """fhe_hip_copy_keys (MultiEngine's key fan-out): a context that received another context's resident keys
+    device to device computes the same gates as one that packed the host keys itself (STD128, STD128_LMKCDEY,
+    the 64-bit STD192, the K1w STD256Q / STD256Q_3_LMKCDEY layouts)"""
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import check
+    L = bf.L()
+    L.fhe_hip_copy_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    keys = bf.keygen(ps, m, 0xB0070000 + ps)
+    a1, b1 = bf.encrypt(ps, m, keys.sk, np.arange(37) % 2, 1)
+    a2, b2 = bf.encrypt(ps, m, keys.sk, np.arange(37) // 2 % 2, 2)
+    src = bf.GateEngine(ps, m, 0)
+    src.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    dst = bf.GateEngine(ps, m, 0)
+    check(L.fhe_hip_copy_keys(dst._h, src._h))
+    for gate in (bf.AND, bf.XOR):
+        ra, rb = src.eval_gate(gate, a1, b1, a2, b2)
+        ga, gb = dst.eval_gate(gate, a1, b1, a2, b2)
+        assert np.array_equal(ra, ga) and np.array_equal(rb, gb), gate
+    other = bf.GateEngine(3 if ps != 3 else 21, 2 if ps != 3 else 3, 0)
+    assert L.fhe_hip_copy_keys(other._h, src._h) == -2   # another parameter set
+    for e in (src, dst, other):
+        e.close()

@@ -118,6 +118,24 @@ def test_gpu_fb_bit_exact_vs_reference(name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", SETS)
+def test_gpu_eval_func_multi_output_bit_exact_vs_reference(name):
+    """EvalFuncMultiOutputBatch (batch.cpp:141-174) in one call (fhe_hip_eval_func_multi_batch): LUT lists of one
+    class (one fused launch for the last bootstraps) and of mixed classes (a shared first bootstrap per class,
+    rows scattered back), every output == the reference's EvalFunc golden for its LUT"""
+    g, (keys, q, p, ms, sa, sb, PL, xs, la, lb), luts = fixture(name)
+    e = engine(name)
+    names = list(luts)
+    for order in (["neg", "neg"], ["per", "per", "per"], names, names[::-1] + ["per", "neg"]):
+        order = [x for x in order if x in luts]
+        tab = np.stack([luts[x] for x in order])
+        ao, bo = e.eval_func_multi(sa, sb, q, tab)
+        L = len(order)
+        for j, lname in enumerate(order):
+            assert same(ao[j::L], g[f"func_{lname}_a"]) and same(bo[j::L], g[f"func_{lname}_b"]), (order, lname)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SETS)
 def test_gpu_fb_ragged_and_large_vs_oracle(name, restatement):
     """ragged batches vs the oracle (incl. BootstrapFunc with an arbitrary table and fmod), and a
     4096-ciphertext EvalFunc batch (tiled key switch) checked by decryption."""

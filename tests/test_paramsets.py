@@ -195,8 +195,9 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
     amod = 2 * P.N if m == 3 else P.q
     acc_a = rng.integers(0, amod, (5, P.n), dtype=np.uint64)
     acc = rng.integers(0, P.Q, (5, 2, P.N), dtype=np.uint64)
-    # GINX seam calls with ciphertexts mod 2N as well (EvalAcc reads a_i with the ciphertext's modulus): the
-    # rows whose K1w has no q = 2N instantiation (2 retained digits) must fall back, not read past their keys
+    # GINX seam calls at a second ciphertext modulus (EvalAcc reads a_i with the ciphertext's modulus): 2N on the
+    # half-resolution rows (no even exponents: K5 must take them), N / 2 on the q = 2N rows (their
+    # full-resolution kernel takes any modulus)
     acc_a2 = rng.integers(0, 2 * P.N, (5, P.n), dtype=np.uint64)
     res = {}
     for flag in ("1", "0"):
@@ -206,8 +207,9 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
         res[flag] = [(e.eval_gate(gate, a1, b1, a2, b2), e.eval_gate_extended(gate, a1, b1, a2, b2))
                      for gate in GATES.values()]
         res[flag].append(((e.blind_rotate_acc(acc_a, amod, acc),), ))
-        if m == 2 and amod != 2 * P.N:
-            res[flag].append(((e.blind_rotate_acc(acc_a2, 2 * P.N, acc),), ))
+        if m == 2:   # the other ciphertext modulus of the table's resolution: 2N (half table) or q / 2 (full)
+            amod2 = 2 * P.N if amod != 2 * P.N else P.N // 2
+            res[flag].append(((e.blind_rotate_acc(acc_a2 % amod2, amod2, acc),), ))
         e.close()
     for (gname, gate), (fast, ref) in zip(GATES.items(), zip(res["1"], res["0"])):
         for u, v in zip(fast, ref):
