@@ -435,7 +435,13 @@ FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
 FHE_DEV uint32_t other_half(uint32_t x, int xaddr) { return (uint32_t)__builtin_amdgcn_ds_bpermute(xaddr, (int)x); }
 
 // key vector load
+#if defined(FHE_ABL_KEYS) && FHE_ABL_KEYS == 1   // timing ablations only (wrong results): keys from a 4 KB L1-resident block
+FHE_DEV uint4 kload(const uint4* p, size_t i) { return p[i & 255]; }
+#elif defined(FHE_ABL_KEYS) && FHE_ABL_KEYS == 2  // no key loads at all
+FHE_DEV uint4 kload(const uint4*, size_t i) { const uint32_t v = (uint32_t)i; return make_uint4(v, v, v, v); }
+#else
 FHE_DEV uint4 kload(const uint4* p, size_t i) { return p[i]; }
+#endif
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 
 // SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = 3: centre x in [0, Q) to
@@ -2302,8 +2308,12 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
 // psi^(g + 2048) - 1 = -(psi^g - 1) - 2 is formed on the fly, (-x - 2, -y - 2R) with 2R centred (|y'| < Q:
 // |acc| < 2.93 Q, bound 30)
 template <int ND, int QM, bool FULL> constexpr int kW2Bound = QM == 2 ? (FULL ? (ND == 4 ? 32 : 30) : 27) : kW2AccBound;
+#ifndef FHE_N2K_ONEWAVE
+#define FHE_N2K_ONEWAVE 0  // bit 0 / 1: the 4- / 3-digit K1w GINX forms at one wave per SIMD (512 registers)
+#endif
 template <int ND, bool ACCIO, int QM = 0, bool FULL = false>
-__global__ void __launch_bounds__(128 * kW2Gates, 2)
+__global__ void __launch_bounds__(128 * kW2Gates,
+                                  (((FHE_N2K_ONEWAVE & 1) && ND == 4) || ((FHE_N2K_ONEWAVE & 2) && ND == 3)) ? 1 : 2)
     k_blind_rotate_n2k(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                        const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {

@@ -87,10 +87,12 @@ uint32_t Engine::kernel_kind(const Params& p) {
 }
 
 bool Engine::ks32_set(const Params& p) {
-    const bool pow2ks = !(p.qKS & (p.qKS - 1)), pow2b = !(p.baseKS & (p.baseKS - 1));
-    const bool shape = ((p.baseKS == 32 || p.baseKS == 64) && p.digitsKS == 3) || (p.baseKS == 16 && p.digitsKS == 4);
-    return !is_large(p.paramset) && !p.timeopt && pow2ks && pow2b && shape && p.qKS <= 65536 && p.n < 2048 &&
-           p.N <= 2048;
+    const bool pow2ks = !(p.qKS & (p.qKS - 1));
+    // the tiled shapes (keyswitch.hip launch_keyswitch): baseKS 32 / 64 with digitsKS 3, 16 with 4, and 21 with 4
+    // (STD256Q_3, digits by division)
+    const bool shape = ((p.baseKS == 32 || p.baseKS == 64) && p.digitsKS == 3) ||
+                       ((p.baseKS == 16 || p.baseKS == 21) && p.digitsKS == 4);
+    return !is_large(p.paramset) && !p.timeopt && pow2ks && shape && p.qKS <= 65536 && p.n < 2048 && p.N <= 2048;
 }
 
 bool Engine::ks32w_set(const Params& p) {

@@ -122,17 +122,19 @@ constexpr int kKsSplitG = 512;
 #ifndef FHE_KS_GPT
 #define FHE_KS_GPT 1  // gates per thread of the 512-thread tiles (1: 512-gate tiles)
 #endif            // the row split's gate tile
-// LOGB = log2(baseKS): 5 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 6 (STD128_3/4,
+// BASE = baseKS: 32 (STD128, STD128Q, LPF_STD128: 32 staged slices per step) or 64 (STD128_3/4,
 // LPF_STD128Q, STD256Q_3_LMKCDEY: 64 slices, 2 values of i per round so that the double buffer keeps the
 // same 104 KB; slices d and d + 32 share a bank slot, a 2-way conflict), both with KD = digitsKS = 3; or
-// 4 with KD = 4 (STD256Q: baseKS 16, qKS 2^16; 2 values of i per round, 35 KB)
+// 16 with KD = 4 (STD256Q: baseKS 16, qKS 2^16; 2 values of i per round, 35 KB)
 // W32: u32 rows and u32 column sums (exact mod any power-of-two qKS <= 2^32: STD192Q_4, STD256Q_4,
 // STD256Q_4_LMKCDEY), one value of i per round, 264-byte slices (8-byte piece k of slice d in bank slot
 // (d + k) mod 32)
-template <int LOGB, int IPR, int KD = 3, bool W32 = false> struct KsShape {
-    static constexpr int base  = 1 << LOGB;
+// BASE 21 with KD = 4 (STD256Q_3: qKS 2^16): 21 staged slices, digits by division (ks_digit), 2 values of i per
+// round (24 KB per buffer)
+template <int BASE, int IPR, int KD = 3, bool W32 = false> struct KsShape {
+    static constexpr int base  = BASE;
     static constexpr int eb    = W32 ? 4 : 2;                     // bytes per KSK element
-    static constexpr int ipr   = W32 ? 1 : LOGB == 5 ? IPR : 2;
+    static constexpr int ipr   = W32 ? 1 : BASE == 32 ? IPR : 2;
     static constexpr int step  = ipr * KD;                        // (i, j) steps per round / LDS buffer / barrier
     static constexpr int rowb  = kKsCols * eb + (W32 || FHE_KS_B64 ? 8 : 16);  // LDS bytes per staged slice
     static constexpr int pps   = kKsCols * eb / 16;               // 16-byte parts per slice
@@ -146,12 +148,22 @@ template <int LOGB, int IPR, int KD = 3, bool W32 = false> struct KsShape {
 // staged once per gate tile (the per-gate kernel re-reads 3 MB of rows per ciphertext).
 // GPT: gates per thread (u16 rows, no row split): a workgroup's tile is G GPT gates, so every staged KSK
 // slice serves GPT times as many gates (KSK traffic / GPT); thread t owns gates t, t + G, ...
-template <int G, bool SPLIT, int LOGB, int IPR, int KD = 3, bool W32 = false, int GPT = 1>
+// digit j of a (base BASE, the reference's a0 = atmp % baseKS; atmp /= baseKS, lwe-pke.cpp:362-364): a bit
+// field for a power-of-two base, a division by the constant BASE^j otherwise
+template <int BASE>
+FHE_DEV uint32_t ks_digit(uint32_t a, int j) {
+    if ((BASE & (BASE - 1)) == 0) return (a >> (__builtin_ctz(BASE) * j)) & (BASE - 1);
+    uint32_t p = 1;
+    for (int k = 0; k < j; ++k) p *= BASE;
+    return (a / p) % BASE;
+}
+
+template <int G, bool SPLIT, int BASE, int IPR, int KD = 3, bool W32 = false, int GPT = 1>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const void* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                       uint64_t* __restrict__ b_out, uint32_t* __restrict__ part) {
-    using S_ = KsShape<LOGB, IPR, KD, W32>;
+    using S_ = KsShape<BASE, IPR, KD, W32>;
     constexpr int kKsDigits = KD;
     constexpr int kKsParts = S_::parts, kKsStep = S_::step, kIPR = S_::ipr, kBase = S_::base;
     constexpr int kRowB = S_::rowb, kPps = S_::pps, kEB = S_::eb;
@@ -260,7 +272,7 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
                 for (int u = 0; u < GPT; ++u) {
                     const uint32_t* as = reinterpret_cast<const uint32_t*>(&avs[u]);
-                    const uint32_t dig = (as[q / kKsDigits] >> (LOGB * (q % kKsDigits))) & (kBase - 1);
+                    const uint32_t dig = ks_digit<kBase>(as[q / kKsDigits], q % kKsDigits);
                     const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kRowB);
                     uint2 w[kKsCols / 4];
 #pragma unroll
@@ -279,7 +291,7 @@ __global__ void __launch_bounds__(G)
         const uint32_t* as = reinterpret_cast<const uint32_t*>(&avs[0]);
 #pragma unroll
         for (int q = 0; q < kKsStep; ++q) {
-            const uint32_t dig = (as[q / kKsDigits] >> (LOGB * (q % kKsDigits))) & (kBase - 1);
+            const uint32_t dig = ks_digit<kBase>(as[q / kKsDigits], q % kKsDigits);
             if (W32) {  // u32 columns: 32 8-byte pieces, one v_sub_u32 per column
                 const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kRowB);
                 uint2 w[kKsCols / 2];
@@ -438,10 +450,11 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
                             const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
                             uint64_t* b_out, hipStream_t s, uint32_t* part, size_t part_words) {
     if (g.count == 0) return hipSuccess;
-    if (baseKS & (baseKS - 1)) return hipErrorInvalidValue;
+    const bool base21 = baseKS == 21 && digitsKS == 4;  // STD256Q_3: the tiled kernel only
+    if ((baseKS & (baseKS - 1)) && !base21) return hipErrorInvalidValue;
     if (g.qKS & (g.qKS - 1) || g.qKS > 65536 || g.n >= 2048 || g.N > 2048) return hipErrorInvalidValue;
     const uint32_t W = ksk_width(g.n);
-    const uint32_t logBase = (uint32_t)__builtin_ctz(baseKS);
+    const uint32_t logBase = base21 ? 0u : (uint32_t)__builtin_ctz(baseKS);
 #ifndef FHE_KS_TILE
 #define FHE_KS_TILE 0   // 0: choose by batch size; 1: per-gate kernel; 256: gate tile
 #endif
@@ -449,7 +462,9 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
     // tiles need >= 16 x 8 workgroups to pay, or a row split (scratch) below 4096 gates
     if (tile == 0) tile = g.count >= 4096 || part ? 256 : 1;
     const bool shape3 = (logBase == 5 || logBase == 6) && digitsKS == 3, shape4 = logBase == 4 && digitsKS == 4;
-    if (tile > 1 && (!(shape3 || shape4) || g.N % kKsIPR)) tile = 1;
+    if (base21) tile = 256;
+    if (tile > 1 && (!(shape3 || shape4 || base21) || g.N % kKsIPR)) tile = 1;
+    if (base21 && tile == 1) return hipErrorInvalidValue;
     // the per-gate kernel: one thread per column pair, at most 512
     if (tile == 1 && W > 1024) return hipErrorInvalidValue;
     if (tile > 1) {
@@ -461,18 +476,20 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
 #define FHE_KS_LAUNCH(G_, SP, LB, IPR_, ...)                                                                      \
     hipLaunchKernelGGL((k_keyswitch_tiled<G_, SP, LB, IPR_, ##__VA_ARGS__>), grid, dim3(G_), 0, s, g, ksk, ms_a, ms_b, \
                        q_out, a_out, b_out, SP ? part : nullptr)
-        if (shape4) {
-            if (S > 1) FHE_KS_LAUNCH(256, true, 4, 2, 4); else FHE_KS_LAUNCH(256, false, 4, 2, 4);
+        if (base21) {
+            if (S > 1) FHE_KS_LAUNCH(256, true, 21, 2, 4); else FHE_KS_LAUNCH(256, false, 21, 2, 4);
+        } else if (shape4) {
+            if (S > 1) FHE_KS_LAUNCH(256, true, 16, 2, 4); else FHE_KS_LAUNCH(256, false, 16, 2, 4);
         } else if (logBase == 5) {
-            if (S > 1) FHE_KS_LAUNCH(kKsSplitG, true, 5, 4);
+            if (S > 1) FHE_KS_LAUNCH(kKsSplitG, true, 32, 4);
             else if (G == 512 && FHE_KS_GPT > 1) {  // GPT gates per thread: grid over G GPT-gate tiles
                 const dim3 gg((g.count + 512 * FHE_KS_GPT - 1) / (512 * FHE_KS_GPT), W / kKsCols, 1);
-                hipLaunchKernelGGL((k_keyswitch_tiled<512, false, 5, 2, 3, false, FHE_KS_GPT>), gg, dim3(512), 0, s, g,
+                hipLaunchKernelGGL((k_keyswitch_tiled<512, false, 32, 2, 3, false, FHE_KS_GPT>), gg, dim3(512), 0, s, g,
                                    ksk, ms_a, ms_b, q_out, a_out, b_out, nullptr);
-            } else if (G == 512) FHE_KS_LAUNCH(512, false, 5, 2);
-            else FHE_KS_LAUNCH(256, false, 5, 4);
+            } else if (G == 512) FHE_KS_LAUNCH(512, false, 32, 2);
+            else FHE_KS_LAUNCH(256, false, 32, 4);
         } else {
-            if (S > 1) FHE_KS_LAUNCH(256, true, 6, 2); else FHE_KS_LAUNCH(256, false, 6, 2);
+            if (S > 1) FHE_KS_LAUNCH(256, true, 64, 2); else FHE_KS_LAUNCH(256, false, 64, 2);
         }
 #undef FHE_KS_LAUNCH
         if (S > 1) {
@@ -512,11 +529,11 @@ hipError_t launch_keyswitch_w32(const GateArgs& g, uint32_t baseKS, uint32_t dig
     hipLaunchKernelGGL((k_keyswitch_tiled<G, SP, LB, 1, KD_, true>), grid, dim3(G), 0, s, g, ksk, ms_a, ms_b, q_out, \
                        a_out, b_out, SP ? part : nullptr)
     if (baseKS == 16 && digitsKS == 5) {
-        if (S > 1) FHE_KSW_LAUNCH(true, 4, 5); else FHE_KSW_LAUNCH(false, 4, 5);
+        if (S > 1) FHE_KSW_LAUNCH(true, 16, 5); else FHE_KSW_LAUNCH(false, 16, 5);
     } else if (baseKS == 16) {
-        if (S > 1) FHE_KSW_LAUNCH(true, 4, 6); else FHE_KSW_LAUNCH(false, 4, 6);
+        if (S > 1) FHE_KSW_LAUNCH(true, 16, 6); else FHE_KSW_LAUNCH(false, 16, 6);
     } else {
-        if (S > 1) FHE_KSW_LAUNCH(true, 6, 3); else FHE_KSW_LAUNCH(false, 6, 3);
+        if (S > 1) FHE_KSW_LAUNCH(true, 64, 3); else FHE_KSW_LAUNCH(false, 64, 3);
     }
 #undef FHE_KSW_LAUNCH
     if (S > 1) {

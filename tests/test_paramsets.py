@@ -112,12 +112,13 @@ def test_gpu_digitsg4_split_kernel_matches_64bit_accumulator(name, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["std128_3", "std128q"])
+@pytest.mark.parametrize("name", ["std128_3", "std128q", "std256q_3"])
 def test_gpu_digitsg4_keyswitch_vs_reference(name):
     """the 32-bit key switch these sets now use (u16 rows of 1024 columns; gate-tiled with 64 staged
     slices at baseKS = 64 (STD128_3), 32 at baseKS = 32 (STD128Q); row split below 4096) on uniform
     inputs mod qKS, incl. a ragged last tile, vs the reference's own LWEEncryptionScheme::KeySwitch
-    (oracle/_ref, the restatement covers the STD128 sets only)"""
+    (oracle/_ref, the restatement covers the STD128 sets only).  STD256Q_3 (round 5): baseKS 21, its
+    four digits by division, 21 staged slices, 1408-column rows at n = 1400"""
     from fhe_amd import binfhe as bf
     from make_golden import GATE_SETS
     from oracle_lib import Ref
