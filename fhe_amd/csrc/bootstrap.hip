@@ -93,6 +93,9 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_AKPF
 #define FHE_LMK_AKPF 1   // the same for the automorphism keys (4 slots x 2 rows)
 #endif
+#ifndef FHE_LMK_SWAP
+#define FHE_LMK_SWAP 1   // LMKCDEY automorphism: the digits into the half-wave layout by v_permlane32_swap
+#endif
 #ifndef FHE_LMK_KPF
 #define FHE_LMK_KPF 1    // op-list kernel: key chunks (4 slots x 4 rows) requested ahead of their MAC
 #endif
@@ -1120,6 +1123,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 uint32_t a0[16];
                 automorphism_wide(acc, a0, tile, tileW, l, lane, kexp);
                 inv_wave_s<20, LZ>(a0, tileW, lane, s_tabI, T.w1R, m.oneR, m);
+#if FHE_LMK_SWAP
+                // coefficient x = (r << 6) | lane goes to half-wave register (x >> 5), lane x & 31 of half 0
+                // (digit A) and half 1 (digit B): one half exchange per register pair (v_permlane32_swap:
+                // lanes 32..63 of x trade places with lanes 0..31 of y) instead of a pass through LDS
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    uint32_t x, y;
+                    decompose2<true>(a0[r], dec, x, y);
+                    const auto p = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+                    dA[2 * r]     = p[0];
+                    dA[2 * r + 1] = p[1];
+                }
+#else
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     uint32_t x, y;
@@ -1132,6 +1148,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #pragma unroll
                 for (int r = 0; r < 32; ++r) dA[r] = tile[l * 33 + r];
                 wave_lds_sync();
+#endif
             }
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
             const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
