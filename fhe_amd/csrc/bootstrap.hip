@@ -2324,7 +2324,15 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
 // FULL (q = 2N, STD256_4: odd monomial exponents): the table holds psi^g - 1 for g in [0, 2048] and
 // psi^(g + 2048) - 1 = -(psi^g - 1) - 2 is formed on the fly, (-x - 2, -y - 2R) with 2R centred (|y'| < Q:
 // |acc| < 2.93 Q, bound 30)
-template <int ND, int QM, bool FULL> constexpr int kW2Bound = QM == 2 ? (FULL ? (ND == 4 ? 32 : 30) : 27) : kW2AccBound;
+// QM 3 (round 5): the centred products of QM 2 for Q < 2^27 (STD256Q_3 / STD256Q_4: q = 2N, 4 digits), with QM 0's
+// unreduced forward transform and 16 Q inverse plan: |D| < 11 Q + 2^(g-1), |S+-| < 44 Q^2, so each pair's hi part
+// times a monomial half adds < 0.05 Q; own word < Q/2 (lo parts) + 0.09 Q + A/32 + Q/2, the partner's the same
+// without A: A < 2.25 Q (bound 25)
+template <int ND, int QM, bool FULL>
+constexpr int kW2Bound = QM == 3 ? 25 : QM == 2 ? (FULL ? (ND == 4 ? 32 : 30) : 27) : kW2AccBound;
+#ifndef FHE_N2K_QM3
+#define FHE_N2K_QM3 1  // 4-digit K1w GINX at Q < 2^27 in the QM 3 class (0: QM 2, the round-4 form)
+#endif
 #ifndef FHE_N2K_ONEWAVE
 #define FHE_N2K_ONEWAVE 0  // bit 0 / 1: the 4- / 3-digit K1w GINX forms at one wave per SIMD (512 registers)
 #endif
@@ -2335,8 +2343,10 @@ __global__ void __launch_bounds__(128 * kW2Gates,
                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
                        const uint32_t* __restrict__ twAf, const uint32_t* __restrict__ twAi) {
     constexpr int kQ = 2 * ND;  // key vectors per slot pair: ND digit rows x 2 columns
-    static_assert(!FULL || QM == 2, "the full-resolution monomials need the centred (QM 2) products");
+    static_assert(!FULL || QM >= 2, "the full-resolution monomials need the centred (QM 2 / 3) products");
     constexpr int BIN = kW2Bound<ND, QM, FULL>, LIM = QM == 2 ? 40 : 160;
+    constexpr int QF = QM == 3 ? 0 : QM;  // the forward transform's reduction class
+    constexpr bool CEN = QM >= 2;         // centred monomial pairs and signed lo halves
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 2048;
@@ -2348,7 +2358,7 @@ __global__ void __launch_bounds__(128 * kW2Gates,
     }
     for (int i = threadIdx.x; i < kW2Mono; i += blockDim.x) {
         uint32_t mx = T.monoP[i], my = T.mono[i];
-        if (QM == 2) {  // centred: (-Q/2, Q/2]
+        if (CEN) {  // centred: (-Q/2, Q/2]
             mx = mx > T.Q / 2 ? mx - T.Q : mx;
             my = my > T.Q / 2 ? my - T.Q : my;
         }
@@ -2385,7 +2395,7 @@ __global__ void __launch_bounds__(128 * kW2Gates,
             }
             tv[0][r] = v;
         }
-        fwd_2k_s<1, QM, true>(tv, tile, L, twAf, s_tab, m);
+        fwd_2k_s<1, QF, true>(tv, tile, L, twAf, s_tab, m);
 #pragma unroll
         for (int r = 0; r < 32; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
     } else {
@@ -2437,7 +2447,7 @@ __global__ void __launch_bounds__(128 * kW2Gates,
         inv_2k_s<BIN, LIM>(d[0], tile, L, twI, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
         for (int r = 0; r < 32; ++r) decompose_n<ND>(d[0][r], dec, d, r);
-        fwd_2k_s<ND, QM, true>(d, tile, L, twF, s_tab, m);
+        fwd_2k_s<ND, QF, true>(d, tile, L, twF, s_tab, m);
         constexpr uint32_t EM = FULL ? 4095u : 2047u;
         const uint32_t fl = (as * lmul) & EM;
 #pragma unroll
@@ -2484,7 +2494,7 @@ __global__ void __launch_bounds__(128 * kW2Gates,
                         S2 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.w : kv.z);
                     }
                     int64_t S;
-                    if (QM == 2) {  // S1 = hi 2^32 + lo with lo signed
+                    if (CEN) {  // S1 = hi 2^32 + lo with lo signed
                         const int32_t l1 = (int32_t)S1, l2 = (int32_t)S2;
                         const int32_t h1 = (int32_t)((S1 - l1) >> 32), h2 = (int32_t)((S2 - l2) >> 32);
                         S = (int64_t)l1 * (int32_t)mp.x + (int64_t)h1 * (int32_t)mp.y;
@@ -2565,7 +2575,9 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, false, 2, true>),
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<3, true, 2, true>),
                               reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, false, 2, true>),
-                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, true, 2, true>)})
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, true, 2, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, false, 3, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_n2k<4, true, 3, true>)})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)w2_lds());
         return true;
     }();
@@ -2576,7 +2588,9 @@ hipError_t launch_blind_rotate_n2k(const GateArgs& g, const BootTables& t, const
     hipLaunchKernelGGL((k_blind_rotate_n2k<ND_, IO, QM_, ##__VA_ARGS__>), dim3(blocks), dim3(128 * kW2Gates), w2_lds(), \
                        s, g, t, k, idx, tvb, ext_a, ext_b, t.twA_fwd, t.twA_inv)
     if (g.q == 2 * g.N) {  // full-resolution table: STD256_4 (29-bit Q, q = 2N); STD256Q_3 / STD256Q_4 (4 digits)
-        if (nd == 4) { if (g.acc_io) FHE_N2K(4, true, 2, true); else FHE_N2K(4, false, 2, true); }
+        if (nd == 4 && FHE_N2K_QM3 && t.Q < (1u << 27)) {  // STD256Q_3 / STD256Q_4: no forward reductions (QM 3)
+            if (g.acc_io) FHE_N2K(4, true, 3, true); else FHE_N2K(4, false, 3, true);
+        } else if (nd == 4) { if (g.acc_io) FHE_N2K(4, true, 2, true); else FHE_N2K(4, false, 2, true); }
         else if (g.acc_io) FHE_N2K(3, true, 2, true); else FHE_N2K(3, false, 2, true);
     } else if (t.Q < (1u << 27)) {  // STD256Q
         if (g.acc_io) FHE_N2K(3, true, 0); else FHE_N2K(3, false, 0);
