@@ -32,6 +32,18 @@
 #define FHE_WAVES_PER_EU 2
 #endif
 
+// Forward-transform bounds from the product itself (round 5): a signed Montgomery product is below
+// |y| |w| 2^-32 + Q/2 < (Q / 2^32) |y| + Q/2, so a Cooley-Tukey stage takes a bound B to (1 + Q / 2^32) B + Q/2
+// rather than B + Q.  From signed digits (B ~ 0): ten stages stay below 6.67 Q for Q < 2^28 (Q / 2^32 < 1/16),
+// inside the 8 Q of 32-bit signed words, so FM 2 needs no reduction (the LMKCDEY accumulator bound grows from
+// 2.0 Q to 2.2 Q: four digits < 6.67 Q times keys < Q, 26.7 Q^2 2^-32 + Q/2); and for Q < 2^29 (1/8) five
+// stages stay below 3.21 Q < 4 Q, so K1w's QM 2 reduces after five stages and after nine (below 0.9 Q each
+// time, 3.84 Q before the second) instead of after three, six and nine; for Q < 2^28 eleven stages stay below
+// 7.59 Q < 8 Q, so K1w's QM 1 (STD256Q_LMKCDEY) drops its one reduction.  FHE_FWD_TIGHT=0: the round-4 points.
+#ifndef FHE_FWD_TIGHT
+#define FHE_FWD_TIGHT 1
+#endif
+
 namespace fhe_amd {
 
 namespace {
@@ -228,7 +240,7 @@ FHE_DEV void fwd_pass2(uint32_t (&v)[32], uint32_t (&u)[32], uint32_t* tile, int
     }
     transpose32(v, tile, l);
     transpose32(u, tile, l);
-    if (FM == 2) {
+    if (FM == 2 && !FHE_FWD_TIGHT) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             v[r] = smont_mul(v[r], m.oneR, m);
@@ -267,7 +279,7 @@ FHE_DEV void fwd_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
         }
     }
     transpose32(v, tile, l);
-    if (FM == 2) {
+    if (FM == 2 && !FHE_FWD_TIGHT) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = smont_mul(v[r], m.oneR, m);
     }
@@ -438,13 +450,7 @@ FHE_DEV void inv_pass_s(uint32_t (&v)[32], uint32_t* tile, int l, const uint32_t
 FHE_DEV uint32_t other_half(uint32_t x, int xaddr) { return (uint32_t)__builtin_amdgcn_ds_bpermute(xaddr, (int)x); }
 
 // key vector load
-#if defined(FHE_ABL_KEYS) && FHE_ABL_KEYS == 1   // timing ablations only (wrong results): keys from a 4 KB L1-resident block
-FHE_DEV uint4 kload(const uint4* p, size_t i) { return p[i & 255]; }
-#elif defined(FHE_ABL_KEYS) && FHE_ABL_KEYS == 2  // no key loads at all
-FHE_DEV uint4 kload(const uint4*, size_t i) { const uint32_t v = (uint32_t)i; return make_uint4(v, v, v, v); }
-#else
 FHE_DEV uint4 kload(const uint4* p, size_t i) { return p[i]; }
-#endif
 FHE_DEV uint32_t brv5(uint32_t x) { return __builtin_bitreverse32(x) >> 27; }
 
 // SignedDigitDecompose (rgsw-acc.cpp:54-91) for digitsG = 3: centre x in [0, Q) to
@@ -829,18 +835,32 @@ FHE_DEV void automorphism_eval(uint32_t (&v)[32], uint32_t* region, int l, uint3
 FHE_DEV int wt64(int x) { return x + ((x >> 6) << 2); }
 struct InvPlanWW {
     bool red[10][16];  // reduce register r before stage s (C bit 0, C bit 1, B bits 0..3, A bits 0..2, last)
+    bool redT[2][16];  // ... before the C -> B / B -> A transpose
     int fin[8];        // last-stage sum: |x + y| < 2^fin Q
+    int cost;          // 2 per reduction + 1 per final conditional subtraction (their issue-cycle ratio)
 };
+// a transpose mixes every register, so the largest bound reaches all of them: registers above the
+// threshold TT[k] are reduced before transpose k (round 5; without it the A stages of the LMKCDEY
+// automorphism's inverse took 36 reductions per lane, with it 16).  make_inv_plan_ww searches the thresholds.
 template <int BIN, int LIM>
-constexpr InvPlanWW make_inv_plan_ww() {
+constexpr InvPlanWW inv_plan_ww_t(int T0, int T1) {
     InvPlanWW p{};
     int B[16] = {};
     for (int r = 0; r < 16; ++r) B[r] = BIN;
     const int bits[10] = {0, 1, 0, 1, 2, 3, 0, 1, 2, 3};
+    int nred = 0;
     for (int st = 0; st < 10; ++st) {
-        if (st == 2 || st == 6) {  // a transpose mixes every register
+        if (st == 2 || st == 6) {
+            const int k = st == 2 ? 0 : 1, T = k ? T1 : T0;
             int U = 0;
-            for (int r = 0; r < 16; ++r) U = B[r] > U ? B[r] : U;
+            for (int r = 0; r < 16; ++r) {
+                if (B[r] > T) {
+                    B[r]         = 10;
+                    p.redT[k][r] = true;
+                    ++nred;
+                }
+                U = B[r] > U ? B[r] : U;
+            }
             for (int r = 0; r < 16; ++r) B[r] = U;
         }
         const int bt = bits[st];
@@ -851,6 +871,7 @@ constexpr InvPlanWW make_inv_plan_ww() {
                 const int e  = B[r] >= B[q] ? r : q;
                 B[e]         = 10;
                 p.red[st][e] = true;
+                ++nred;
             }
             if (st == 9) {
                 int f = 0;
@@ -861,7 +882,24 @@ constexpr InvPlanWW make_inv_plan_ww() {
             B[q] = 10;
         }
     }
+    p.cost = 2 * nred;
+    for (int r = 0; r < 8; ++r) p.cost += p.fin[r] + 1;
     return p;
+}
+constexpr int kPlanT[8] = {10, 15, 20, 30, 40, 60, 80, 1 << 20};  // candidate thresholds (the last: none)
+#ifndef FHE_PLAN_T
+#define FHE_PLAN_T 1  // 0: no reductions before the transposes (the round-4 plans)
+#endif
+constexpr int kPlanTN = FHE_PLAN_T ? 8 : 0;
+template <int BIN, int LIM>
+constexpr InvPlanWW make_inv_plan_ww() {
+    InvPlanWW best = inv_plan_ww_t<BIN, LIM>(kPlanT[7], kPlanT[7]);
+    for (int a = 0; a < kPlanTN; ++a)
+        for (int b = 0; b < kPlanTN; ++b) {
+            const InvPlanWW p = inv_plan_ww_t<BIN, LIM>(kPlanT[a], kPlanT[b]);
+            if (p.cost < best.cost) best = p;
+        }
+    return best;
 }
 // EVAL (layout C, |v| < BIN Q / 10) -> canonical COEF (layout A); the keys carry N^-1, so the last
 // stage scales by TableI[1] only (as inv_pass_s).  tile: 1088 words of this wave; s_tabI: TableI.
@@ -873,6 +911,11 @@ FHE_DEV void inv_wave_s(uint32_t (&v)[16], uint32_t* tile, int L, const uint32_t
 #pragma unroll
         for (int r = 0; r < 16; ++r)
             if (P.red[st][r]) v[r] = smont_mul(v[r], oneR, m);
+    };
+    auto redt = [&](int k) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (P.redT[k][r]) v[r] = smont_mul(v[r], oneR, m);
     };
     auto gs = [&](uint32_t& x, uint32_t& y, uint32_t w) {
         const uint32_t t = x + y;
@@ -895,6 +938,7 @@ FHE_DEV void inv_wave_s(uint32_t (&v)[16], uint32_t* tile, int L, const uint32_t
         gs(v[4 * hh + 1], v[4 * hh + 3], w1);
     }
     // C -> B
+    redt(0);
 #pragma unroll
     for (int hh = 0; hh < 4; ++hh)
         *reinterpret_cast<uint4*>(tile + wt64((hh << 8) | (L << 2))) = make_uint4(v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]);
@@ -913,6 +957,7 @@ FHE_DEV void inv_wave_s(uint32_t (&v)[16], uint32_t* tile, int L, const uint32_t
         }
     }
     // B -> A
+    redt(1);
 #pragma unroll
     for (int r = 0; r < 16; ++r) tile[wt64((G << 6) | (r << 2) | jj)] = v[r];
     wave_lds_sync();
@@ -972,6 +1017,8 @@ FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* 
 
 }  // namespace
 
+// |acc| between ops (units of Q/10): 2 Q, or 2.2 Q for Q >= 2^27 with FHE_FWD_TIGHT (see there)
+template <bool LZ> constexpr int kLmkAcc = (!LZ && FHE_FWD_TIGHT) ? 22 : 20;
 // DM: the AP/DM accumulator runs the same op loop with external products only (AddToAccDM ==
 // AddToAccLMKCDEY, rgsw-acc-dm.cpp:119-145) and no initial automorphism of acc1.
 // DM needs no automorphism path and fits 168 VGPRs: 3 waves per SIMD
@@ -1065,7 +1112,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
             uint4 kq[KPF + 1][4];
 #pragma unroll
             for (int r = 0; r < 32; ++r) dA[r] = acc[r];
-            inv_pass_s<20, LZ, !DM && FHE_LMK_PRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
+            inv_pass_s<kLmkAcc<LZ>, LZ, !DM && FHE_LMK_PRE>(dA, tile, l, twAi, s_twBi, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 32; ++r) decompose2<true>(dA[r], dec, dA[r], dB[r]);
             fwd_pass2<FM, !DM && FHE_LMK_PRE>(dA, dB, tile, l, twAf, s_twBf, m);
@@ -1101,8 +1148,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                     const uint32_t D0 = dA[r], D2 = dB[r];
                     const uint32_t D1 = PIPE ? xq[kk & 1][2 * e] : other_half(dA[r], xaddr);
                     const uint32_t D3 = PIPE ? xq[kk & 1][2 * e + 1] : other_half(dB[r], xaddr);
-                    // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28): |S| < 40 Q^2 or 24 Q^2, so
-                    // |S| 2^-32 + Q/2 < 2Q
+                    // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28; 6.67Q with FHE_FWD_TIGHT): |S| < 40 Q^2
+                    // or 24 Q^2 (26.7 Q^2), so |S| 2^-32 + Q/2 < 2Q (2.2Q: kLmkAcc)
                     const int64_t S = (int64_t)mac4<true>(D0, D1, D2, D3, KC(0), KC(1), KC(2), KC(3), 0);
                     acc[r] = smont_red(S, m);
 #undef KC
@@ -1122,7 +1169,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                 // digits scattered into the two tiles in A' order (digit A for half 0, B for half 1)
                 uint32_t a0[16];
                 automorphism_wide(acc, a0, tile, tileW, l, lane, kexp);
-                inv_wave_s<20, LZ>(a0, tileW, lane, s_tabI, T.w1R, m.oneR, m);
+                inv_wave_s<kLmkAcc<LZ>, LZ>(a0, tileW, lane, s_tabI, T.w1R, m.oneR, m);
 #if FHE_LMK_SWAP
                 // coefficient x = (r << 6) | lane goes to half-wave register (x >> 5), lane x & 31 of half 0
                 // (digit A) and half 1 (digit B): one half exchange per register pair (v_permlane32_swap:
@@ -1193,7 +1240,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         return;
     }
     // extraction, identical to GINX
-    inv_pass_s<20, LZ>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m.oneR, m);
+    inv_pass_s<kLmkAcc<LZ>, LZ>(acc, tile, l, T.twA_inv, s_twBi, T.w1R, m.oneR, m);
     wave_lds_sync();
     if (h == 0) {
 #pragma unroll
@@ -2162,10 +2209,11 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
     fwd_2k_stage<NP, false>(v, 10, G, twA, m);
     fwd_2k_stage<NP, false>(v, 9, G, twA, m);
     fwd_2k_stage<NP, false>(v, 8, G, twA, m);
-    if (QM == 2) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 3
+    if (QM == 2 && !FHE_FWD_TIGHT) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 3
     fwd_2k_stage<NP, false>(v, 7, G, twA, m);
     fwd_2k_stage<NP, false>(v, 6, G, twA, m);
-    if (QM == 1) red_2k<NP>(v, m);
+    if (QM == 1 && !FHE_FWD_TIGHT) red_2k<NP>(v, m);
+    if (QM == 2 && FHE_FWD_TIGHT) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 5
 #pragma unroll
     for (int p = 0; p < NP; ++p) {  // A -> B
 #pragma unroll
@@ -2176,7 +2224,7 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
         wave_lds_sync();
     }
     fwd_2k_stage<NP, true>(v, 5, G, s_tab, m);
-    if (QM == 2) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 6
+    if (QM == 2 && !FHE_FWD_TIGHT) FRED ? red_2k_f<NP>(v, m) : red_2k<NP>(v, m);  // after stage 6
     fwd_2k_stage<NP, true>(v, 4, G, s_tab, m);
     fwd_2k_stage<NP, true>(v, 3, G, s_tab, m);
     fwd_2k_stage<NP, true>(v, 2, G, s_tab, m);
@@ -2208,18 +2256,29 @@ FHE_DEV void fwd_2k_s(uint32_t (&v)[NP][32], uint32_t* t, int L, const uint32_t*
 // transpose precedes stages 1 and 6
 struct InvPlan2k {
     bool red[11][32];
+    bool redT[2][32];  // before the C -> B / B -> A transpose (as InvPlanWW)
     int fin[16];
+    int cost;
 };
 template <int BIN, int LIM>
-constexpr InvPlan2k make_inv_plan_2k() {
+constexpr InvPlan2k inv_plan_2k_t(int T0, int T1) {
     InvPlan2k p{};
     int B[32] = {};
     for (int r = 0; r < 32; ++r) B[r] = BIN;
     const int bits[11] = {0, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4};
+    int nred = 0;
     for (int st = 0; st < 11; ++st) {
         if (st == 1 || st == 6) {
+            const int k = st == 1 ? 0 : 1, T = k ? T1 : T0;
             int U = 0;
-            for (int r = 0; r < 32; ++r) U = B[r] > U ? B[r] : U;
+            for (int r = 0; r < 32; ++r) {
+                if (B[r] > T) {
+                    B[r]         = 10;
+                    p.redT[k][r] = true;
+                    ++nred;
+                }
+                U = B[r] > U ? B[r] : U;
+            }
             for (int r = 0; r < 32; ++r) B[r] = U;
         }
         const int bt = bits[st];
@@ -2230,6 +2289,7 @@ constexpr InvPlan2k make_inv_plan_2k() {
                 const int e = B[r] >= B[q] ? r : q;
                 B[e]        = 10;
                 p.red[st][e] = true;
+                ++nred;
             }
             if (st == 10) {
                 int f = 0;
@@ -2240,7 +2300,19 @@ constexpr InvPlan2k make_inv_plan_2k() {
             B[q] = 10;
         }
     }
+    p.cost = 2 * nred;
+    for (int r = 0; r < 16; ++r) p.cost += p.fin[r] + 1;
     return p;
+}
+template <int BIN, int LIM>
+constexpr InvPlan2k make_inv_plan_2k() {
+    InvPlan2k best = inv_plan_2k_t<BIN, LIM>(kPlanT[7], kPlanT[7]);
+    for (int a = 0; a < kPlanTN; ++a)
+        for (int b = 0; b < kPlanTN; ++b) {
+            const InvPlan2k p = inv_plan_2k_t<BIN, LIM>(kPlanT[a], kPlanT[b]);
+            if (p.cost < best.cost) best = p;
+        }
+    return best;
 }
 // signed inverse NTT, layout C (EVAL, |v| < BIN Q / 10) -> A (COEF), canonical [0, Q); the keys carry
 // N^-1, so the last stage scales by TableI[1] only (w1R)
@@ -2255,6 +2327,11 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
         for (int r = 0; r < 32; ++r)
             if (P.red[st][r]) v[r] = smont_mul(v[r], oneR, m);
     };
+    auto redt = [&](int k) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r)
+            if (P.redT[k][r]) v[r] = smont_mul(v[r], oneR, m);
+    };
     auto gs = [&](uint32_t& x, uint32_t& y, uint32_t w) {
         const uint32_t s = x + y;
         y                = smont_mul(x - y, w, m);
@@ -2268,6 +2345,7 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
 #pragma unroll
     for (int rh = 0; rh < 16; ++rh) gs(v[2 * rh], v[2 * rh + 1], s_tabI[1024 + (rh << 6) + L]);
     // C -> B
+    redt(0);
 #pragma unroll
     for (int rh = 0; rh < 16; ++rh)
         *reinterpret_cast<uint2*>(tc + 132 * rh) = make_uint2(v[2 * rh], v[2 * rh + 1]);
@@ -2286,6 +2364,7 @@ FHE_DEV void inv_2k_s(uint32_t (&v)[32], uint32_t* t, int L, const uint32_t* __r
         }
     }
     // B -> A
+    redt(1);
 #pragma unroll
     for (int r = 0; r < 32; ++r) tb[2 * r] = v[r];
     wave_lds_sync();
@@ -2626,7 +2705,10 @@ namespace {
 // |acc| between ops, units of Q/10: 2 (ND (11 Q + 2^(g-1)) Q 2^-32 + Q/2) for Q < 2^27; Q28 (ND = 2,
 // 2^27 <= Q < 2^28, the forward transform reduced once): 2 (2 (6.82 Q) Q 2^-32 + Q/2) < 2.8 Q
 // QM 2 (Q < 2^29, digits below 3 Q after the forward transform): 2 (ND 3 Q Q 2^-32 + Q/2) -> 33 (ND 3)
-template <int ND, int QM> constexpr int kL2AccBound = QM == 1 ? (ND == 3 ? 36 : 28) : QM == 2 ? (ND == 3 ? 33 : 25) : 33;
+// FHE_FWD_TIGHT, Q28: no forward reduction, digits below 7.59 Q (see there): 2 (ND 7.59 Q Q 2^-32 + Q/2) -> 29 / 39
+template <int ND, int QM>
+constexpr int kL2AccBound = QM == 1 ? (FHE_FWD_TIGHT ? (ND == 3 ? 39 : 29) : (ND == 3 ? 36 : 28))
+                                    : QM == 2 ? (ND == 3 ? 33 : 25) : 33;
 constexpr size_t l2k_lds() { return (size_t)(2048 + 2048 + 2 * kW2Tile) * 4; }
 
 // EVAL automorphism X -> X^k on layout C through this wave's tile (as automorphism_c at N = 1024):
