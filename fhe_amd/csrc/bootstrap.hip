@@ -1277,8 +1277,8 @@ constexpr int kPrepWaves = 4;
 
 // LMKCDEY: the op schedule described at k_blind_rotate_lmk (rgsw-acc-lmkcdey.cpp:83-157).  Lanes compute the group position of every a_i and
 // count them (LDS atomics), a wave scan gives the group starts, a chunked stable placement
-// (rank among equal positions of lower lanes) fills the sorted order, and the nSkips state
-// machine runs on scalar registers over 64-position ballots of the non-empty groups.
+// (rank among equal positions of lower lanes) writes every a_i's index straight to its op slot, whose
+// offsets the nSkips logic gives in closed form per 64 positions (below).
 // NMAX: the largest ring dimension and LWE dimension the LDS arrays hold (1024: the 32-bit sets;
 // 2048: N = 2048 and n up to 2048 for the 64-bit accumulator)
 template <int NMAX>
@@ -1288,7 +1288,6 @@ __global__ void __launch_bounds__(64 * kPrepWaves)
     __shared__ uint32_t s_start[kPrepWaves][NMAX + 1];
     __shared__ uint16_t s_fill[kPrepWaves][NMAX];
     __shared__ uint16_t s_bkt[kPrepWaves][NMAX];
-    __shared__ uint16_t s_sorted[kPrepWaves][NMAX];
     __shared__ uint32_t s_part[kPrepWaves][64];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t gate = blockIdx.x * kPrepWaves + wv;
@@ -1297,7 +1296,6 @@ __global__ void __launch_bounds__(64 * kPrepWaves)
     uint32_t* start = s_start[wv];
     uint16_t* fill = s_fill[wv];
     uint16_t* bkt = s_bkt[wv];
-    uint16_t* sorted = s_sorted[wv];
     for (uint32_t p = lane; p < N; p += 64) start[p] = 0;
     wave_lds_sync();
     for (uint32_t i = lane; i < n; i += 64) {
@@ -1323,12 +1321,54 @@ __global__ void __launch_bounds__(64 * kPrepWaves)
     for (uint32_t t = 0; t < per; ++t) {
         const uint32_t c = start[lane * per + t];
         start[lane * per + t] = run;
-        fill[lane * per + t]  = (uint16_t)run;
         run += c;
     }
     if (lane == 0) start[N] = n;
     wave_lds_sync();
-    // stable placement, 64 items at a time (increasing i within a group)
+    // emission offsets (nSkips logic of rgsw-acc-lmkcdey.cpp:99-157), 64 positions at a time.  The ops
+    // follow the group order 0..N-1 with AUTO ops between groups, so group p's items start at
+    // start[p] + (AUTO ops before them).  Within a half the skip counter before position t is
+    // (t - q) mod numAutoKeys after the last non-empty position q < t (that group leaves it at 1),
+    // else (carry + t) mod numAutoKeys; a position emits at most a pre-group AUTO and a capping AUTO,
+    // so two ballots give every lane its AUTO count below.
+    uint16_t* o = ops + (size_t)gate * maxops;
+    const uint32_t cap = numAutoKeys;
+    uint32_t A = 0;  // AUTO ops emitted so far (wave-uniform)
+    for (uint32_t half = 0; half < 2; ++half) {
+        const uint32_t base = half ? Nh : 0u;
+        uint32_t nS = 0;  // skip counter entering the chunk
+        for (uint32_t tb = 0; tb < Nh - 1; tb += 64) {
+            const uint32_t t = tb + lane, p = base + t;
+            const bool ok = t < Nh - 1;
+            const uint32_t s = ok ? start[p] : 0u, e = ok ? start[p + 1] : 0u;
+            const bool ne = ok && e > s;
+            const uint64_t lowm = (1ull << lane) - 1ull;
+            const uint64_t mb = ballot(ne) & lowm;
+            const uint32_t nsb = mb ? (lane - (63u - (uint32_t)__builtin_clzll(mb))) % cap : (nS + lane) % cap;
+            const bool pre = ne && nsb != 0;
+            const uint32_t aft = ne ? 1u : nsb + 1u;
+            const bool capE = ok && (aft == cap || t == Nh - 2);  // t = Nh - 2: i == 1
+            const uint64_t bp = ballot(pre), bc = ballot(capE);
+            const uint32_t ab = A + __builtin_popcountll(bp & lowm) + __builtin_popcountll(bc & lowm);
+            if (pre) o[s + ab] = (uint16_t)(0x8000u | nsb);
+            if (ok) fill[p] = (uint16_t)(s + ab + (pre ? 1u : 0u));
+            if (capE) o[e + ab + (pre ? 1u : 0u)] = (uint16_t)(0x8000u | aft);
+            A += __builtin_popcountll(bp) + __builtin_popcountll(bc);
+            const uint32_t cnt = (Nh - 1 - tb) < 64 ? Nh - 1 - tb : 64;
+            nS = __builtin_amdgcn_readlane(capE ? 0u : aft, cnt - 1);
+        }
+        if (half == 0) {
+            if (lane == 0) {
+                fill[Nh - 1] = (uint16_t)(start[Nh - 1] + A);  // -1
+                o[start[Nh] + A] = (uint16_t)0x8000u;          // automorphism by 2N - 5 with key 0
+            }
+            ++A;
+        } else if (lane == 0) {
+            fill[N - 1] = (uint16_t)(start[N - 1] + A);       // 0
+        }
+    }
+    wave_lds_sync();
+    // stable placement, 64 items at a time (increasing i within a group), straight into the op list
     for (uint32_t c = 0; c < n; c += 64) {
         const uint32_t i = c + lane;
         const bool valid = i < n;
@@ -1344,54 +1384,12 @@ __global__ void __launch_bounds__(64 * kPrepWaves)
         const uint32_t pos = valid ? fill[b] + rank : 0u;
         wave_lds_sync();
         if (valid) {
-            sorted[pos] = (uint16_t)i;
+            o[pos] = (uint16_t)i;
             if (last) fill[b] = (uint16_t)(pos + 1);
         }
         wave_lds_sync();
     }
-    // emission (nSkips logic of rgsw-acc-lmkcdey.cpp:99-157) on scalar state
-    uint16_t* o = ops + (size_t)gate * maxops;
-    uint32_t k = 0, nSkips = 0;
-    auto emit1 = [&](uint32_t x) {
-        if (lane == 0) o[k] = (uint16_t)x;
-        ++k;
-    };
-    auto emit_group = [&](uint32_t s, uint32_t e) {
-        for (uint32_t q = s; q < e; q += 64)
-            if (q + lane < e) o[k + (q - s) + lane] = sorted[q + lane];
-        k += e - s;
-    };
-    for (uint32_t half = 0; half < 2; ++half) {
-        const uint32_t base = half ? Nh : 0u;
-        for (uint32_t tb = 0; tb < Nh - 1; tb += 64) {
-            const uint32_t t = tb + lane;
-            const bool ok = t < Nh - 1;
-            const uint32_t s = ok ? start[base + t] : 0u, e = ok ? start[base + t + 1] : 0u;
-            const uint64_t ne = ballot(ok && e > s);
-            const uint32_t cnt = (Nh - 1 - tb) < 64 ? Nh - 1 - tb : 64;
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const uint32_t i = Nh - 1 - (tb + j);
-                if ((ne >> j) & 1ull) {
-                    if (nSkips != 0) {
-                        emit1(0x8000u | nSkips);
-                        nSkips = 0;
-                    }
-                    emit_group(__builtin_amdgcn_readlane(s, j), __builtin_amdgcn_readlane(e, j));
-                }
-                nSkips++;
-                if (nSkips == numAutoKeys || i == 1) {
-                    emit1(0x8000u | nSkips);
-                    nSkips = 0;
-                }
-            }
-        }
-        if (half == 0) {
-            emit_group(start[Nh - 1], start[Nh]);  // -1
-            emit1(0x8000u);                        // automorphism by 2N - 5 with key 0
-        } else {
-            emit_group(start[N - 1], start[N]);    // 0
-        }
-    }
+    const uint32_t k = n + A;
     if (lane == 0) {
         nops[gate] = k;
         tvb[gate]  = combine(in, in.b, gate, in.boff, qm, g.xor_double);
@@ -1438,7 +1436,7 @@ hipError_t launch_prep_lmk(const GateArgs& g, const GateInputs& in, const int16_
                            uint16_t* ops, uint32_t* nops, uint32_t* tvb, uint32_t maxops, uint32_t numAutoKeys,
                            hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if (in.k < 1 || in.k > 4) return hipErrorInvalidValue;
+    if (in.k < 1 || in.k > 4 || numAutoKeys == 0) return hipErrorInvalidValue;
     if (g.n > 2048 || (g.N != 512 && g.N != 1024 && g.N != 2048)) return hipErrorInvalidValue;  // LDS sizes
     if (g.n <= 1024 && g.N <= 1024)
         hipLaunchKernelGGL(k_prep_lmk_w<1024>, dim3((g.count + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0,
