@@ -277,6 +277,16 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else None
+    # which devices the ranks ran on, as the process group saw them (the driver's N-GPU line must show N
+    # distinct GPUs under RCCL; a rank sharing a device with another is refused there, marked a rehearsal here)
+    from fhe_amd.dist import check_topology, device_identity, gather_identities, topology_record
+    topo = topology_record(gather_identities(device_identity(torch, dev, rank, local)),
+                           backend if world > 1 else None, rehearsal=bool(dmap))
+    try:
+        check_topology(topo)
+    except RuntimeError as e:
+        log(f"error: {e}")
+        sys.exit(3)
     stream = torch.cuda.Stream(dev)     # a real (non-null) stream: our kernels launch on it and
     assert stream.cuda_stream, "need a non-default stream handle"   # the timing events are recorded on it
     ctx = {"dev": dev, "stream": stream}
@@ -325,6 +335,7 @@ def main():
             "roofline": roofline,
             "valu_roofline": valu,
             "hbm_per_gpu": per_gpu_hbm(args.method, hi - lo, main_r["elapsed"] / args.steps),
+            "distributed": topo,
         }
         if lmk_r is not None:
             lr, lv = rooflines("lmkcdey", lmk_r["B"], lmk_r["br_ms"], lmk_r["ks_ms"])

@@ -130,6 +130,8 @@ def _setup(L):
     L.fhe_hip_eval_func_multi_batch_device.argtypes = [vp, sz, vp, vp, u64, vp, sz, ctypes.c_uint32, vp, vp, vp]
     L.fhe_hip_keygen_ring_secret.argtypes = [ctypes.c_int, ctypes.c_int, u64, vp]
     L.fhe_hip_encrypt_large.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u64, ctypes.c_uint32, vp, vp]
+    L.fhe_hip_gate_kernel.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_char_p)]
+    L.fhe_hip_copy_keys.argtypes = [vp, vp]
     L._binfhe_ready = True
     return L
 
@@ -398,6 +400,22 @@ class GateEngine:
         ao, bo = np.zeros_like(a), np.zeros_like(b)
         check(L().fhe_hip_bootstrap_batch(self._h, b.size, ptr(a), ptr(b), ptr(ao), ptr(bo)))
         return ao, bo
+
+    def gate_kernel(self, count):
+        """the blind-rotation kernel a gate batch of `count` runs on in this context (fhe_hip_gate_kernel)"""
+        name = ctypes.c_char_p()
+        check(L().fhe_hip_gate_kernel(self._h, count, ctypes.byref(name)))
+        return name.value.decode()
+
+    def kernel(self):
+        """fhe_hip_params::kernel of this context (its own kernel flags, fhe_hip_get_params)"""
+        p = _Params()
+        check(L().fhe_hip_get_params(self._h, ctypes.byref(p)))
+        return p.kernel
+
+    def copy_keys_from(self, src):
+        """the resident keys of another context of the same set (fhe_hip_copy_keys)"""
+        check(L().fhe_hip_copy_keys(self._h, src._h))
 
     def close(self):
         if self._h:
@@ -774,11 +792,17 @@ class BinFHEContext:
             self.engine.load_keys_cereal(bsk.data, kskA.data)
         else:
             self.engine.load_keys(bsk, kskA, kskB)
+        # the loaded keys may come from elsewhere: their RLWE secret is not the one BTKeyGen's seed derives,
+        # so LARGE_DIM encryption (which needs it) refuses until the next BTKeyGen
+        self._key_seed = None
 
     def Encrypt(self, sk, m, output=None, p=4, mod=0):
-        """Encrypt(sk, m, SMALL_DIM, p, mod) (binfhecontext.cpp:220-234).  output = LARGE_DIM: the
-        dimension-N encryption mod Q that Encrypt(pk, m, LARGE_DIM, p) makes (:236-252), under the RLWE
-        secret of the keys BTKeyGen generated"""
+        """Encrypt(sk, m, SMALL_DIM, p, mod) (binfhecontext.cpp:220-234).  output = LARGE_DIM: a
+        dimension-N ciphertext mod Q like the one Encrypt(pk, m, LARGE_DIM, p) makes (:236-252), under the RLWE
+        secret of the keys BTKeyGen generated (refused after BTKeyLoad: the loaded keys' secret is unknown).
+        The reference's LARGE_DIM encryption is public-key (EncryptN); this one is symmetric under that
+        secret, so it decrypts and bootstraps the same but its noise distribution is not the reference's
+        (parity of the distribution is unpinned; outputs of gates on it are pinned by tests/test_mixed.py)"""
         if output == LARGE_DIM:
             if getattr(self, "_key_seed", None) is None:
                 raise FheHipError(-11, "LARGE_DIM encryption needs the keys of BTKeyGen")

@@ -108,6 +108,11 @@ hipError_t launch_repack_ginx2(const void* bsk, uint32_t n, void* bsk2, hipStrea
 hipError_t launch_blind_rotate_ginx2(const GateArgs& g, const BootTables& t, const void* bsk2, const uint16_t* idx,
                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 bool ginx2_supported(const GateArgs& g, const BootTables& t);
+// K1x: two waves per gate with K1w's one-word exchange (the small-batch GINX kernel), same support as K1s;
+// keys repacked from the resident layout into [i][c][q < 4][k2 < 8][64 lanes][4 words] (launch_repack_ginx2x)
+hipError_t launch_repack_ginx2x(const void* bsk, uint32_t n, void* bskx, hipStream_t s);
+hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
+                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 // The same split kernel with three retained digits per component (digitsG = 4 at N = 1024, Q < 2^27:
 // STD128_3, STD128Q; with q = 2N: STD128_4, LPF_STD128, LPF_STD128Q) for the sets whose keys otherwise
 // live on the 64-bit accumulator: keys in the g2_key_word layout (nd = 3), u64 ctExt into that

@@ -31,6 +31,12 @@
 #ifndef FHE_WAVES_PER_EU
 #define FHE_WAVES_PER_EU 2
 #endif
+#ifndef FHE_K1_PRIO
+#define FHE_K1_PRIO 0     // A/B: K1's waves of odd workgroup slots on a CU at priority 1
+#endif
+#ifndef FHE_K1_STAGGER
+#define FHE_K1_STAGGER 0  // A/B: odd workgroup slots start FHE_K1_STAGGER x 8128 cycles late
+#endif
 
 // Forward-transform bounds from the product itself (round 5): a signed Montgomery product is below
 // |y| |w| 2^-32 + Q/2 < (Q / 2^32) |y| + Q/2, so a Cooley-Tukey stage takes a bound B to (1 + Q / 2^32) B + Q/2
@@ -597,6 +603,14 @@ __global__ void __launch_bounds__(256, FHE_WAVES_PER_EU)
     uint32_t* tile  = tileW + h * kTile;
     const Mod m0 = make_mod(T);
     const Mod& m  = m0;
+#if FHE_K1_PRIO || FHE_K1_STAGGER
+    uint32_t hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    const uint32_t tgs = (hwid >> 16) & 15;  // the workgroup's slot on its CU
+    if (FHE_K1_PRIO && (tgs & 1)) __builtin_amdgcn_s_setprio(1);
+    if (tgs & 1)
+        for (int z = 0; z < FHE_K1_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
+#endif
 
     // test vector (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
     uint32_t acc[32];
@@ -1522,11 +1536,14 @@ constexpr size_t g2_lds(int nd) { return (size_t)(1024 + 1024 + 2 * kMonoHalfWor
 // key layout: boot.h g2_key_word / g2_row
 
 // signed forward NTT of NP polynomials, layout A (|v| < B) -> C (|v| < B + 10 Q); polynomial p
-// goes through the tile t + p kG2Tile
-template <int NP>
+// goes through the tile t + p kG2Tile, or with NT = 1 all of them through the one tile t in turn
+// t1 (optional): the tiles of polynomials 1.. at t1, t1 + kG2Tile, .. instead of after t
+template <int NP, int NT = NP>
 FHE_DEV void fwd_wave_s(uint32_t (&v)[NP][16], uint32_t* t, int L, const uint32_t* __restrict__ twA,
-                        const uint32_t* s_tab, const Mod& m) {
+                        const uint32_t* s_tab, const Mod& m, uint32_t* t1 = nullptr) {
+    static_assert(NT == NP || NT == 1, "one tile per polynomial, or one tile for all");
     const int G = L >> 2, jj = L & 3;
+    auto tp = [&](int p) { return p == 0 ? t : t1 ? t1 + (p - 1) * kG2Tile : t + p * kG2Tile; };
 #pragma unroll
     for (int b = 9; b >= 6; --b) {
         const int rb = b - 6;
@@ -1538,16 +1555,66 @@ FHE_DEV void fwd_wave_s(uint32_t (&v)[NP][16], uint32_t* t, int L, const uint32_
             for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
         }
     }
+    if (NT == 1 && NP > 1) {  // both transposes polynomial by polynomial through the one tile
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t[wt64((r << 6) | L)] = v[p][r];
+            wave_lds_sync();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[p][r] = t[wt64((G << 6) | (r << 2) | jj)];
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int b = 5; b >= 2; --b) {
+            const int rb = b - 2;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                if (r & (1 << rb)) continue;
+                const uint32_t w = s_tab[(1 << (9 - b)) + (G << (5 - b)) + (r >> (rb + 1))];
+#pragma unroll
+                for (int p = 0; p < NP; ++p) ct_bf_s(v[p][r], v[p][r | (1 << rb)], w, m);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t[wt64((G << 6) | (r << 2) | jj)] = v[p][r];
+            wave_lds_sync();
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const uint4 q = *reinterpret_cast<const uint4*>(t + wt64((hh << 8) | (L << 2)));
+                v[p][4 * hh] = q.x; v[p][4 * hh + 1] = q.y; v[p][4 * hh + 2] = q.z; v[p][4 * hh + 3] = q.w;
+            }
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh) {
+            const uint32_t w1 = s_tab[256 + (hh << 6) + L];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                ct_bf_s(v[p][4 * hh], v[p][4 * hh + 2], w1, m);
+                ct_bf_s(v[p][4 * hh + 1], v[p][4 * hh + 3], w1, m);
+            }
+            const uint2 w0 = *reinterpret_cast<const uint2*>(s_tab + 512 + (hh << 7) + (L << 1));
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                ct_bf_s(v[p][4 * hh], v[p][4 * hh + 1], w0.x, m);
+                ct_bf_s(v[p][4 * hh + 2], v[p][4 * hh + 3], w0.y, m);
+            }
+        }
+        return;
+    }
     // A -> B
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) t[p * kG2Tile + wt64((r << 6) | L)] = v[p][r];
+        for (int p = 0; p < NP; ++p) tp(p)[wt64((r << 6) | L)] = v[p][r];
     wave_lds_sync();
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) v[p][r] = t[p * kG2Tile + wt64((G << 6) | (r << 2) | jj)];
+        for (int p = 0; p < NP; ++p) v[p][r] = tp(p)[wt64((G << 6) | (r << 2) | jj)];
 #pragma unroll
     for (int b = 5; b >= 2; --b) {
         const int rb = b - 2;
@@ -1564,13 +1631,13 @@ FHE_DEV void fwd_wave_s(uint32_t (&v)[NP][16], uint32_t* t, int L, const uint32_
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) t[p * kG2Tile + wt64((G << 6) | (r << 2) | jj)] = v[p][r];
+        for (int p = 0; p < NP; ++p) tp(p)[wt64((G << 6) | (r << 2) | jj)] = v[p][r];
     wave_lds_sync();
 #pragma unroll
     for (int hh = 0; hh < 4; ++hh)
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-            const uint4 q = *reinterpret_cast<const uint4*>(t + p * kG2Tile + wt64((hh << 8) | (L << 2)));
+            const uint4 q = *reinterpret_cast<const uint4*>(tp(p) + wt64((hh << 8) | (L << 2)));
             v[p][4 * hh] = q.x; v[p][4 * hh + 1] = q.y; v[p][4 * hh + 2] = q.z; v[p][4 * hh + 3] = q.w;
         }
     wave_lds_sync();
@@ -1863,6 +1930,259 @@ hipError_t launch_blind_rotate_ginx3(const GateArgs& g, const BootTables& t, con
     else if (mf) FHE_LAUNCH_G3(true, false);
     else FHE_LAUNCH_G3(false, false);
 #undef FHE_LAUNCH_G3
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K1x: GINX at N = 1024 with two waves per gate and K1w's exchange (k_blind_rotate_ginx2x), the
+// small-batch kernel: at 1024 STD128 gates (config 3) the one-wave kernel K1 has one wave per SIMD,
+// which issues VALU in 68% of its cycles.  Wave c owns component c in layout C (16 registers x 64 lanes,
+// as K1s).  Per index (AddToAccCGGI, rgsw-acc-cggi.cpp:102-151): inverse NTT of acc_c, SignedDigitDecompose
+// into its 2 retained digits (rgsw-acc.cpp:54-91; digit rows c and 2 + c), forward NTT of both; then per
+// slot its OWN digits times the key columns of BOTH components: the sum for component c, with the
+// monomials and acc_c folded in, is reduced into acc_c; the other one is reduced to one word per slot and
+// written to this wave's exchange buffer (i & 1); one workgroup barrier; the partner's word is added.  The
+// transpose tile is private to the wave and the exchange buffers alternate, so one barrier per index
+// suffices (K1s exchanges the digit polynomials: two barriers per index and the partner's digits read
+// inside the MAC).  acc_c <- acc_c + S+_c (X^a - 1) + S-_c (X^-a - 1) as in K1; only the order of the
+// modular additions differs, so the outputs are the same.
+// Keys (launch_repack_ginx2x from the resident layout), per index i and wave c: [c][q < 4][k2 < 8][64][4]
+// = (K+[r], K+[r+1], K-[r], K-[r+1]), r = 2 k2, slot x(L, r) of layout C; q = 2 j + o: digit row 2 j + c,
+// column c (o = 0) or 1 - c (o = 1).
+// Bounds (Q < 2^27): |D| < 10 Q + 2^(g-1) after the forward NTT; |S+-| < 2 (10 Q + 2^9) Q < 21 Q^2, so
+// |hi(S)| < 0.66 Q; the own word is below 2 Q + 0.04 Q + A Q / 2^32 + Q / 2 < 2.54 Q + A / 32, the
+// partner's below 2.54 Q: A < 5.3 Q between indices (the inverse plan's BIN, as K1w's kW2AccBound).
+// ---------------------------------------------------------------------------
+namespace {
+#ifndef FHE_X_GATES
+#define FHE_X_GATES 2   // gates per workgroup (two waves each)
+#endif
+#ifndef FHE_X_TILES
+#define FHE_X_TILES 2   // transpose tiles of the forward NTT: 1 (the two digit polynomials in turn) or 2
+#endif
+#ifndef FHE_X_ABL
+#define FHE_X_ABL 0     // timing-only ablations (wrong results): 1 no barrier, 2 no key loads
+#endif
+#if FHE_X_ABL == 2
+#define XKEY(p, o) make_uint4((uint32_t)(o), (uint32_t)(o) ^ 5u, (uint32_t)(o) + 3u, (uint32_t)(size_t)(p))
+#else
+#define XKEY(p, o) (p)[o]
+#endif
+#ifndef FHE_X_PRIO
+#define FHE_X_PRIO 0    // A/B: waves of odd workgroup slots on a CU at priority 1
+#endif
+#ifndef FHE_X_STAGGER
+#define FHE_X_STAGGER 0 // A/B: odd workgroup slots start FHE_X_STAGGER x 8128 cycles late (phase offset)
+#endif
+constexpr int kXGates = FHE_X_GATES;
+constexpr int kXTiles = FHE_X_TILES;
+// words per wave: a transpose tile and two exchange buffers (padded to tiles: with kXTiles = 2 the exchange
+// buffer of index i is the forward transform's second tile before it takes the partner's words, see below)
+constexpr int kXWave  = 3 * kG2Tile;
+constexpr int kXAcc   = 53;                            // |acc| < 5.3 Q between indices (units of Q/10)
+constexpr size_t x_lds() { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 2 * kXGates * kXWave) * 4; }
+static_assert(x_lds() <= 160 * 1024, "LDS per workgroup");
+static_assert(kXTiles == 1 || kXTiles == 2, "transpose tiles");
+}  // namespace
+
+__global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
+    k_blind_rotate_ginx2x(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
+                          const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
+                          const uint32_t* __restrict__ twAf) {
+    constexpr int ND = 2, kQ = 2 * ND;  // key vectors per slot pair: 2 digit rows x 2 columns
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_tab  = sm;
+    uint32_t* s_tabI = sm + 1024;
+    uint2* s_mono2   = reinterpret_cast<uint2*>(sm + 2048);
+    uint32_t* s_wave = sm + 2048 + 2 * kMonoHalfWords;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        s_tab[i]  = T.tabF[i];
+        s_tabI[i] = T.tabI[i];
+    }
+    for (int i = threadIdx.x; i < kMonoHalfWords; i += blockDim.x) s_mono2[i] = make_uint2(T.monoP[i], T.mono[i]);
+
+    const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int c = wave & 1;  // RLWE component of this wave
+    const uint32_t gslot = blockIdx.x * kXGates + (wave >> 1);
+    const bool live = gslot < g.count;
+    const uint32_t gate = live ? gslot : g.count - 1;  // spare waves shadow the last gate: every wave meets every barrier
+    uint32_t* tile = s_wave + wave * kXWave;
+    uint32_t* xown = tile + kG2Tile;                                   // exchange buffers, this wave's ...
+    const uint32_t* xpar = s_wave + (wave ^ 1) * kXWave + kG2Tile + L;  // ... and the partner's
+    const Mod m0 = make_mod(T);
+    const Mod& m = m0;
+    __syncthreads();
+#if FHE_X_PRIO || FHE_X_STAGGER
+    uint32_t hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    const uint32_t tgs = (hwid >> 16) & 15;  // the workgroup's slot on its CU
+#endif
+#if FHE_X_PRIO
+    if (tgs & 1) __builtin_amdgcn_s_setprio(1);
+#endif
+#if FHE_X_STAGGER
+    if (tgs & 1)
+        for (int z = 0; z < FHE_X_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
+#endif
+
+    // initial accumulator (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
+    uint32_t acc[16];
+    if (c == 1) {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        uint32_t tv[1][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            uint32_t v = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            tv[0][r] = v;
+        }
+        fwd_wave_s<1>(tv, tile, L, twAf, s_tab, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);  // (-Q, Q), N^-1 scaled
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0;
+    }
+
+    const uint16_t* gidx = idx + (size_t)gate * g.n;
+    const DecN dec = make_decn(m.Q, g.gbits, ND);
+    // monomial index of slot x(L, r) in half-table units, as K1s: a per-lane part as' (8 brv6(L) + 1) and a
+    // per-register part as' (512 brv2(r & 3) + 2 brv2(r >> 2)); registers 2 k2 and 2 k2 + 1 share it
+    const uint32_t lmul = 8 * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1;
+    const uint4* kc = keys + (size_t)c * (kQ * 8 * 64) + L;
+    for (uint32_t i = 0; i < g.n; ++i) {
+        const Mod m = fresh_nq(m0);
+        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> 1;  // even exponents (ctmod < 2N)
+        const uint4* kb = kc + (size_t)i * (2 * kQ * 8 * 64);
+#if FHE_X_ABL == 2
+        asm volatile("" : "+v"(kb));
+#endif
+        uint4 kq[2][kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) kq[0][q] = XKEY(kb, (q * 8 + 0) * 64);
+        uint32_t d[ND][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
+        inv_wave_s<kXAcc, true>(d[0], tile, L, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+        // the second digit polynomial's tile: this index's exchange buffer, whose last contents (index i - 2)
+        // the partner read before it reached the barrier of index i - 1, which this wave has passed
+        uint32_t* xb = xown + (i & 1) * kG2Tile;
+        fwd_wave_s<ND, kXTiles>(d, tile, L, twAf, s_tab, m, xb);
+        if (kXTiles == 2) wave_lds_sync();  // its last reads done before the partner words overwrite it
+        const uint32_t fl = (as * lmul) & 1023u;
+        uint32_t* xo = xb + L;
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) {
+            if (k2 + 1 < 8) {
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) kq[(k2 + 1) & 1][q] = XKEY(kb, (q * 8 + k2 + 1) * 64);
+            }
+            asm volatile("" ::: "memory");
+            const int r0 = 2 * k2;
+            const uint32_t ur = __builtin_amdgcn_readfirstlane(
+                (as * (512u * (__builtin_bitreverse32((uint32_t)(r0 & 3)) >> 30) +
+                       2u * (__builtin_bitreverse32((uint32_t)(r0 >> 2)) >> 30))) & 1023u);
+            const uint32_t f  = fl + ur;    // < 2N
+            const uint32_t fn = 2048u - f;  // -a: 2N - f
+            const uint2 mp = s_mono2[f + (f >> 5)], mn = s_mono2[fn + (fn >> 5)];
+            const uint4* q4 = kq[k2 & 1];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r = r0 + e;
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {  // o = 0: this wave's component, 1: the partner's
+                    int64_t S1 = 0, S2 = 0;
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) {
+                        const uint4 kv = q4[2 * j + o];
+                        S1 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.y : kv.x);
+                        S2 += (int64_t)(int32_t)d[j][r] * (int32_t)(e ? kv.w : kv.z);
+                    }
+                    int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
+                    S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
+                    if (o == 0) {
+                        S += (int64_t)(int32_t)acc[r] * (int32_t)T.oneR;
+                        acc[r] = smont_red(S, m);
+                    } else {
+                        xo[r << 6] = smont_red(S, m);
+                    }
+                }
+            }
+        }
+        // both waves' partner words are in LDS (the buffer i & 1 is written again at index i + 2, after the
+        // partner has passed the next barrier, i.e. after it read this one)
+#if FHE_X_ABL != 1
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#endif
+        const uint32_t* xp = xpar + (i & 1) * kG2Tile;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += xp[r << 6];
+    }
+
+    // extraction (binfhe-base-scheme.cpp:110-121): canonical COEF in layout A; wave 0 writes the transposed
+    // acc0 (coefficient k -> position N - k, negated), wave 1 the b term from acc1[0] (tile private: no barrier)
+    inv_wave_s<kXAcc, true>(acc, tile, L, s_tabI, T.w1R, m.oneR, m);
+    if (!live) return;
+    if (c == 0) {
+        uint32_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            const uint32_t v = acc[r];
+            const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
+            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+        }
+    } else if (L == 0) {
+        const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
+        ext_b[gate] = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+// the resident GINX layout (ginx_u4_off, half-swapped rows) -> the k_blind_rotate_ginx2x layout
+__global__ void k_repack_ginx2x(const uint32_t* __restrict__ src, uint32_t n, uint32_t* __restrict__ dst) {
+    const uint64_t words = (uint64_t)n * 16384;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = t >> 14;
+        const uint32_t w = (uint32_t)(t & 16383);
+        const uint32_t e4 = w & 3, L = (w >> 2) & 63, k2 = (w >> 8) & 7, q = (w >> 11) & 3, c = w >> 13;
+        const uint32_t r = 2 * k2 + (e4 & 1), ks = e4 >> 1;
+        const uint32_t x = ((r >> 2) << 8) | (L << 2) | (r & 3);  // EVAL slot
+        const uint32_t row = 2 * (q >> 1) + c, col = c ^ (q & 1);
+        const uint32_t lane = col * 32 + (x >> 5), kk = (x & 31) >> 1, e = x & 1;
+        const uint32_t dpos = kBskHalfSwap ? row ^ col : row;
+        dst[t] = src[i * 16384 + ginx_u4_off(ks, dpos, kk, lane, e)];
+    }
+}
+
+hipError_t launch_repack_ginx2x(const void* bsk, uint32_t n, void* bskx, hipStream_t s) {
+    const uint64_t words = (uint64_t)n * 16384;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((words + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_repack_ginx2x, dim3(blocks), dim3(256), 0, s, static_cast<const uint32_t*>(bsk), n,
+                       static_cast<uint32_t*>(bskx));
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
+                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!ginx2_supported(g, t)) return hipErrorInvalidValue;
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2x),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)x_lds());
+        return true;
+    }();
+    (void)attr;
+    const uint32_t blocks = (g.count + kXGates - 1) / kXGates;
+    hipLaunchKernelGGL(k_blind_rotate_ginx2x, dim3(blocks), dim3(128 * kXGates), x_lds(), s, g, t,
+                       static_cast<const uint4*>(bskx), idx, tvb, ext_a, ext_b, t.twA_fwd);
     return hipGetLastError();
 }
 

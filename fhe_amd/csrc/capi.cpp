@@ -258,7 +258,16 @@ void fhe_hip_destroy(fhe_hip_ctx* ctx) {
 int fhe_hip_get_params(const fhe_hip_ctx* ctx, fhe_hip_params* out) {
     if (!ctx || !out) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     fill_params(ctx->eng.params(), out);
+    out->kernel = ctx->eng.kernel();  // what this context runs (its own kernel flags, read at creation)
     return FHE_HIP_OK;
+}
+
+int fhe_hip_gate_kernel(const fhe_hip_ctx* ctx, size_t count, const char** name) {
+    if (!ctx || !name) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
+    return guarded([&]() -> int {
+        *name = ctx->eng.gate_kernel(count);
+        return FHE_HIP_OK;
+    });
 }
 
 void* fhe_hip_stream(fhe_hip_ctx* ctx) { return ctx ? (void*)ctx->eng.stream() : nullptr; }
@@ -636,15 +645,20 @@ int fhe_hip_switch_to_qn_batch_device(fhe_hip_ctx* ctx, size_t count, const uint
 static bool mixed_args_ok(uint32_t k, size_t count, const uint64_t* const* a_in, const uint64_t* const* b_in,
                           const uint64_t* a_out, const uint64_t* b_out) {
     if (!count) return true;
-    if (!a_in || !b_in || !a_out || !b_out || k < 1 || k > 4) return false;
-    for (uint32_t j = 0; j < k; ++j)
+    if (!a_in || !b_in || !a_out || !b_out) return false;
+    for (uint32_t j = 0; j < k && j < 4; ++j)
         if (!a_in[j] || !b_in[j]) return false;
     return true;
 }
+// the column count of the mixed entry points: 1..4 (Bootstrap 1, 2-input gates 2, AND3 / OR3 / MAJORITY /
+// CMUX 3, AND4 / OR4 4); reported apart from null pointers
+#define FHE_MIXED_K_CHECK(k)                                                                          \
+    if ((k) < 1 || (k) > 4) return fail(FHE_HIP_ERR_INVALID_PARAM, "k: 1 to 4 input columns")
 
 int fhe_hip_eval_mixed_batch(fhe_hip_ctx* ctx, int op, uint32_t k, uint32_t ptmod, size_t count,
                              const uint64_t* const* a_in, const uint64_t* const* b_in, const uint8_t* const* large,
                              uint64_t* a_out, uint64_t* b_out, int extended) {
+    FHE_MIXED_K_CHECK(k);
     if (!ctx || !mixed_args_ok(k, count, a_in, b_in, a_out, b_out)) return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {
         ctx_stream(ctx, nullptr);
@@ -657,6 +671,7 @@ int fhe_hip_eval_mixed_batch_device(fhe_hip_ctx* ctx, int op, uint32_t k, uint32
                                     const uint64_t* const* d_a_in, const uint64_t* const* d_b_in,
                                     const uint8_t* const* d_large, uint64_t* d_a_out, uint64_t* d_b_out, int extended,
                                     void* stream) {
+    FHE_MIXED_K_CHECK(k);
     if (!ctx || !mixed_args_ok(k, count, d_a_in, d_b_in, d_a_out, d_b_out))
         return fail(FHE_HIP_ERR_NULL_PTR, "null argument");
     return guarded([&]() -> int {

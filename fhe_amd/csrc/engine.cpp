@@ -86,6 +86,38 @@ uint32_t Engine::kernel_kind(const Params& p) {
     return 0;
 }
 
+uint32_t Engine::kernel() const {
+    if (!wide_) return 1;
+    if (g3_) return 2;
+    if (n2k_) return 4;
+    if (narrow_) return 3;
+    return 0;
+}
+
+int Engine::ginx_choice(const GateArgs& g) const {
+    const bool two = d_bsk2_ && ginx2_supported(g, tabs_);
+    if (two && ginx_kernel_ == 2) return 2;
+    if (two && (ginx_kernel_ == 3 || (ginx_kernel_ == 0 && g.count <= x_batch_))) return 3;
+    return 1;
+}
+
+const char* Engine::gate_kernel(size_t count) const {
+    const GateArgs g = gate_args(G_AND, count ? count : 1);
+    const int nd = (int)p_.digitsG - 1;
+    const bool lmk = p_.method == M_LMKCDEY;
+    if (wide_) {  // rotate_device's order
+        if (g3_ && lmk) return "k_blind_rotate_lmk3";
+        if (n2k_ && lmk && lmk2k_supported(g, tabs2k_, nd)) return "k_blind_rotate_lmk2k";
+        if (lmk || p_.method == M_AP) return "k_blind_rotate_wide_ops";
+        if (n2k_ && n2k_supported(g, tabs2k_, nd)) return "k_blind_rotate_n2k";
+        if (g3_ && ginx3_supported(g, tabs_)) return "k_blind_rotate_ginx2";
+        return "k_blind_rotate_wide";
+    }
+    if (p_.method != M_GINX) return "k_blind_rotate_lmk";
+    const int k = ginx_choice(g);
+    return k == 2 ? "k_blind_rotate_ginx2" : k == 3 ? "k_blind_rotate_ginx2x" : "k_blind_rotate_ginx";
+}
+
 bool Engine::ks32_set(const Params& p) {
     const bool pow2ks = !(p.qKS & (p.qKS - 1));
     // the tiled shapes (keyswitch.hip launch_keyswitch): baseKS 32 / 64 with digitsKS 3, 16 with 4, and 21 with 4
@@ -326,8 +358,15 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     FHE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     build_tables();
     maxops_ = p_.N + p_.n + 128;
-    // FHE_HIP_GINX_KERNEL = wave | split: pin the GINX blind-rotation kernel (tests, A/B); default by batch size
-    if (const char* k = std::getenv("FHE_HIP_GINX_KERNEL")) ginx_kernel_ = std::string(k) == "split" ? 2 : std::string(k) == "wave" ? 1 : 0;
+    // FHE_HIP_GINX_KERNEL = wave | split | xsplit: pin the GINX blind-rotation kernel (tests, A/B); default by
+    // batch size (K1x below kXBatch gates, K1 above)
+    if (const char* k = std::getenv("FHE_HIP_GINX_KERNEL")) {
+        const std::string v(k);
+        ginx_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : v == "xsplit" ? 3 : 0;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
+        x_batch_ = 2 * (uint32_t)cus;   // K1x: one two-gate workgroup per CU
 }
 
 Engine::~Engine() {
@@ -631,13 +670,14 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
     repack_ginx2();
 }
 
-// the split GINX kernel's key layout (k_blind_rotate_ginx2), repacked on the device from the resident one
+// the two-wave GINX kernels' key layouts, repacked on the device from the resident one: K1s's
+// (k_blind_rotate_ginx2, FHE_HIP_GINX_KERNEL=split) or K1x's (k_blind_rotate_ginx2x, the small-batch default)
 void Engine::repack_ginx2() {
-    // only when the split kernel can run (pinned, or chosen below kSplitBatch gates)
-    if (p_.method != M_GINX || wide_ || !d_bsk_ || (ginx_kernel_ != 2 && kSplitBatch == 0)) return;
+    if (p_.method != M_GINX || wide_ || !d_bsk_ || ginx_kernel_ == 1 || (ginx_kernel_ == 0 && x_batch_ == 0)) return;
     FHE_HIP_CHECK(hipSetDevice(device_));
     if (!d_bsk2_) FHE_HIP_CHECK(hipMalloc(&d_bsk2_, (size_t)p_.n * 16384 * 4));
-    FHE_HIP_CHECK(launch_repack_ginx2(d_bsk_, p_.n, d_bsk2_, stream_));
+    if (ginx_kernel_ == 2) FHE_HIP_CHECK(launch_repack_ginx2(d_bsk_, p_.n, d_bsk2_, stream_));
+    else FHE_HIP_CHECK(launch_repack_ginx2x(d_bsk_, p_.n, d_bsk2_, stream_));
     FHE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
@@ -703,6 +743,15 @@ void Engine::load_ksk(const uint64_t* A, size_t nA, const uint64_t* B, size_t nB
 void Engine::copy_keys_from(const Engine& src) {
     if (src.p_.paramset != p_.paramset || src.p_.method != p_.method)
         throw std::invalid_argument("copy_keys_from: another parameter set");
+    // the packed layouts also follow knobs each context read from the environment at creation (word size of
+    // the wide keys, which layout d_bsk2_ holds, the key switch's row form): a copy between contexts created
+    // under different knobs would hand a kernel buffers of another layout
+    const int two_src = src.ginx_kernel_ == 1 ? 0 : src.ginx_kernel_ == 2 ? 2 : 3;
+    const int two_dst = ginx_kernel_ == 1 ? 0 : ginx_kernel_ == 2 ? 2 : 3;
+    if (src.wide_ != wide_ || src.narrow_ != narrow_ || src.g3_ != g3_ || src.n2k_ != n2k_ || src.ks32_ != ks32_ ||
+        src.ks32w_ != ks32w_ || (!wide_ && p_.method == M_GINX && two_src != two_dst))
+        throw std::invalid_argument("copy_keys_from: the contexts pack their keys in different layouts "
+                                    "(created under different FHE_HIP_* kernel settings)");
     if (!src.ready()) throw std::logic_error("copy_keys_from: the source context has no keys");
     if (src.device_ != device_) {
         int can = 0;
@@ -959,11 +1008,12 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
     if (g.gbits < 2 || h * (1 + (1ull << g.gbits) + (1ull << (2 * g.gbits))) + p_.Q >= (1ull << 32))
         throw std::invalid_argument("device path expects log2(baseG) <= 10");
     if (p_.method == M_GINX) {
-        // two waves per gate below kSplitBatch gates (fills the chip at small batches), else one
-        const bool split = d_bsk2_ && ginx2_supported(g, tabs_) &&
-                           (ginx_kernel_ == 2 || (ginx_kernel_ == 0 && g.count < kSplitBatch));
-        if (split)
+        // two waves per gate up to x_batch_ gates (K1x: small batches would leave SIMDs idle), else one
+        const int k = ginx_choice(g);
+        if (k == 2)
             FHE_HIP_CHECK(launch_blind_rotate_ginx2(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+        else if (k == 3)
+            FHE_HIP_CHECK(launch_blind_rotate_ginx2x(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
         else
             FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
     } else {

@@ -67,6 +67,10 @@ public:
     // the accumulator kernels a context of this set runs on (fhe_hip_params::kernel), with the A/B
     // environment knobs a context reads at creation (FHE_HIP_GINX3, FHE_HIP_N2K, FHE_HIP_NARROW)
     static uint32_t kernel_kind(const Params& p);
+    // the same for this context: its own kernel flags, read from the environment when it was created
+    uint32_t kernel() const;
+    // the blind-rotation kernel a 2-input gate batch of `count` ciphertexts runs on in this context
+    const char* gate_kernel(size_t count) const;
 
     // raw reference layouts (see include/fhe_hip.h)
     void load_bsk(const uint64_t* bsk, size_t words);
@@ -241,14 +245,19 @@ private:
     uint32_t* d_kspart_ = nullptr;   // row-split key-switch partials (ks_part)
     static constexpr size_t kKsPartWords = (size_t)1 << 25;  // 2^16 rows x 512 u32
     uint32_t* ks_part(size_t count);
-    // GINX kernel choice: 0 by batch size, 1 one wave per gate, 2 two waves per gate.  Measured
-    // (tools/gate_time.py, STD128 AND): the split kernel is slower at every batch size -- 1024 gates
-    // 5.55 vs 5.17 ms, 65,536 gates 260 vs 211 ms (twice the LDS traffic: two transposes per
-    // 16-coefficient transform plus the digit exchange, two workgroup barriers per index) -- so the
-    // default never selects it (kSplitBatch = 0); FHE_HIP_GINX_KERNEL=split pins it.
+    // GINX kernel choice: 0 by batch size, 1 one wave per gate (K1), 2 two waves per gate with the digit
+    // exchange (K1s), 3 two waves per gate with K1w's one-word exchange (K1x).  K1s is slower than K1 at
+    // every batch size (1024 gates 4.87 vs 4.37 ms: two barriers per index, the partner's digits read in
+    // the MAC) and only FHE_HIP_GINX_KERNEL=split pins it; K1x runs batches of up to kXBatch gates.
     int ginx_kernel_ = 0;
-    static constexpr uint32_t kSplitBatch = 0;
-    void* d_bsk2_ = nullptr;   // k_blind_rotate_ginx2 key layout (g3_: its nd = 3 layout)
+    // GINX kernel of a gate launch (ginx_kernel_ pins, else by batch size): 1 K1, 2 K1s, 3 K1x
+    int ginx_choice(const GateArgs& g) const;
+    // K1x runs batches of up to x_batch_ gates: one two-gate workgroup per CU (2 x the CU count, 512 on
+    // MI355X).  Measured (tools/gate_time.py, STD128 AND, profiles/r06_k1x_ab2.txt): 512 gates 2.69 vs 4.16 ms
+    // (K1), 768 gates 4.28 vs 4.18, 1024 gates 4.56 vs 4.24: once two of its waves share a SIMD they overlap
+    // poorly, and the one-wave kernel wins
+    uint32_t x_batch_ = 512;
+    void* d_bsk2_ = nullptr;   // K1s / K1x key layout (g3_: K1s's nd = 3 layout; n2k_: K1w's)
     void repack_ginx2();
     // digitsG = 4 GINX sets at N = 1024, Q < 2^27 (STD128_3, STD128Q, STD128_4, LPF_STD128, LPF_STD128Q):
     // gates on the split kernel with three digits per component (launch_blind_rotate_ginx3) over the

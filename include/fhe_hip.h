@@ -113,7 +113,12 @@ typedef struct {
 int fhe_hip_params_get(int paramset, int method, fhe_hip_params* out);
 int fhe_hip_create(int paramset, int method, int device, fhe_hip_ctx** out);
 void fhe_hip_destroy(fhe_hip_ctx* ctx);
+/* the context's parameters; its kernel field reports the kernels THIS context runs (the FHE_HIP_* kernel
+ * settings it was created under), fhe_hip_params_get's the default for the set */
 int fhe_hip_get_params(const fhe_hip_ctx* ctx, fhe_hip_params* out);
+/* the blind-rotation kernel a 2-input gate batch of `count` ciphertexts runs on in this context (a static
+ * string, e.g. "k_blind_rotate_ginx" / "k_blind_rotate_ginx2x": the rocprof kernel name) */
+int fhe_hip_gate_kernel(const fhe_hip_ctx* ctx, size_t count, const char** name);
 /* the context's stream (hipStream_t) */
 void* fhe_hip_stream(fhe_hip_ctx* ctx);
 /* upload keys (BTKeyLoad, binfhecontext.h:273-275; Backend::PackBootstrappingKey) */
@@ -240,7 +245,9 @@ int fhe_hip_switch_to_qn_batch_device(fhe_hip_ctx* ctx, size_t count, const uint
  * otherwise rows of N words, large[j][g] = 1 marking a ciphertext mod Q (dimension N), 0 one mod q (its first
  * n words used).  Outputs [count][n] mod q, or ctExt [count][N] mod Q when extended.
  * Bootstrap of an input mod Q keeps the reference's constant ct->GetModulus() >> 2 (:201), added at q by
- * ModAddFast, so its test vector is the window's constant uv. */
+ * ModAddFast, so its test vector is the window's constant uv.  That shortcut needs
+ * Q / 4 >= 2.5 q, true for every parameter row (the smallest ratio is far above it); a set below it is refused
+ * with FHE_HIP_ERR_INVALID_PARAM rather than computed differently from the reference. */
 #define FHE_HIP_OP_BOOTSTRAP (-1)
 int fhe_hip_eval_mixed_batch(fhe_hip_ctx* ctx, int op, uint32_t k, uint32_t ptmod, size_t count,
                              const uint64_t* const* a_in, const uint64_t* const* b_in, const uint8_t* const* large,

@@ -149,3 +149,57 @@ def test_gpu_copy_keys_fan_out_matches_host_load(ps, m):
     assert L.fhe_hip_copy_keys(other._h, src._h) == -2   # another parameter set
     for e in (src, dst, other):
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ps,m,knob,val", [(3, 2, "FHE_HIP_GINX_KERNEL", "wave"), (0, 2, "FHE_HIP_NARROW", "0")])
+def test_gpu_copy_keys_refuses_contexts_of_other_kernel_layouts(ps, m, knob, val, monkeypatch):
+    """contexts created under different FHE_HIP_* kernel settings pack their keys in different layouts (STD128:
+    the two-wave kernels' repacked BSK or none; TOY: u32 or u64 words of the 64-bit-path BSK): fhe_hip_copy_keys
+    refuses the pair with FHE_HIP_ERR_INVALID_PARAM instead of handing a kernel a buffer of another layout; the
+    contexts' own kernel fields differ accordingly where the knob changes the accumulator (TOY)"""
+    from fhe_amd import binfhe as bf
+    from fhe_amd._lib import check
+    L = bf.L()
+    keys = bf.keygen(ps, m, 0xB0070000 + ps)
+    src = bf.GateEngine(ps, m, 0)
+    src.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    monkeypatch.setenv(knob, val)
+    dst = bf.GateEngine(ps, m, 0)
+    monkeypatch.delenv(knob)
+    assert L.fhe_hip_copy_keys(dst._h, src._h) == -2
+    assert "different layouts" in L.fhe_hip_last_error().decode()
+    same = bf.GateEngine(ps, m, 0)
+    check(L.fhe_hip_copy_keys(same._h, src._h))
+    if knob == "FHE_HIP_NARROW":
+        assert (src.kernel(), dst.kernel()) == (3, 0)
+    for e in (src, dst, same):
+        e.close()
+
+
+@pytest.mark.gpu
+def test_gpu_gate_kernel_reports_the_launched_kernel(monkeypatch):
+    """fhe_hip_gate_kernel: the STD128 GINX context runs K1x (k_blind_rotate_ginx2x) up to two gates per CU and
+    K1 above; FHE_HIP_GINX_KERNEL pins it; LMKCDEY runs its op-list kernel"""
+    from fhe_amd import binfhe as bf
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    keys = bf.keygen(bf.STD128, bf.GINX, 5)
+    e = bf.GateEngine(bf.STD128, bf.GINX, 0)
+    e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+    assert [e.gate_kernel(c) for c in (1, 2 * cus, 2 * cus + 1, 65536)] == \
+        ["k_blind_rotate_ginx2x"] * 2 + ["k_blind_rotate_ginx"] * 2
+    assert e.kernel() == 1
+    for val, name in (("wave", "k_blind_rotate_ginx"), ("split", "k_blind_rotate_ginx2"), ("xsplit", "k_blind_rotate_ginx2x")):
+        monkeypatch.setenv("FHE_HIP_GINX_KERNEL", val)
+        p = bf.GateEngine(bf.STD128, bf.GINX, 0)
+        p.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        assert p.gate_kernel(4096) == name, val
+        p.close()
+    monkeypatch.delenv("FHE_HIP_GINX_KERNEL")
+    lk = bf.keygen(bf.STD128_LMKCDEY, bf.LMKCDEY, 5)
+    l = bf.GateEngine(bf.STD128_LMKCDEY, bf.LMKCDEY, 0)
+    l.load_keys(lk.bsk, lk.kskA, lk.kskB)
+    assert l.gate_kernel(1024) == "k_blind_rotate_lmk"
+    for x in (e, l):
+        x.close()

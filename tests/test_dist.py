@@ -158,3 +158,41 @@ def test_bench_reads_the_newest_pmc_summary_in_either_shape(tmp_path, monkeypatc
     json.dump(bare, open(tmp_path / "profiles" / "r99_pmc_traffic.json", "w"))
     assert bench.pmc_summary("kx", "hbm_bytes_per_launch") == (400, 20)
     assert bench.pmc_traffic("kx", 40) == 800
+
+
+def _topology_worker(rank, world, port, outdir):
+    """one gloo rank: a device identity (stand-in values: no GPU here) gathered to every rank"""
+    import json
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fhe_amd.dist import gather_identities, topology_record
+    out = {}
+    for case, dev in (("distinct", rank), ("shared", 0)):
+        ident = {"rank": rank, "local_rank": rank, "device": dev, "pci": f"0000:{0x10 + dev:02x}:00",
+                 "uuid": f"GPU-{dev}", "name": "stand-in", "host": "h0", "peer_access": [True, True]}
+        out[case] = topology_record(gather_identities(ident), "gloo", rehearsal=False)
+    json.dump(out, open(os.path.join(outdir, f"t{rank}.json"), "w"))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_topology_record(tmp_path):
+    """bench.py's "distributed" object: world size and backend of the process group, every rank's device
+    gathered in rank order, distinct-device check; two ranks on one device are a rehearsal, and refused
+    under nccl (check_topology)"""
+    import json
+    from fhe_amd.dist import check_topology
+    world = 2
+    mp.spawn(_topology_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    recs = [json.load(open(tmp_path / f"t{r}.json")) for r in range(world)]
+    assert recs[0] == recs[1]                       # every rank sees the same gathered record
+    d, s = recs[0]["distinct"], recs[0]["shared"]
+    assert d["world_size"] == 2 and d["backend"] == "gloo" and [i["rank"] for i in d["ranks"]] == [0, 1]
+    assert d["distinct_devices"] and d["devices"] == 2 and not d["rehearsal"]
+    assert [i["pci"] for i in d["ranks"]] == ["0000:10:00", "0000:11:00"]
+    assert not s["distinct_devices"] and s["devices"] == 1 and s["rehearsal"]
+    check_topology(d)
+    check_topology(s)                                # gloo: a rehearsal is allowed
+    with pytest.raises(RuntimeError, match="share a device"):
+        check_topology(dict(s, backend="nccl"))
+    check_topology(dict(d, backend="nccl"))

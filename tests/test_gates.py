@@ -315,14 +315,16 @@ def test_gpu_multi_engine_shards_match_single():
 
 
 @pytest.mark.gpu
-def test_gpu_split_ginx_kernel_bit_exact():
-    """k_blind_rotate_ginx2 (two waves per gate, FHE_HIP_GINX_KERNEL=split) == the reference goldens and
-    == the one-wave kernel on ragged batches"""
+@pytest.mark.parametrize("kind", ["split", "xsplit"])
+def test_gpu_split_ginx_kernel_bit_exact(kind):
+    """the two-wave GINX kernels pinned by FHE_HIP_GINX_KERNEL -- split: k_blind_rotate_ginx2 (digit exchange),
+    xsplit: k_blind_rotate_ginx2x (K1x, one reduced word per slot exchanged) -- == the reference goldens and
+    == the one-wave kernel on ragged batches (1027 gates: K1x's last workgroup holds one live gate)"""
     import os
     from fhe_amd import binfhe as bf
     g, keys, (a1, b1, a2, b2) = fixture("std128")
     engines = {}
-    for kind in ("split", "wave"):
+    for kind in (kind, "wave"):
         os.environ["FHE_HIP_GINX_KERNEL"] = kind
         try:
             e = bf.GateEngine(bf.STD128, bf.GINX, device=0)
@@ -330,15 +332,16 @@ def test_gpu_split_ginx_kernel_bit_exact():
             del os.environ["FHE_HIP_GINX_KERNEL"]
         e.load_keys(keys.bsk, keys.kskA, keys.kskB)
         engines[kind] = e
+    two = engines[next(k for k in engines if k != "wave")]
     for i, gate, sl in per_gate(g):
-        ao, bo = engines["split"].eval_gate(gate, a1[sl], b1[sl], a2[sl], b2[sl])
+        ao, bo = two.eval_gate(gate, a1[sl], b1[sl], a2[sl], b2[sl])
         assert np.array_equal(ao, g["out_a"][sl].astype(np.uint64)) and np.array_equal(bo, g["out_b"][sl].astype(np.uint64))
     rng = np.random.default_rng(77)
     for count in (1, 5, 1027):
         x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
         c1, d1 = bf.encrypt(bf.STD128, bf.GINX, keys.sk, x1, 90 + count)
         c2, d2 = bf.encrypt(bf.STD128, bf.GINX, keys.sk, x2, 91 + count)
-        s = engines["split"].eval_gate(bf.XOR, c1, d1, c2, d2)
+        s = two.eval_gate(bf.XOR, c1, d1, c2, d2)
         w = engines["wave"].eval_gate(bf.XOR, c1, d1, c2, d2)
         assert np.array_equal(s[0], w[0]) and np.array_equal(s[1], w[1]), count
     for e in engines.values():
