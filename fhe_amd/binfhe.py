@@ -23,6 +23,21 @@ from ._lib import FheHipError, check, lib, ptr, sz, u64, vp
 
 # reference enum values (src/binfhe/include/binfhe-constants.h:49-126)
 TOY, STD128_AP, STD128, STD128_LMKCDEY = 0, 2, 3, 21
+# every BINFHE_PARAMSET name in enum order (binfhe-constants.h:49-95)
+PARAMSETS = ("TOY MEDIUM STD128_AP STD128 STD128_3 STD128_4 STD128Q STD128Q_3 STD128Q_4 STD192 STD192_3 STD192_4 "
+             "STD192Q STD192Q_3 STD192Q_4 STD256 STD256_3 STD256_4 STD256Q STD256Q_3 STD256Q_4 STD128_LMKCDEY "
+             "STD128_3_LMKCDEY STD128_4_LMKCDEY STD128Q_LMKCDEY STD128Q_3_LMKCDEY STD128Q_4_LMKCDEY STD192_LMKCDEY "
+             "STD192_3_LMKCDEY STD192_4_LMKCDEY STD192Q_LMKCDEY STD192Q_3_LMKCDEY STD192Q_4_LMKCDEY STD256_LMKCDEY "
+             "STD256_3_LMKCDEY STD256_4_LMKCDEY STD256Q_LMKCDEY STD256Q_3_LMKCDEY STD256Q_4_LMKCDEY LPF_STD128 "
+             "LPF_STD128Q LPF_STD128_LMKCDEY LPF_STD128Q_LMKCDEY SIGNED_MOD_TEST").split()
+
+
+def method_compatible(paramset, method):
+    """GenerateBinFHEContext(set, method) accepts the pair (binfhecontext.cpp:113-159: the *_LMKCDEY rows, TOY
+    and MEDIUM take LMKCDEY; the CGGI rows, TOY .. STD256Q_4, LPF_STD128/Q and SIGNED_MOD_TEST take GINX and AP)"""
+    lmk = paramset in (0, 1, 41, 42) or 21 <= paramset <= 38
+    cggi = paramset <= 20 or paramset in (39, 40, 43)
+    return lmk if method == 3 else cggi if method in (1, 2) else False
 LARGE = 1 << 30
 TIMEOPT = 1 << 14
 

@@ -114,6 +114,12 @@ FHE_DEV void ct_bf(uint32_t& x, uint32_t& y, uint32_t wR, const Mod& m) {
 #ifndef FHE_LMK_SWAP
 #define FHE_LMK_SWAP 1   // LMKCDEY automorphism: the digits into the half-wave layout by v_permlane32_swap
 #endif
+#ifndef FHE_LMK_ABL
+#define FHE_LMK_ABL 0    // timing-only ablations of the LMKCDEY op-list kernel (wrong results), bits: 1 every EXT op
+                         // reads the keys of index 0, 2 every AUTO op those of key 0 (cache-resident: the data-
+                         // dependent key traffic removed), 4 the automorphism gathers at linear positions, 8 no digit
+                         // exchange between the half-waves in EXT
+#endif
 #ifndef FHE_LMK_KPF
 #define FHE_LMK_KPF 1    // op-list kernel: key chunks (4 slots x 4 rows) requested ahead of their MAC
 #endif
@@ -1017,14 +1023,15 @@ FHE_DEV void automorphism_wide(uint32_t (&v)[32], uint32_t (&a0)[16], uint32_t* 
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
         const uint32_t sr = ((__builtin_bitreverse32((uint32_t)r) >> 27) << 6) * k;  // uniform
-        v[r]              = region[(((cl + sr) >> 1) & 1023)];
+        // FHE_LMK_ABL bit 2 (timing only): every gather at a conflict-free linear position instead
+        v[r]              = region[(FHE_LMK_ABL & 4) ? ((((cl + sr) >> 1) & 992) | (uint32_t)l) : (((cl + sr) >> 1) & 1023)];
     }
     const uint32_t cL = (((__builtin_bitreverse32((uint32_t)L) >> 26) << 3) + 1) * k;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t H = (uint32_t)r >> 2, j = (uint32_t)r & 3;
         const uint32_t su = ((((j & 1) << 1 | j >> 1) << 9) + (((H & 1) << 1 | H >> 1) << 1)) * k;  // uniform
-        a0[r]             = region0[(((cL + su) >> 1) & 1023)];
+        a0[r]             = region0[(FHE_LMK_ABL & 4) ? ((((cL + su) >> 1) & 960) | (uint32_t)L) : (((cL + su) >> 1) & 1023)];
     }
     wave_lds_sync();
 }
@@ -1121,7 +1128,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
         uint32_t dA[32], dB[32];
         if (DM || !(op & 0x8000u)) {
             // ---- AddToAccLMKCDEY / AddToAccDM: acc <- sum_d D_d * ek[op][d]   (acc replaced)
-            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)op * (4 * 8 * 64);
+            const uint4* kb4 = reinterpret_cast<const uint4*>(bsk) + (size_t)((FHE_LMK_ABL & 1) ? 0u : op) * (4 * 8 * 64);
             constexpr int KPF = FHE_LMK_KPF;
             uint4 kq[KPF + 1][4];
 #pragma unroll
@@ -1160,8 +1167,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
                     const int r = 4 * kk + e;
 #define KC(d) (e == 0 ? kq[kk % (KPF + 1)][d].x : e == 1 ? kq[kk % (KPF + 1)][d].y : e == 2 ? kq[kk % (KPF + 1)][d].z : kq[kk % (KPF + 1)][d].w)
                     const uint32_t D0 = dA[r], D2 = dB[r];
-                    const uint32_t D1 = PIPE ? xq[kk & 1][2 * e] : other_half(dA[r], xaddr);
-                    const uint32_t D3 = PIPE ? xq[kk & 1][2 * e + 1] : other_half(dB[r], xaddr);
+                    const uint32_t D1 = (FHE_LMK_ABL & 8) ? dA[r] ^ 1u : PIPE ? xq[kk & 1][2 * e] : other_half(dA[r], xaddr);
+                    const uint32_t D3 = (FHE_LMK_ABL & 8) ? dB[r] ^ 1u : PIPE ? xq[kk & 1][2 * e + 1] : other_half(dB[r], xaddr);
                     // |D| < 10Q + 2^8 (Q < 2^27) or 6Q (Q < 2^28; 6.67Q with FHE_FWD_TIGHT): |S| < 40 Q^2
                     // or 24 Q^2 (26.7 Q^2), so |S| 2^-32 + Q/2 < 2Q (2.2Q: kLmkAcc)
                     const int64_t S = (int64_t)mac4<true>(D0, D1, D2, D3, KC(0), KC(1), KC(2), KC(3), 0);
@@ -1212,7 +1219,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM ? F
 #endif
             }
             fwd_pass_s<FM>(dA, tile, l, twAf, s_twBf, m);  // half 0: EVAL digit A, half 1: EVAL digit B
-            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)t * (2 * 8 * 64);
+            const uint4* kb4 = reinterpret_cast<const uint4*>(autok) + (size_t)((FHE_LMK_ABL & 2) ? 0u : t) * (2 * 8 * 64);
             constexpr int AKPF = FHE_LMK_AKPF;
             uint4 ka[AKPF + 1][2];
 #pragma unroll
@@ -1968,6 +1975,10 @@ namespace {
 #else
 #define XKEY(p, o) (p)[o]
 #endif
+#ifndef FHE_X_MPF
+#define FHE_X_MPF 0     // 1: the MAC's monomial pairs requested one slot pair ahead (measured slower,
+                        // profiles/r06_lmk_attr.txt: 2.84 / 2.83 vs 2.74 / 2.71 ms at 512 gates)
+#endif
 #ifndef FHE_X_PRIO
 #define FHE_X_PRIO 0    // A/B: waves of odd workgroup slots on a CU at priority 1
 #endif
@@ -2077,20 +2088,37 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
         if (kXTiles == 2) wave_lds_sync();  // its last reads done before the partner words overwrite it
         const uint32_t fl = (as * lmul) & 1023u;
         uint32_t* xo = xb + L;
-#pragma unroll
-        for (int k2 = 0; k2 < 8; ++k2) {
-            if (k2 + 1 < 8) {
-#pragma unroll
-                for (int q = 0; q < kQ; ++q) kq[(k2 + 1) & 1][q] = XKEY(kb, (q * 8 + k2 + 1) * 64);
-            }
-            asm volatile("" ::: "memory");
+        // the monomial pair of slot pair k2: psi^(2f) - 1 and psi^(-2f) - 1, requested one slot pair ahead
+        // of its use (LDS latency off the MAC's critical path, as K1's issue())
+        auto mono = [&](int k2, uint2& mp, uint2& mn) {
             const int r0 = 2 * k2;
             const uint32_t ur = __builtin_amdgcn_readfirstlane(
                 (as * (512u * (__builtin_bitreverse32((uint32_t)(r0 & 3)) >> 30) +
                        2u * (__builtin_bitreverse32((uint32_t)(r0 >> 2)) >> 30))) & 1023u);
             const uint32_t f  = fl + ur;    // < 2N
             const uint32_t fn = 2048u - f;  // -a: 2N - f
-            const uint2 mp = s_mono2[f + (f >> 5)], mn = s_mono2[fn + (fn >> 5)];
+            mp = s_mono2[f + (f >> 5)];
+            mn = s_mono2[fn + (fn >> 5)];
+        };
+        uint2 mq[2][2];
+#if FHE_X_MPF
+        mono(0, mq[0][0], mq[0][1]);
+#endif
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) {
+            if (k2 + 1 < 8) {
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) kq[(k2 + 1) & 1][q] = XKEY(kb, (q * 8 + k2 + 1) * 64);
+#if FHE_X_MPF
+                mono(k2 + 1, mq[(k2 + 1) & 1][0], mq[(k2 + 1) & 1][1]);
+#endif
+            }
+            asm volatile("" ::: "memory");
+            const int r0 = 2 * k2;
+#if !FHE_X_MPF
+            mono(k2, mq[k2 & 1][0], mq[k2 & 1][1]);
+#endif
+            const uint2 mp = mq[k2 & 1][0], mn = mq[k2 & 1][1];
             const uint4* q4 = kq[k2 & 1];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {

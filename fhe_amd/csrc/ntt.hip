@@ -569,6 +569,9 @@ FHE_DEV void wave_sync() {
 FHE_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
 FHE_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
 
+#ifndef FHE_NTT64_PHASE
+#define FHE_NTT64_PHASE 0  // A/B: load phasing of k_ntt1024w64's co-resident waves (units of 1024 cycles)
+#endif
 #ifndef FHE_NTT64_WPS
 #define FHE_NTT64_WPS 4  // k_ntt1024w64: waves per SIMD (register budget and grid size)
 #endif
@@ -788,6 +791,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FHE_NT
     // the first polynomial's rows, then the twiddle table; the forward transform runs its layout-A
     // stages (uniform twiddles, no LDS) on the rows as they land, before the table's barrier
     Raw bufA;
+#if FHE_NTT64_PHASE
+    {  // A/B: the four waves of a SIMD request their rows one after the other, FHE_NTT64_PHASE x 1024 cycles apart
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        const uint32_t slot = ((hw >> 16) & 1) * 2 + (uint32_t)__builtin_amdgcn_readfirstlane(wv >> 2);
+        for (uint32_t z = 0; z < slot * FHE_NTT64_PHASE; ++z) __builtin_amdgcn_s_sleep(16);
+    }
+#endif
     if (poly < count) load(bufA, poly);
     ntt_stagger(wv);
     const ulonglong2 tw0 = tab[threadIdx.x], tw1 = tab[threadIdx.x + 512];  // 512 threads (launch_wave64)

@@ -220,3 +220,32 @@ def test_gpu_n2k_kernel_matches_64bit_accumulator(monkeypatch, name):
         assert np.array_equal(dec, TRUTH[gate](x1, x2)), gname
     for u, v in zip(res["1"][len(GATES):], res["0"][len(GATES):]):
         assert np.array_equal(u[0][0], v[0][0])
+
+
+def test_integration_kernel_table_matches_params():
+    """INTEGRATION.md's "Which kernel serves a parameter set" table lists every compatible (set, method) pair of
+    binfhecontext.cpp:113-159 exactly once, with the `kernel` fhe_hip_params_get reports for it (default kernel
+    settings: the FHE_HIP_* knobs unset)"""
+    import re
+    from fhe_amd import binfhe as bf
+    for k in ("FHE_HIP_GINX3", "FHE_HIP_N2K", "FHE_HIP_NARROW"):
+        assert k not in os.environ, k
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(root, "INTEGRATION.md")).read()
+    sec = text[text.index("## Which kernel serves a parameter set"):text.index("## Raw key layout")]
+    methods = {"AP": bf.AP, "GINX": bf.GINX, "LMKCDEY": bf.LMKCDEY}
+    seen = {}
+    for line in sec.splitlines():
+        cells = [c.strip() for c in line.strip().strip("|").split("|")]
+        if len(cells) < 3 or cells[1] not in methods:
+            continue
+        kernel = int(cells[2])
+        for name in (n.strip() for n in cells[0].split(",")):
+            ps, m = bf.PARAMSETS.index(name), methods[cells[1]]
+            assert (ps, m) not in seen, (name, cells[1])
+            assert bf.method_compatible(ps, m), (name, cells[1])
+            seen[(ps, m)] = kernel
+            assert bf.params(ps, m).kernel == kernel, (name, cells[1], bf.params(ps, m).kernel, kernel)
+    want = {(ps, m) for ps in range(len(bf.PARAMSETS)) for m in methods.values() if bf.method_compatible(ps, m)}
+    assert set(seen) == want, sorted(want - set(seen))
+    assert re.search(r"1 = K1, 2 = K1s / K1m, 3 = K5 A32, 4 = K1w, 0 = K5 A64", sec)
