@@ -266,6 +266,7 @@ def main():
     # rehearsal knobs (not used by the driver): FHE_BENCH_DEVICE_MAP="0,0" puts ranks on
     # chosen devices, FHE_BENCH_BACKEND=gloo for a one-GPU box
     dmap = os.environ.get("FHE_BENCH_DEVICE_MAP")
+    env_local = local
     if dmap:
         local = int(dmap.split(",")[local])
     backend = os.environ.get("FHE_BENCH_BACKEND", "nccl")
@@ -280,7 +281,7 @@ def main():
     # which devices the ranks ran on, as the process group saw them (the driver's N-GPU line must show N
     # distinct GPUs under RCCL; a rank sharing a device with another is refused there, marked a rehearsal here)
     from fhe_amd.dist import check_topology, device_identity, gather_identities, topology_record
-    topo = topology_record(gather_identities(device_identity(torch, dev, rank, local)),
+    topo = topology_record(gather_identities(device_identity(torch, dev, rank, env_local)),
                            backend if world > 1 else None, rehearsal=bool(dmap))
     try:
         check_topology(topo)
