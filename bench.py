@@ -168,10 +168,11 @@ def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None):
     dec = bf.decrypt(ps, method, keys.sk, ao, bo)
     verified = bool(np.array_equal(dec, (x1[lo:hi] & x2[lo:hi]).astype(np.int64)))
     exact = golden_check(golden or ("std128" if method_name == "ginx" else "lmkcdey"), lo, hi, total, ao, bo)
+    kernel = eng.gate_kernel(B)   # the blind-rotation kernel this batch launched (fhe_hip_gate_kernel)
     eng.close()
     return {"elapsed": elapsed, "br_ms": br_ms, "ks_ms": ks_ms, "verified": verified, "exact": exact, "B": B,
             "keys": keys, "inputs": (a1[lo:hi], b1[lo:hi], a2[lo:hi], b2[lo:hi]), "out": (ao, bo), "ps": ps,
-            "method": method}
+            "method": method, "kernel": kernel}
 
 
 def per_gpu_hbm(method_name, B, step_s):
@@ -185,12 +186,13 @@ def per_gpu_hbm(method_name, B, step_s):
                      "time (slowest rank); low by construction, the keys are reused by every gate"}
 
 
-def rooflines(method_name, B, br_ms, ks_ms):
-    """roofline (HBM) and valu_roofline of the blind-rotation kernel at B gates per launch."""
+def rooflines(method_name, B, br_ms, ks_ms, kernel=None):
+    """roofline (HBM) and valu_roofline of the blind-rotation kernel at B gates per launch (kernel: the name
+    the context reports for the launch, default K1's)."""
     alg_bytes = BSK_BYTES[method_name] + B * (IN_BYTES_PER_GATE[method_name] + EXT_BYTES_PER_GATE)
     achieved = alg_bytes / (br_ms * 1e-3) / 1e9
     mm_rate = MODMUL_PER_GATE[method_name] * B / (br_ms * 1e-3) / 1e12
-    k1 = K1_NAME[method_name]
+    k1 = kernel or K1_NAME[method_name]
     roofline = {
         "kernel": k1, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(k1, B),
@@ -317,7 +319,7 @@ def main():
 
     result = None
     if rank == 0:
-        roofline, valu = rooflines(args.method, main_r["B"], main_r["br_ms"], main_r["ks_ms"])
+        roofline, valu = rooflines(args.method, main_r["B"], main_r["br_ms"], main_r["ks_ms"], main_r["kernel"])
         value = total * args.steps / main_r["elapsed"]
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "bootstraps/s", "n_gpus": world,
@@ -339,7 +341,7 @@ def main():
             "distributed": topo,
         }
         if lmk_r is not None:
-            lr, lv = rooflines("lmkcdey", lmk_r["B"], lmk_r["br_ms"], lmk_r["ks_ms"])
+            lr, lv = rooflines("lmkcdey", lmk_r["B"], lmk_r["br_ms"], lmk_r["ks_ms"], lmk_r["kernel"])
             result["lmkcdey"] = {
                 "config": f"BASELINE config 5: STD128_LMKCDEY EvalBinGate(AND), {total} gates per step over "
                           f"{world} GPU(s) ({hi - lo} per GPU)",
@@ -351,7 +353,7 @@ def main():
             }
     if world == 1 and not args.no_config3 and args.method == "ginx":
         c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden="std128_b1024")
-        r3, v3 = rooflines("ginx", 1024, c3["br_ms"], c3["ks_ms"])
+        r3, v3 = rooflines("ginx", 1024, c3["br_ms"], c3["ks_ms"], c3["kernel"])
         alg3 = BSK_BYTES["ginx"] + KSK_BYTES["ginx"] + 1024 * (IN_BYTES_PER_GATE["ginx"] + OUT_BYTES_PER_GATE["ginx"])
         step_s = c3["elapsed"] / args.steps
         result["config3"] = {
