@@ -216,7 +216,7 @@ def rooflines(method_name, B, br_ms, ks_ms, kernel=None):
                            "is near 1",
         "basis": "SURVEY 8(a) modular multiplies per gate x gates / launch time; peak = 256 CUs x 4 SIMDs x "
                  "16 lanes/clk (half-rate 32-bit multiplies) x 2.4 GHz / 3 multiplies per modmul; the measured "
-                 "multiply issue rate (profiles/r01_ubench_valu_rates.txt, 35.1 T lane-op/s) is 11.7 T modmul/s",
+                 "multiply issue rate (profiles/archive/r01_ubench_valu_rates.txt, 35.1 T lane-op/s) is 11.7 T modmul/s",
     }
     return roofline, valu
 

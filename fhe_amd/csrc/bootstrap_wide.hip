@@ -28,7 +28,7 @@
 #endif
 // the A32 instantiations: the gate kernel at 4 (113 VGPRs, 64 KB of LDS with its tables; with the
 // monomial table through the caches and 6 waves it spills 14 VGPRs and runs 21-29% slower), the
-// op-list kernel at 6 (80 VGPRs: +8% on STD256_LMKCDEY / STD256Q_3_LMKCDEY, profiles/r03_bench_sets_narrow.txt)
+// op-list kernel at 6 (80 VGPRs: +8% on STD256_LMKCDEY / STD256Q_3_LMKCDEY, profiles/archive/r03_bench_sets_narrow.txt)
 #ifndef FHE_WIDE32_WAVES
 #define FHE_WIDE32_WAVES 4
 #endif
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 4, A::kWaves)
         for (uint32_t L = 0; 2 * L < dG2; ++L) {
             // A32: this level's 32 key words per thread requested before its digit transform, so they
             // land during it (wg_sync's LDS-only barriers do not drain them): +1.2% on the N = 2048
-            // GINX rows, 121 VGPRs (profiles/r03_ab_wide.txt; the op-list kernel's EXT keys the same
+            // GINX rows, 121 VGPRs (profiles/archive/r03_ab_wide.txt; the op-list kernel's EXT keys the same
             // way lose 1% at 6 waves per SIMD with spills, 7% at 5)
             constexpr bool kpf = sizeof(T) == 4;
             T kr[kpf ? 2 : 1][2][2][kpf ? S : 1];

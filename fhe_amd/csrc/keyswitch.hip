@@ -103,7 +103,7 @@ constexpr int kKsCols  = FHE_KS_COLS;           // columns per workgroup (packed
 // 8-byte bank slot (17 d + k) mod 32, distinct for all 32 slices, so the random per-gate slice
 // choices never conflict (16-byte reads with a 144-B stride collide for slices d, d + 16).
 // Tile shapes (G gates per workgroup, IPR values of i per round at baseKS = 32), by batch size
-// (round 3, profiles/r03_ab_keyswitch.txt, per launch at 65,536 / 8192 / 1024 gates):
+// (round 3, profiles/archive/r03_ab_keyswitch.txt, per launch at 65,536 / 8192 / 1024 gates):
 //   G 256, IPR 4 (104 KB of LDS, one workgroup per CU):       6.64 ms / 0.82 ms / 125 + 11 us
 //   G 512, IPR 4:                                              4.58 ms / 0.95 ms /  79 + 11 us
 //   G 512, IPR 2 (52 KB: several workgroups per CU):           3.27 ms / 1.12 ms /  73 + 20 us

@@ -70,7 +70,7 @@ FHE_DEV int wt(int x) { return x + ((x >> 6) << 2); }
 // k_ntt1024w64: staggered wave priorities.  With equal priority the waves sharing a SIMD interleave,
 // finish together and leave all their stores for the end of the pass; ranked (waves 4..7 of a
 // workgroup above 0..3, two per SIMD each), the high pair finishes first and its stores overlap the
-// low pair's arithmetic.  Round 3, interleaved A/B (profiles/r03_ab_ntt_prio.txt): 20.8 / 20.6 ->
+// low pair's arithmetic.  Round 3, interleaved A/B (profiles/archive/r03_ab_ntt_prio.txt): 20.8 / 20.6 ->
 // 20.0 / 20.2 us per 60-bit forward / inverse pass; four levels (by grid half too) and the 32-bit
 // kernel gain nothing.
 FHE_DEV void ntt_stagger(int wv) {
