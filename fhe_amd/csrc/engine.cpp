@@ -129,8 +129,10 @@ bool Engine::ks32_set(const Params& p) {
 
 bool Engine::ks32w_set(const Params& p) {
     const bool pow2ks = p.qKS && !(p.qKS & (p.qKS - 1));
-    // qKS < 2^32: GateArgs::qKS is a u32 word (launch_keyswitch_w32 reads it from there)
-    return !is_large(p.paramset) && !p.timeopt && pow2ks && p.qKS > 65536 && p.qKS < (1ull << 32) &&
+    // qKS < 2^32: GateArgs::qKS is a u32 word (launch_keyswitch_w32 reads it from there).  Round 6: also the prime
+    // qKS of TOY / SIGNED_MOD_TEST (modKS = PRIME: qKS = Q < 2^28, baseKS 25), whose u32 sums are kept mod qKS
+    const bool prime = p.baseKS == 25 && (p.qKS & 1) && p.qKS < (1ull << 28);
+    return !is_large(p.paramset) && !p.timeopt && (prime || (pow2ks && p.qKS > 65536 && p.qKS < (1ull << 32))) &&
            keyswitch_w32_shape(p.baseKS, p.digitsKS) && p.n < 2048 && p.N <= 2048;
 }
 

@@ -158,7 +158,10 @@ FHE_DEV uint32_t ks_digit(uint32_t a, int j) {
     return (a / p) % BASE;
 }
 
-template <int G, bool SPLIT, int BASE, int IPR, int KD = 3, bool W32 = false, int GPT = 1>
+// PRIME (with W32): a prime qKS (TOY, SIGNED_MOD_TEST: modKS = PRIME, qKS = Q < 2^28, baseKS 25): the column
+// sums are kept in [0, qKS) by one conditional add per subtraction (min(d, d + qKS) on the unsigned words) instead of
+// wrapping mod 2^32, and the epilogue adds b mod qKS
+template <int G, bool SPLIT, int BASE, int IPR, int KD = 3, bool W32 = false, int GPT = 1, bool PRIME = false>
 __global__ void __launch_bounds__(G)
     k_keyswitch_tiled(GateArgs g, const void* __restrict__ ksk, const uint32_t* __restrict__ ms_a,
                       const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
@@ -169,6 +172,8 @@ __global__ void __launch_bounds__(G)
     constexpr int kRowB = S_::rowb, kPps = S_::pps, kEB = S_::eb;
     constexpr int kAcc = W32 ? kKsCols : kKsCols / 2;  // u32 sums, or packed u16 pairs
     static_assert(GPT == 1 || (!SPLIT && !W32 && FHE_KS_B64), "GPT > 1: the u16, single-pass form");
+    static_assert(!PRIME || W32, "a prime qKS needs u32 sums");
+    const uint32_t qks = g.qKS;
     static_assert(kKsParts % G == 0 || kKsParts < G, "staging split");
     constexpr int P = kKsParts >= G ? kKsParts / G : 1;  // parts per thread per step
     __shared__ __attribute__((aligned(16))) unsigned char s_buf[2][kKsStep][kBase * kRowB];
@@ -302,8 +307,14 @@ __global__ void __launch_bounds__(G)
                 }
 #pragma unroll
                 for (int k = 0; k < kKsCols / 2; ++k) {
-                    acc[2 * k + 0] -= w[k].x;
-                    acc[2 * k + 1] -= w[k].y;
+                    if (PRIME) {  // acc, w < qKS: acc - w in (-qKS, qKS), brought back to [0, qKS)
+                        const uint32_t d0 = acc[2 * k + 0] - w[k].x, d1 = acc[2 * k + 1] - w[k].y;
+                        acc[2 * k + 0] = min(d0, d0 + qks);
+                        acc[2 * k + 1] = min(d1, d1 + qks);
+                    } else {
+                        acc[2 * k + 0] -= w[k].x;
+                        acc[2 * k + 1] -= w[k].y;
+                    }
                 }
             } else if (FHE_KS_B64) {
                 const uint2* src = reinterpret_cast<const uint2*>(s_buf[buf][q] + dig * kRowB);
@@ -371,7 +382,13 @@ __global__ void __launch_bounds__(G)
 #pragma unroll
         for (int k = 0; k < kKsCols; ++k) {
             const uint32_t c = col0 + k;
-            uint64_t v = ((c == g.n ? b : 0u) + acc[k]) & qm;  // acc = -sum mod 2^32
+            uint64_t v;
+            if (PRIME) {  // acc = -sum mod qKS in [0, qKS), b < qKS
+                const uint32_t x = (c == g.n ? b : 0u) + acc[k];
+                v = min(x, x - qks);
+            } else {
+                v = ((c == g.n ? b : 0u) + acc[k]) & qm;  // acc = -sum mod 2^32
+            }
             if (q_out) v = mod_switch_up(v, g.qKS, q_out);
             if (c < g.n) oa[c] = v;
             else if (c == g.n) b_out[gate] = v;
@@ -394,20 +411,29 @@ __global__ void __launch_bounds__(G)
 
 // the S row-split partials of a gate, one packed column pair per thread and step (hw = W / 2 pairs, up
 // to 640 at W = 1280, on at most 512 threads), then the epilogue
-template <bool W32>
+template <bool W32, bool PRIME = false>
 __global__ void __launch_bounds__(512)
     k_keyswitch_reduce(GateArgs g, const uint32_t* __restrict__ part, uint32_t S, uint32_t hw,
                        const uint32_t* __restrict__ ms_b, uint64_t q_out, uint64_t* __restrict__ a_out,
                        uint64_t* __restrict__ b_out) {
     const uint32_t gate = blockIdx.x;
-    const uint32_t qm = g.qKS - 1;
+    const uint32_t qm = g.qKS - 1, qks = g.qKS;
     const uint32_t b = ms_b[gate];
     uint64_t* oa = a_out + (size_t)gate * g.n;
-    if (W32) {  // hw = ksk_width u32 sums (mod 2^32)
+    if (W32) {  // hw = ksk_width u32 sums (mod 2^32; PRIME: partials in [0, qKS), summed mod qKS)
         for (uint32_t c = threadIdx.x; c < hw; c += blockDim.x) {
             uint32_t acc = 0;
-            for (uint32_t z = 0; z < S; ++z) acc += part[((size_t)z * g.count + gate) * hw + c];
-            uint64_t v = ((c == g.n ? b : 0u) + acc) & qm;
+            for (uint32_t z = 0; z < S; ++z) {
+                acc += part[((size_t)z * g.count + gate) * hw + c];
+                if (PRIME) acc = min(acc, acc - qks);
+            }
+            uint64_t v;
+            if (PRIME) {
+                const uint32_t x = (c == g.n ? b : 0u) + acc;
+                v = min(x, x - qks);
+            } else {
+                v = ((c == g.n ? b : 0u) + acc) & qm;
+            }
             if (q_out) v = mod_switch_up(v, g.qKS, q_out);
             if (c < g.n) oa[c] = v;
             else if (c == g.n) b_out[gate] = v;
@@ -506,7 +532,8 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
 }
 
 bool keyswitch_w32_shape(uint32_t baseKS, uint32_t digitsKS) {
-    return (baseKS == 16 && (digitsKS == 5 || digitsKS == 6)) || (baseKS == 64 && digitsKS == 3);
+    return (baseKS == 16 && (digitsKS == 5 || digitsKS == 6)) || (baseKS == 64 && digitsKS == 3) ||
+           (baseKS == 25 && (digitsKS == 6 || digitsKS == 7));  // the prime-qKS rows (TOY, SIGNED_MOD_TEST)
 }
 
 // u32 rows (ksk_width(n) columns: A then B at column n), any power-of-two qKS <= 2^32, the shapes of
@@ -515,9 +542,34 @@ hipError_t launch_keyswitch_w32(const GateArgs& g, uint32_t baseKS, uint32_t dig
                                 const uint32_t* ms_a, const uint32_t* ms_b, uint64_t q_out, uint64_t* a_out,
                                 uint64_t* b_out, hipStream_t s, uint32_t* part, size_t part_words) {
     if (g.count == 0) return hipSuccess;
-    if (!keyswitch_w32_shape(baseKS, digitsKS) || (g.qKS & (g.qKS - 1)) || g.qKS == 0 || g.n >= 2048 || g.N > 2048)
+    // baseKS 25: a prime qKS below 2^28 (sums kept mod qKS); otherwise a power of two (sums mod 2^32)
+    const bool prime = baseKS == 25;
+    if (!keyswitch_w32_shape(baseKS, digitsKS) || g.qKS < 2 || g.n >= 2048 || g.N > 2048 ||
+        (prime ? (g.qKS >= (1u << 28) || !(g.qKS & 1)) : (g.qKS & (g.qKS - 1)) != 0))
         return hipErrorInvalidValue;
     const uint32_t W = ksk_width(g.n);
+    if (prime) {  // 25 slices of 16 parts per step: 512-thread tiles (400 stagers), 92 KB of double buffer
+        constexpr uint32_t GP = 512;
+        uint32_t S = 1;
+        if (part) {
+            const size_t tiles = ((g.count + GP - 1) / GP) * (W / kKsCols);
+            while (tiles * S < 1024 && g.N / (2 * S) >= 16 && (size_t)2 * S * g.count * W <= part_words) S *= 2;
+        }
+        const dim3 grid((g.count + GP - 1) / GP, W / kKsCols, S);
+#define FHE_KSP_LAUNCH(SP, KD_)                                                                                     \
+    hipLaunchKernelGGL((k_keyswitch_tiled<GP, SP, 25, 1, KD_, true, 1, true>), grid, dim3(GP), 0, s, g, ksk, ms_a, ms_b, \
+                       q_out, a_out, b_out, SP ? part : nullptr)
+        if (digitsKS == 6) { if (S > 1) FHE_KSP_LAUNCH(true, 6); else FHE_KSP_LAUNCH(false, 6); }
+        else { if (S > 1) FHE_KSP_LAUNCH(true, 7); else FHE_KSP_LAUNCH(false, 7); }
+#undef FHE_KSP_LAUNCH
+        if (S > 1) {
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_keyswitch_reduce<true, true>), dim3(g.count), dim3(512), 0, s, g, part, S, W, ms_b, q_out,
+                               a_out, b_out);
+        }
+        return hipGetLastError();
+    }
     constexpr uint32_t G = 256;
     uint32_t S = 1;
     if (part) {  // enough workgroups for 4 per CU, at least 16 rounds each, within the scratch

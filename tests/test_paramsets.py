@@ -112,13 +112,15 @@ def test_gpu_digitsg4_split_kernel_matches_64bit_accumulator(name, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["std128_3", "std128q", "std256q_3"])
+@pytest.mark.parametrize("name", ["std128_3", "std128q", "std256q_3", "toy", "signed_mod_test"])
 def test_gpu_digitsg4_keyswitch_vs_reference(name):
     """the 32-bit key switch these sets now use (u16 rows of 1024 columns; gate-tiled with 64 staged
     slices at baseKS = 64 (STD128_3), 32 at baseKS = 32 (STD128Q); row split below 4096) on uniform
     inputs mod qKS, incl. a ragged last tile, vs the reference's own LWEEncryptionScheme::KeySwitch
     (oracle/_ref, the restatement covers the STD128 sets only).  STD256Q_3 (round 5): baseKS 21, its
-    four digits by division, 21 staged slices, 1408-column rows at n = 1400"""
+    four digits by division, 21 staged slices, 1408-column rows at n = 1400.  TOY / SIGNED_MOD_TEST (round 6):
+    the prime qKS (modKS = PRIME, qKS = Q) on the u32-row tiled kernel with sums kept mod qKS, baseKS 25 with six /
+    seven digits by division, 512-gate tiles"""
     from fhe_amd import binfhe as bf
     from make_golden import GATE_SETS
     from oracle_lib import Ref
