@@ -119,6 +119,9 @@ constexpr int kKsSplitG = 512;
 #ifndef FHE_KS_XCD
 #define FHE_KS_XCD 0
 #endif
+#ifndef FHE_KS_G1024
+#define FHE_KS_G1024 0  // A/B: 1024-thread workgroups with one gate per thread from 32,768 gates (baseKS 32)
+#endif
 #ifndef FHE_KS_GPT
 #define FHE_KS_GPT 1  // gates per thread of the 512-thread tiles (1: 512-gate tiles)
 #endif            // the row split's gate tile
@@ -512,6 +515,10 @@ hipError_t launch_keyswitch(const GateArgs& g, uint32_t baseKS, uint32_t digitsK
                 const dim3 gg((g.count + 512 * FHE_KS_GPT - 1) / (512 * FHE_KS_GPT), W / kKsCols, 1);
                 hipLaunchKernelGGL((k_keyswitch_tiled<512, false, 32, 2, 3, false, FHE_KS_GPT>), gg, dim3(512), 0, s, g,
                                    ksk, ms_a, ms_b, q_out, a_out, b_out, nullptr);
+            } else if (G == 512 && FHE_KS_G1024 && g.count >= 32768) {  // 1024-gate tiles, one thread per gate
+                const dim3 gg((g.count + 1023) / 1024, W / kKsCols, 1);
+                hipLaunchKernelGGL((k_keyswitch_tiled<1024, false, 32, 2>), gg, dim3(1024), 0, s, g, ksk, ms_a, ms_b, q_out,
+                                   a_out, b_out, nullptr);
             } else if (G == 512) FHE_KS_LAUNCH(512, false, 32, 2);
             else FHE_KS_LAUNCH(256, false, 32, 4);
         } else {
