@@ -1996,6 +1996,10 @@ static_assert(x_lds() <= 160 * 1024, "LDS per workgroup");
 static_assert(kXTiles == 1 || kXTiles == 2, "transpose tiles");
 }  // namespace
 
+// MF: ciphertext modulus 2N (BootstrapFunc of EvalFunc's arbitrary functions, seam calls at 2N): any exponent, the
+// full-resolution table psi^e - 1 restricted to e in [0, 2N] (as K1s); ACCIO: the Backend::BlindRotate seam
+// (GateArgs::acc_io), as K1 / K1s.  Test-vector tables (g.tv, BootstrapFuncCore) are read as K1 reads them.
+template <bool MF, bool ACCIO>
 __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
     k_blind_rotate_ginx2x(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
                           const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
@@ -2010,7 +2014,8 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
         s_tab[i]  = T.tabF[i];
         s_tabI[i] = T.tabI[i];
     }
-    for (int i = threadIdx.x; i < kMonoHalfWords; i += blockDim.x) s_mono2[i] = make_uint2(T.monoP[i], T.mono[i]);
+    for (int i = threadIdx.x; i < kMonoHalfWords; i += blockDim.x)
+        s_mono2[i] = MF ? make_uint2(T.monoP_full[i], T.mono_full[i]) : make_uint2(T.monoP[i], T.mono[i]);
 
     const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
     const int c = wave & 1;  // RLWE component of this wave
@@ -2036,10 +2041,15 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
         for (int z = 0; z < FHE_X_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
 #endif
 
-    // initial accumulator (BootstrapGateCore, binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0
+    // initial accumulator (BootstrapGateCore, binfhe-base-scheme.cpp:556-575, or BootstrapFuncCore :596-608 from
+    // the table g.tv): acc1 = NTT(m), acc0 = 0; the seam's accumulators from g.acc_io
     uint32_t acc[16];
-    if (c == 1) {
+    if (ACCIO && !g.acc_tv) {
+        acc_load_c(acc, g, gate, c, L, T.ninvR, m);
+    } else if (c == 1) {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        // EvalFuncMultiOutput: table gate % tv_mod (GateArgs::tv_mod)
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
         uint32_t tv[1][16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -2047,7 +2057,7 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
             uint32_t v = 0;
             if (x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
-                v = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                v = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
             tv[0][r] = v;
         }
@@ -2067,7 +2077,7 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
     const uint4* kc = keys + (size_t)c * (kQ * 8 * 64) + L;
     for (uint32_t i = 0; i < g.n; ++i) {
         const Mod m = fresh_nq(m0);
-        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> 1;  // even exponents (ctmod < 2N)
+        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> (MF ? 0 : 1);  // even unless MF
         const uint4* kb = kc + (size_t)i * (2 * kQ * 8 * 64);
 #if FHE_X_ABL == 2
         asm volatile("" : "+v"(kb));
@@ -2086,20 +2096,20 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
         uint32_t* xb = xown + (i & 1) * kG2Tile;
         fwd_wave_s<ND, kXTiles>(d, tile, L, twAf, s_tab, m, xb);
         if (kXTiles == 2) wave_lds_sync();  // its last reads done before the partner words overwrite it
-        const uint32_t fl = (as * lmul) & 1023u;
+        const uint32_t fl = (as * lmul) & (MF ? 2047u : 1023u);
         uint32_t* xo = xb + L;
-        // the monomial pair of slot pair k2: psi^(2f) - 1 and psi^(-2f) - 1, requested one slot pair ahead
-        // of its use (LDS latency off the MAC's critical path, as K1's issue())
-        auto mono = [&](int k2, uint2& mp, uint2& mn) {
-            const int r0 = 2 * k2;
+        // the monomial pair of slot pair k2: psi^(2f) - 1 and psi^(-2f) - 1 (MF: of register r0 = 2 k2,
+        // psi^e - 1 and psi^(2N - e) - 1), requested one slot pair ahead of its use when FHE_X_MPF
+        auto mono_r = [&](int r0, uint2& mp, uint2& mn) {
             const uint32_t ur = __builtin_amdgcn_readfirstlane(
                 (as * (512u * (__builtin_bitreverse32((uint32_t)(r0 & 3)) >> 30) +
-                       2u * (__builtin_bitreverse32((uint32_t)(r0 >> 2)) >> 30))) & 1023u);
-            const uint32_t f  = fl + ur;    // < 2N
-            const uint32_t fn = 2048u - f;  // -a: 2N - f
+                       2u * (__builtin_bitreverse32((uint32_t)(r0 >> 2)) >> 30))) & (MF ? 2047u : 1023u));
+            const uint32_t f  = MF ? (fl + ur) & 2047u : fl + ur;  // < 2N
+            const uint32_t fn = 2048u - f;                        // -a: 2N - f
             mp = s_mono2[f + (f >> 5)];
             mn = s_mono2[fn + (fn >> 5)];
         };
+        auto mono = [&](int k2, uint2& mp, uint2& mn) { mono_r(2 * k2, mp, mn); };
         uint2 mq[2][2];
 #if FHE_X_MPF
         mono(0, mq[0][0], mq[0][1]);
@@ -2118,11 +2128,13 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
 #if !FHE_X_MPF
             mono(k2, mq[k2 & 1][0], mq[k2 & 1][1]);
 #endif
-            const uint2 mp = mq[k2 & 1][0], mn = mq[k2 & 1][1];
+            uint2 mp = mq[k2 & 1][0], mn = mq[k2 & 1][1];
             const uint4* q4 = kq[k2 & 1];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = r0 + e;
+                // MF: x bit 0 adds 1024 a to the exponent: registers r0, r0 + 1 differ for odd a
+                if (MF && e == 1) mono_r(r, mp, mn);
 #pragma unroll
                 for (int o = 0; o < 2; ++o) {  // o = 0: this wave's component, 1: the partner's
                     int64_t S1 = 0, S2 = 0;
@@ -2155,6 +2167,10 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
         for (int r = 0; r < 16; ++r) acc[r] += xp[r << 6];
     }
 
+    if (ACCIO) {  // after the last barrier: every wave of the workgroup leaves here
+        if (live) acc_store_c(acc, g, gate, c, L, T.nR, m);
+        return;
+    }
     // extraction (binfhe-base-scheme.cpp:110-121): canonical COEF in layout A; wave 0 writes the transposed
     // acc0 (coefficient k -> position N - k, negated), wave 1 the b term from acc1[0] (tile private: no barrier)
     inv_wave_s<kXAcc, true>(acc, tile, L, s_tabI, T.w1R, m.oneR, m);
@@ -2198,19 +2214,33 @@ hipError_t launch_repack_ginx2x(const void* bsk, uint32_t n, void* bskx, hipStre
     return hipGetLastError();
 }
 
+bool ginx2x_supported(const GateArgs& g, const BootTables& t) {
+    return t.Q < (1u << 27) && g.N == 1024 && g.ctmod <= 2 * g.N && g.tv64 == nullptr && g.gbits >= 2 &&
+           3 * g.gbits <= 32;
+}
+
 hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
                                       const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if (!ginx2_supported(g, t)) return hipErrorInvalidValue;
+    if (!ginx2x_supported(g, t)) return hipErrorInvalidValue;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blind_rotate_ginx2x),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)x_lds());
+        for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_ginx2x<false, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx2x<true, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx2x<false, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx2x<true, true>)})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)x_lds());
         return true;
     }();
     (void)attr;
     const uint32_t blocks = (g.count + kXGates - 1) / kXGates;
-    hipLaunchKernelGGL(k_blind_rotate_ginx2x, dim3(blocks), dim3(128 * kXGates), x_lds(), s, g, t,
-                       static_cast<const uint4*>(bskx), idx, tvb, ext_a, ext_b, t.twA_fwd);
+#define FHE_LAUNCH_X(MF_, IO)                                                                                       \
+    hipLaunchKernelGGL((k_blind_rotate_ginx2x<MF_, IO>), dim3(blocks), dim3(128 * kXGates), x_lds(), s, g, t,         \
+                       static_cast<const uint4*>(bskx), idx, tvb, ext_a, ext_b, t.twA_fwd)
+    const bool mf = g.ctmod == 2 * g.N;
+    if (g.acc_io) { if (mf) FHE_LAUNCH_X(true, true); else FHE_LAUNCH_X(false, true); }
+    else if (mf) FHE_LAUNCH_X(true, false);
+    else FHE_LAUNCH_X(false, false);
+#undef FHE_LAUNCH_X
     return hipGetLastError();
 }
 

@@ -95,9 +95,10 @@ uint32_t Engine::kernel() const {
 }
 
 int Engine::ginx_choice(const GateArgs& g) const {
-    const bool two = d_bsk2_ && ginx2_supported(g, tabs_);
-    if (two && ginx_kernel_ == 2) return 2;
-    if (two && (ginx_kernel_ == 3 || (ginx_kernel_ == 0 && g.count <= x_batch_))) return 3;
+    if (!d_bsk2_) return 1;
+    if (ginx_kernel_ == 2) return ginx2_supported(g, tabs_) ? 2 : 1;
+    // K1x: gates, BootstrapFunc tables and the seam's accumulators, ciphertext modulus q or 2N
+    if (ginx2x_supported(g, tabs_) && (ginx_kernel_ == 3 || (ginx_kernel_ == 0 && g.count <= x_batch_))) return 3;
     return 1;
 }
 

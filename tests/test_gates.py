@@ -346,3 +346,48 @@ def test_gpu_split_ginx_kernel_bit_exact(kind):
         assert np.array_equal(s[0], w[0]) and np.array_equal(s[1], w[1]), count
     for e in engines.values():
         e.close()
+
+
+@pytest.mark.gpu
+def test_gpu_k1x_bootstrap_func_and_seam_match_one_wave_kernel():
+    """K1x (FHE_HIP_GINX_KERNEL=xsplit) beyond gates: BootstrapFunc with test-vector tables at ciphertext modulus q
+    and 2N (the full-resolution monomials: odd exponents), EvalFuncMultiOutput's per-gate tables (tv_mod), and the
+    seam's BlindRotate on arbitrary accumulators at moduli q and 2N == the one-wave kernel K1 on the same inputs
+    (K1 is pinned to the reference by tests/test_fb.py and tests/test_backend.py); the default context runs K1x on
+    these small batches and reproduces K1 too"""
+    import os
+    from fhe_amd import binfhe as bf
+    ps, m = bf.STD128, bf.GINX
+    keys = bf.keygen(ps, m, 9)
+    eng = {}
+    for kind in ("xsplit", "wave", None):
+        if kind:
+            os.environ["FHE_HIP_GINX_KERNEL"] = kind
+        try:
+            e = bf.GateEngine(ps, m, device=0)
+        finally:
+            os.environ.pop("FHE_HIP_GINX_KERNEL", None)
+        e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        eng[kind or "default"] = e
+    P = eng["wave"].params
+    rng = np.random.default_rng(123)
+    for kind in ("xsplit", "default"):
+        x, w = eng[kind], eng["wave"]
+        for ctmod in (P.q, 2 * P.N):
+            cnt = 37
+            a = rng.integers(0, ctmod, (cnt, P.n), dtype=np.uint64)
+            b = rng.integers(0, ctmod, cnt, dtype=np.uint64)
+            f = rng.integers(0, 8, ctmod, dtype=np.uint64)
+            assert all(np.array_equal(u, v) for u, v in zip(x.bootstrap_func(a, b, ctmod, f, 8),
+                                                              w.bootstrap_func(a, b, ctmod, f, 8))), (kind, ctmod)
+            acc = rng.integers(0, P.Q, (cnt, 2, P.N), dtype=np.uint64)
+            assert np.array_equal(x.blind_rotate_acc(a, ctmod, acc), w.blind_rotate_acc(a, ctmod, acc)), (kind, ctmod)
+        bits = rng.integers(0, 4, 13)
+        ca, cb = bf.encrypt(ps, m, keys.sk, bits, 77, p=8)
+        xs = np.arange(P.q) * 8 // P.q    # GenerateLUTviaFunction's form for p = 8: (f(x) mod p) q / p
+        luts = np.stack([((xs * k + 1) % 8) * (P.q // 8) for k in (1, 3, 5)]).astype(np.uint64)
+        assert all(np.array_equal(u, v) for u, v in zip(x.eval_func_multi(ca, cb, P.q, luts),
+                                                          w.eval_func_multi(ca, cb, P.q, luts)))
+        assert x.gate_kernel(37) == "k_blind_rotate_ginx2x"
+    for e in eng.values():
+        e.close()
