@@ -129,6 +129,15 @@ bool ginx3_supported(const GateArgs& g, const BootTables& t);
 hipError_t launch_blind_rotate_lmk3(const GateArgs& g, const BootTables& t, const void* ek, const void* ak,
                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
                                     uint64_t* ext_a, uint64_t* ext_b, hipStream_t s);
+// Its two-digit form (K1m, ND = 2) as the small-batch LMKCDEY kernel of the fast path (digitsG = 3, N = 1024,
+// Q < 2^28: STD128_LMKCDEY, STD128_3_LMKCDEY, STD128Q_LMKCDEY, LPF_STD128_LMKCDEY, MEDIUM): keys repacked on the
+// device from the resident layout (launch_repack_lmkx: n * 8192 + nauto * 4096 words), u32 ctExt, tables g.tv;
+// gw gates per workgroup (1 or 2: k_blind_rotate_lmk3)
+hipError_t launch_repack_lmkx(const void* bsk, uint32_t n, uint32_t nauto, void* bskx, hipStream_t s);
+hipError_t launch_blind_rotate_lmkx(const GateArgs& g, const BootTables& t, const void* ekx, uint32_t n,
+                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                    uint32_t* ext_a, uint32_t* ext_b, int gw, hipStream_t s);
+bool lmkx_supported(const GateArgs& g, const BootTables& t);
 // split-kernel key layout, per index i (8192 nd words): [c][p < 2 nd][k2 < 8][64 lanes][4 words]
 // = (K+[r], K+[r+1], K-[r], K-[r+1]) of component c, digit row g2_row(c, p, nd), r = 2 k2, EVAL slot
 // x(L, r) = ((r >> 2) << 8) | (L << 2) | (r & 3): wave c multiplies (own digits D_c, D_{2+c}, ..,

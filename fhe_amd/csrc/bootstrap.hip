@@ -2259,10 +2259,20 @@ hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, co
 // Keys (Engine::pack_ginx3, u32 Montgomery with N^-1 folded in), one uint4 = 4 registers:
 //   ek: [i][c][p < 6][k4 < 4][64 lanes] rows g2_row(c, p, 3);  ak: [t][c][d < 3][k4 < 4][64 lanes].
 // Bounds (Q < 2^27): |D| < 10 Q + 2^6, |S| < 61 Q^2 < 2^60, acc < 61 Q / 32 + Q / 2 < 2.8 Q.
+// Round 6, ND = 2 (digitsG = 3: STD128_LMKCDEY, STD128_3_LMKCDEY, STD128Q_LMKCDEY, LPF_STD128_LMKCDEY, MEDIUM),
+// the small-batch form of the one-wave op-list kernel k_blind_rotate_lmk on its fast path (u32 ctExt, keys
+// repacked on the device by k_repack_lmkx, test-vector tables g.tv): LZ = Q < 2^27, else Q < 2^28 with the
+// 8 Q headroom (kL3Acc; the test vector centred before its forward transform: |v| <= Q/2 grows to < 7.6 Q).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kL3Reg = 3 * kG2Tile;  // words per wave: 3 tiles / the 3 digit polynomials / a permutation
-constexpr size_t l3_lds() { return (size_t)(1024 + 1024 + 2 * kL3Reg) * 4; }
+// words per wave: ND tiles / the ND digit polynomials / a permutation
+constexpr int l3_reg(int nd) { return nd * kG2Tile; }
+constexpr size_t l3_lds(int nd, int gw) { return (size_t)(1024 + 1024 + 2 * gw * l3_reg(nd) + 4 * gw) * 4; }
+// |acc| between ops (units of Q/10): 2.8 Q for Q < 2^27 (above); for Q < 2^28 (ND = 2: STD128_LMKCDEY, MEDIUM)
+// the forward transform takes signed digits to < 6.67 Q (FHE_FWD_TIGHT), so an EXT sum is below
+// 4 (6.67 Q) Q = 26.7 Q^2 and the reduced acc below 26.7 Q / 16 + Q / 2 < 2.2 Q; an AUTO sum of acc1 is below
+// 2.2 Q Q + 2 (6.67 Q) Q
+template <bool LZ> constexpr int kL3Acc = LZ ? kAccBoundLZ : 22;
 // EVAL automorphism X -> X^k (as automorphism_eval) on layout C through this wave's region:
 // slot x(L, r) has brv10(x) = brv2(r & 3) << 8 | brv6(L) << 2 | brv2(r >> 2), so
 // (2 brv10(x) + 1) k = k (8 brv6(L) + 1) + k (512 brv2(r & 3) + 2 brv2(r >> 2))
@@ -2286,13 +2296,19 @@ FHE_DEV void automorphism_c(uint32_t (&v)[16], uint32_t* region, int L, uint32_t
 }
 }  // namespace
 
-template <bool ACCIO>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
+// GW: gates per workgroup.  GW = 1 up to one gate per CU; GW = 2 up to two (round 6, STD128_LMKCDEY): four waves of
+// one workgroup take the four SIMDs of a CU, where two 128-thread workgroups may share two of them (512 gates
+// 5.2 ms against 3.7 at 64).  The two gates' op lists differ, so a workgroup barrier would run them in lockstep
+// (every op as long as the slower of the two: 4.1 ms at 64 gates); the two waves of a gate meet instead at a
+// pair of LDS counters (gate_sync): 4.3 ms at 512 gates
+template <int ND, bool LZ, typename OutT, bool ACCIO, int GW>
+__global__ void __launch_bounds__(128 * GW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_blind_rotate_lmk3(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
                         const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
-                        const uint32_t* __restrict__ tvb, uint64_t* __restrict__ ext_a, uint64_t* __restrict__ ext_b,
+                        const uint32_t* __restrict__ tvb, OutT* __restrict__ ext_a, OutT* __restrict__ ext_b,
                         const uint32_t* __restrict__ twAf) {
-    constexpr int ND = 3, kRows = 2 * ND;
+    constexpr int kRows = 2 * ND;
+    constexpr int BIN = kL3Acc<LZ>;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     uint32_t* s_tab  = sm;
     uint32_t* s_tabI = sm + 1024;
@@ -2301,15 +2317,36 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
         s_tab[i]  = T.tabF[i];
         s_tabI[i] = T.tabI[i];
     }
-    const int c = threadIdx.x >> 6, L = threadIdx.x & 63;  // wave c: RLWE component c
-    const uint32_t gate = blockIdx.x;
-    uint32_t* region  = s_reg + c * kL3Reg;
-    uint32_t* partner = s_reg + (c ^ 1) * kL3Reg;
+    uint32_t* s_flag = s_reg + 2 * GW * l3_reg(ND);  // GW > 1: one counter per wave
+    if (GW > 1 && threadIdx.x < 2 * GW) s_flag[threadIdx.x] = 0;
+    const int wave = threadIdx.x >> 6, c = wave & 1, L = threadIdx.x & 63;  // wave c of a gate: RLWE component c
+    const uint32_t gslot = blockIdx.x * GW + (wave >> 1);
+    const bool live = gslot < g.count;
+    const uint32_t gate = live ? gslot : g.count - 1;  // a spare gate's waves shadow the last gate's
+    uint32_t* region  = s_reg + wave * l3_reg(ND);
+    uint32_t* partner = s_reg + (wave ^ 1) * l3_reg(ND);
     uint32_t* t0 = region;
     const Mod m0 = make_mod(T);
     const Mod& m = m0;
     const uint32_t M = 2 * g.N;
     __syncthreads();
+    if (GW > 1 && !live) return;  // (no workgroup barrier below when GW > 1)
+    // the two waves of this gate meet: sync k publishes this wave's LDS writes and reads before it and waits for
+    // the partner's sync k (LDS ordering only: key loads in flight stay in flight)
+    uint32_t nsync = 0;
+    auto gate_sync = [&]() {
+        if (GW == 1) {
+            __syncthreads();
+            return;
+        }
+        ++nsync;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __hip_atomic_store(s_flag + wave, nsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(s_flag + (wave ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < nsync)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
 
     // BootstrapGateCore (binfhe-base-scheme.cpp:556-575): acc1 = NTT(m), acc0 = 0; then
     // acc1 <- acc1(X^(2N-5)) (:99; acc0 = 0 is invariant)
@@ -2319,6 +2356,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
         if (c == 1) automorphism_c(acc, region, L, M - 5);   // acc1 <- acc1(X^(2N-5)) (:99)
     } else if (c == 1) {
         const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        // BootstrapFuncCore's table g.tv (:596-608), EvalFuncMultiOutput: table gate % tv_mod (GateArgs::tv_mod)
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
         uint32_t tv[1][16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -2326,8 +2365,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             uint32_t v = 0;
             if (x % g.factor == 0) {
                 const uint32_t bx = (b - x / g.factor) & cm;
-                v = (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+                v = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
             }
+            if (!LZ) v = v > (m.Q >> 1) ? v - m.Q : v;  // centred: |v| <= Q/2 (8 Q headroom)
             tv[0][r] = v;
         }
         fwd_wave_s<1>(tv, t0, L, twAf, s_tab, m);
@@ -2346,7 +2386,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (uint32_t it = 0; it < cnt; ++it) {
         const Mod m = fresh_nq(m0);
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
-        __syncthreads();  // the partner wave has read this wave's region (previous op)
+        gate_sync();  // the partner wave has read this wave's region (previous op)
         uint32_t d[ND][16];
         if (!(op & 0x8000u)) {
             // ---- AddToAccLMKCDEY: acc_c <- sum_p D_p ek[op][g2_row(c, p)][c]   (acc replaced)
@@ -2356,7 +2396,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int p = 0; p < kRows; ++p) kq[0][p] = kb[(p * 4 + 0) * 64];
 #pragma unroll
             for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
-            inv_wave_s<kAccBoundLZ, true>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
+            inv_wave_s<BIN, LZ>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
             for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
             fwd_wave_s<ND>(d, t0, L, twAf, s_tab, m);
@@ -2365,7 +2405,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int r = 0; r < 16; ++r)
 #pragma unroll
                 for (int j = 0; j < ND; ++j) region[j * 1024 + ((r << 6) | L)] = d[j][r];
-            __syncthreads();  // both waves' digits are in LDS
+            gate_sync();  // both waves' digits are in LDS
 #pragma unroll
             for (int k4 = 0; k4 < 4; ++k4) {
                 if (k4 + 1 < 4) {
@@ -2403,7 +2443,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
             if (c == 0) {  // acc0' -> COEF -> 3 digits -> EVAL, to this wave's region
 #pragma unroll
                 for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
-                inv_wave_s<kAccBoundLZ, true>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
+                inv_wave_s<BIN, LZ>(d[0], t0, L, s_tabI, T.w1R, m.oneR, m);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
                 fwd_wave_s<ND>(d, t0, L, twAf, s_tab, m);
@@ -2413,7 +2453,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
                     for (int j = 0; j < ND; ++j) region[j * 1024 + ((r << 6) | L)] = d[j][r];
             }
-            __syncthreads();  // acc0's digits are in wave 0's region
+            gate_sync();  // acc0's digits are in wave 0's region
             const uint32_t* src = c == 0 ? region : partner;
 #pragma unroll
             for (int k4 = 0; k4 < 4; ++k4) {
@@ -2440,14 +2480,15 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 
     if (ACCIO) {
-        acc_store_c(acc, g, gate, c, L, T.nR, m);
+        if (live) acc_store_c(acc, g, gate, c, L, T.nR, m);
         return;
     }
     // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_ginx2
-    __syncthreads();
-    inv_wave_s<kAccBoundLZ, true>(acc, t0, L, s_tabI, T.w1R, m.oneR, m);
+    gate_sync();
+    inv_wave_s<BIN, LZ>(acc, t0, L, s_tabI, T.w1R, m.oneR, m);
+    if (!live) return;
     if (c == 0) {
-        uint64_t* oa = ext_a + (size_t)gate * g.N;
+        OutT* oa = ext_a + (size_t)gate * g.N;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
@@ -2468,14 +2509,66 @@ hipError_t launch_blind_rotate_lmk3(const GateArgs& g, const BootTables& t, cons
     if (!(t.Q < (1u << 27) && g.N == 1024 && g.tv == nullptr && g.tv64 == nullptr && g.gbits >= 2 &&
           4 * g.gbits <= 32 && g.qKS <= 65536))
         return hipErrorInvalidValue;
-    if (g.acc_io)
-        hipLaunchKernelGGL(k_blind_rotate_lmk3<true>, dim3(g.count), dim3(128), l3_lds(), s, g, t,
-                           static_cast<const uint4*>(ek), static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a,
-                           ext_b, t.twA_fwd);
-    else
-        hipLaunchKernelGGL(k_blind_rotate_lmk3<false>, dim3(g.count), dim3(128), l3_lds(), s, g, t,
-                           static_cast<const uint4*>(ek), static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a,
-                           ext_b, t.twA_fwd);
+#define FHE_LAUNCH_L3(IO)                                                                                          \
+    hipLaunchKernelGGL((k_blind_rotate_lmk3<3, true, uint64_t, IO, 1>), dim3(g.count), dim3(128), l3_lds(3, 1), s, g, t, \
+                       static_cast<const uint4*>(ek), static_cast<const uint4*>(ak), ops, nops, maxops, tvb, ext_a,  \
+                       ext_b, t.twA_fwd)
+    if (g.acc_io) FHE_LAUNCH_L3(true);
+    else FHE_LAUNCH_L3(false);
+#undef FHE_LAUNCH_L3
+    return hipGetLastError();
+}
+
+// the resident LMKCDEY layout (row_off, half-swapped rows: [n][4][16][64] uint2 ++ [nA + 1][2][16][64] uint2) ->
+// k_blind_rotate_lmk3<2, ..>'s: ek [n][c][p < 4][k4 < 4][64][4] (rows g2_row(c, p, 2)) ++ ak [nA + 1][c][d < 2][k4][64][4]
+__global__ void k_repack_lmkx(const uint32_t* __restrict__ src, uint32_t n, uint32_t nauto, uint32_t* __restrict__ dst) {
+    const uint64_t ekw = (uint64_t)n * 8192, words = ekw + (uint64_t)nauto * 4096;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
+        const bool auto_key = t >= ekw;
+        const uint64_t u = auto_key ? t - ekw : t;
+        const uint64_t i = auto_key ? u >> 12 : u >> 13;
+        const uint32_t w = (uint32_t)(u & (auto_key ? 4095 : 8191));
+        const uint32_t e = w & 3, L = (w >> 2) & 63, k4 = (w >> 8) & 3;
+        const uint32_t c = auto_key ? w >> 11 : w >> 12, p = auto_key ? (w >> 10) & 1 : (w >> 10) & 3;
+        const uint32_t row = auto_key ? p : g2_row(c, p, 2);
+        const uint32_t x = (k4 << 8) | (L << 2) | e;  // EVAL slot of layout C
+        const uint32_t lane = c * 32 + (x >> 5), kk = (x & 31) >> 1, ee = x & 1;
+        const uint32_t dpos = kBskHalfSwap ? row ^ c : row;
+        const uint64_t base = auto_key ? ekw + i * 4096 : i * 8192;
+        dst[t] = src[base + row_off(dpos, kk, lane, ee)];
+    }
+}
+
+hipError_t launch_repack_lmkx(const void* bsk, uint32_t n, uint32_t nauto, void* bskx, hipStream_t s) {
+    const uint64_t words = (uint64_t)n * 8192 + (uint64_t)nauto * 4096;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((words + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_repack_lmkx, dim3(blocks), dim3(256), 0, s, static_cast<const uint32_t*>(bsk), n, nauto,
+                       static_cast<uint32_t*>(bskx));
+    return hipGetLastError();
+}
+
+bool lmkx_supported(const GateArgs& g, const BootTables& t) {
+    return t.Q < (1u << 28) && g.N == 1024 && g.tv64 == nullptr && g.gbits >= 2 && 3 * g.gbits <= 32;
+}
+
+hipError_t launch_blind_rotate_lmkx(const GateArgs& g, const BootTables& t, const void* ekx, uint32_t n,
+                                    const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                    uint32_t* ext_a, uint32_t* ext_b, int gw, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!lmkx_supported(g, t) || (gw != 1 && gw != 2)) return hipErrorInvalidValue;
+    const uint4* ek = static_cast<const uint4*>(ekx);
+    const uint4* ak = ek + (size_t)n * 2048;
+#define FHE_LAUNCH_LX(LZ_, IO, GW_)                                                                                    \
+    hipLaunchKernelGGL((k_blind_rotate_lmk3<2, LZ_, uint32_t, IO, GW_>), dim3((g.count + GW_ - 1) / GW_), dim3(128 * GW_), \
+                       l3_lds(2, GW_), s, g, t, ek, ak, ops, nops, maxops, tvb, ext_a, ext_b, t.twA_fwd)
+#define FHE_LAUNCH_LX2(LZ_, IO) \
+    if (gw == 1) FHE_LAUNCH_LX(LZ_, IO, 1); else FHE_LAUNCH_LX(LZ_, IO, 2)
+    const bool lz = t.Q < (1u << 27);
+    if (g.acc_io) { if (lz) { FHE_LAUNCH_LX2(true, true); } else { FHE_LAUNCH_LX2(false, true); } }
+    else if (lz) { FHE_LAUNCH_LX2(true, false); }
+    else { FHE_LAUNCH_LX2(false, false); }
+#undef FHE_LAUNCH_LX2
+#undef FHE_LAUNCH_LX
     return hipGetLastError();
 }
 

@@ -102,6 +102,11 @@ int Engine::ginx_choice(const GateArgs& g) const {
     return 1;
 }
 
+bool Engine::lmk_split(const GateArgs& g) const {
+    if (p_.method != M_LMKCDEY || wide_ || !d_bsk2_ || lmk_kernel_ == 1 || !lmkx_supported(g, tabs_)) return false;
+    return lmk_kernel_ == 2 || g.count <= x_batch_;
+}
+
 const char* Engine::gate_kernel(size_t count) const {
     const GateArgs g = gate_args(G_AND, count ? count : 1);
     const int nd = (int)p_.digitsG - 1;
@@ -114,7 +119,7 @@ const char* Engine::gate_kernel(size_t count) const {
         if (g3_ && ginx3_supported(g, tabs_)) return "k_blind_rotate_ginx2";
         return "k_blind_rotate_wide";
     }
-    if (p_.method != M_GINX) return "k_blind_rotate_lmk";
+    if (p_.method != M_GINX) return lmk_split(g) ? "k_blind_rotate_lmk3" : "k_blind_rotate_lmk";
     const int k = ginx_choice(g);
     return k == 2 ? "k_blind_rotate_ginx2" : k == 3 ? "k_blind_rotate_ginx2x" : "k_blind_rotate_ginx";
 }
@@ -366,6 +371,10 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     if (const char* k = std::getenv("FHE_HIP_GINX_KERNEL")) {
         const std::string v(k);
         ginx_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : v == "xsplit" ? 3 : 0;
+    }
+    if (const char* k = std::getenv("FHE_HIP_LMK_KERNEL")) {
+        const std::string v(k);
+        lmk_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : 0;
     }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
@@ -676,6 +685,14 @@ void Engine::load_bsk(const uint64_t* bsk, size_t words) {
 // the two-wave GINX kernels' key layouts, repacked on the device from the resident one: K1s's
 // (k_blind_rotate_ginx2, FHE_HIP_GINX_KERNEL=split) or K1x's (k_blind_rotate_ginx2x, the small-batch default)
 void Engine::repack_ginx2() {
+    if (p_.method == M_LMKCDEY && !wide_ && d_bsk_ && lmk_kernel_ != 1) {  // K1m's two-digit form
+        FHE_HIP_CHECK(hipSetDevice(device_));
+        const uint32_t nauto = p_.numAutoKeys + 1;
+        if (!d_bsk2_) FHE_HIP_CHECK(hipMalloc(&d_bsk2_, ((size_t)p_.n * 8192 + (size_t)nauto * 4096) * 4));
+        FHE_HIP_CHECK(launch_repack_lmkx(d_bsk_, p_.n, nauto, d_bsk2_, stream_));
+        FHE_HIP_CHECK(hipStreamSynchronize(stream_));
+        return;
+    }
     if (p_.method != M_GINX || wide_ || !d_bsk_ || ginx_kernel_ == 1 || (ginx_kernel_ == 0 && x_batch_ == 0)) return;
     FHE_HIP_CHECK(hipSetDevice(device_));
     if (!d_bsk2_) FHE_HIP_CHECK(hipMalloc(&d_bsk2_, (size_t)p_.n * 16384 * 4));
@@ -752,7 +769,8 @@ void Engine::copy_keys_from(const Engine& src) {
     const int two_src = src.ginx_kernel_ == 1 ? 0 : src.ginx_kernel_ == 2 ? 2 : 3;
     const int two_dst = ginx_kernel_ == 1 ? 0 : ginx_kernel_ == 2 ? 2 : 3;
     if (src.wide_ != wide_ || src.narrow_ != narrow_ || src.g3_ != g3_ || src.n2k_ != n2k_ || src.ks32_ != ks32_ ||
-        src.ks32w_ != ks32w_ || (!wide_ && p_.method == M_GINX && two_src != two_dst))
+        src.ks32w_ != ks32w_ || (!wide_ && p_.method == M_GINX && two_src != two_dst) ||
+        (!wide_ && p_.method == M_LMKCDEY && (src.lmk_kernel_ == 1) != (lmk_kernel_ == 1)))
         throw std::invalid_argument("copy_keys_from: the contexts pack their keys in different layouts "
                                     "(created under different FHE_HIP_* kernel settings)");
     if (!src.ready()) throw std::logic_error("copy_keys_from: the source context has no keys");
@@ -1019,6 +1037,11 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
             FHE_HIP_CHECK(launch_blind_rotate_ginx2x(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
         else
             FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+    } else if (lmk_split(g)) {
+        // two waves per gate up to x_batch_ gates (as K1x for GINX): one gate per 128-thread workgroup up to one
+        // per CU, two per 256-thread workgroup above (bootstrap.hip k_blind_rotate_lmk3's GW)
+        FHE_HIP_CHECK(launch_blind_rotate_lmkx(g, tabs_, d_bsk2_, p_.n, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
+                                               d_ext_b_, 2 * (size_t)g.count <= x_batch_ ? 1 : 2, s));
     } else {
         FHE_HIP_CHECK(launch_blind_rotate_lmk(g, tabs_, d_bsk_, d_autok_, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
                                               d_ext_b_, p_.method == M_AP, s));

@@ -257,7 +257,12 @@ private:
     // (K1), 768 gates 4.28 vs 4.18, 1024 gates 4.56 vs 4.24: once two of its waves share a SIMD they overlap
     // poorly, and the one-wave kernel wins
     uint32_t x_batch_ = 512;
-    void* d_bsk2_ = nullptr;   // K1s / K1x key layout (g3_: K1s's nd = 3 layout; n2k_: K1w's)
+    // LMKCDEY kernel choice on the fast path: 0 by batch size, 1 the one-wave op-list kernel (K1 LMK), 2 two
+    // waves per gate (K1m's two-digit form, k_blind_rotate_lmk3<2, ..>) -- FHE_HIP_LMK_KERNEL = wave | split
+    int lmk_kernel_ = 0;
+    // true: this LMKCDEY launch runs on K1m's two-digit form (lmk_kernel_ pins, else up to x_batch_ gates)
+    bool lmk_split(const GateArgs& g) const;
+    void* d_bsk2_ = nullptr;   // K1s / K1x / K1m-2 key layout (g3_: K1s's nd = 3 layout; n2k_: K1w's)
     void repack_ginx2();
     // digitsG = 4 GINX sets at N = 1024, Q < 2^27 (STD128_3, STD128Q, STD128_4, LPF_STD128, LPF_STD128Q):
     // gates on the split kernel with three digits per component (launch_blind_rotate_ginx3) over the

@@ -391,3 +391,65 @@ def test_gpu_k1x_bootstrap_func_and_seam_match_one_wave_kernel():
         assert x.gate_kernel(37) == "k_blind_rotate_ginx2x"
     for e in eng.values():
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ps_name", ["STD128_LMKCDEY", "STD128Q_LMKCDEY", "MEDIUM"])
+def test_gpu_lmk_split_kernel_matches_one_wave_kernel(ps_name):
+    """LMKCDEY's small-batch kernel, K1m's two-digit form (k_blind_rotate_lmk3<2, ..>: two waves per gate, the default
+    up to two gates per CU, FHE_HIP_LMK_KERNEL=split pins it) == the one-wave op-list kernel K1 LMK
+    (FHE_HIP_LMK_KERNEL=wave, pinned to the reference by the gate / fb / backend goldens) on gates of every type
+    (1, 5, 37 gates and 1027 pinned), BootstrapFunc tables at the moduli q and 2N, EvalFuncMultiOutput and the
+    seam's BlindRotate; Q >= 2^27 (STD128_LMKCDEY, MEDIUM: 8 Q of signed headroom) and Q < 2^27 (STD128Q_LMKCDEY)"""
+    import os
+    from fhe_amd import binfhe as bf
+    ps, m = bf.PARAMSETS.index(ps_name), bf.LMKCDEY
+    keys = bf.keygen(ps, m, 19)
+    eng = {}
+    for kind in ("split", "wave", None):
+        if kind:
+            os.environ["FHE_HIP_LMK_KERNEL"] = kind
+        try:
+            e = bf.GateEngine(ps, m, device=0)
+        finally:
+            os.environ.pop("FHE_HIP_LMK_KERNEL", None)
+        e.load_keys(keys.bsk, keys.kskA, keys.kskB)
+        eng[kind or "default"] = e
+    P = eng["wave"].params
+    assert eng["split"].gate_kernel(4096) == "k_blind_rotate_lmk3" and eng["wave"].gate_kernel(1) == "k_blind_rotate_lmk"
+    assert eng["default"].gate_kernel(37) == "k_blind_rotate_lmk3"
+    rng = np.random.default_rng(5)
+    w = eng["wave"]
+    for count in (1, 5, 1027):
+        x1, x2 = rng.integers(0, 2, count), rng.integers(0, 2, count)
+        c1, d1 = bf.encrypt(ps, m, keys.sk, x1, 90 + count)
+        c2, d2 = bf.encrypt(ps, m, keys.sk, x2, 91 + count)
+        for gate in (bf.AND, bf.XOR, bf.NOR):
+            s = eng["split"].eval_gate(gate, c1, d1, c2, d2)
+            assert all(np.array_equal(u, v) for u, v in zip(s, w.eval_gate(gate, c1, d1, c2, d2))), (count, gate)
+            if count < 1000:
+                assert all(np.array_equal(u, v) for u, v in zip(eng["default"].eval_gate(gate, c1, d1, c2, d2), s))
+        if count == 5:
+            assert np.array_equal(bf.decrypt(ps, m, keys.sk, *s), (1 - (x1 | x2)).astype(np.int64))
+    for kind in ("split", "default"):
+        x = eng[kind]
+        for ctmod in sorted({P.q, 2 * P.N}):
+            cnt = 37
+            a = rng.integers(0, ctmod, (cnt, P.n), dtype=np.uint64)
+            b = rng.integers(0, ctmod, cnt, dtype=np.uint64)
+            f = rng.integers(0, 8, ctmod, dtype=np.uint64)
+            assert all(np.array_equal(u, v) for u, v in zip(x.bootstrap_func(a, b, ctmod, f, 8),
+                                                              w.bootstrap_func(a, b, ctmod, f, 8))), (kind, ctmod)
+            if ctmod == 2 * P.N:  # the LMKCDEY seam takes a_i mod 2N (rgsw-acc-lmkcdey.cpp:84-86)
+                acc = rng.integers(0, P.Q, (cnt, 2, P.N), dtype=np.uint64)
+                assert np.array_equal(x.blind_rotate_acc(a, ctmod, acc), w.blind_rotate_acc(a, ctmod, acc)), (kind, ctmod)
+        if P.q > P.N:  # EvalFunc's arbitrary functions need q <= N (binfhe-base-scheme.cpp:254)
+            continue
+        bits = rng.integers(0, 4, 13)
+        ca, cb = bf.encrypt(ps, m, keys.sk, bits, 77, p=8)
+        xs = np.arange(P.q) * 8 // P.q
+        luts = np.stack([((xs * k + 1) % 8) * (P.q // 8) for k in (1, 3, 5)]).astype(np.uint64)
+        assert all(np.array_equal(u, v) for u, v in zip(x.eval_func_multi(ca, cb, P.q, luts),
+                                                          w.eval_func_multi(ca, cb, P.q, luts)))
+    for e in eng.values():
+        e.close()
