@@ -118,11 +118,13 @@ def golden_check(name, lo, hi, total, ao, bo):
     return all(_sha(ao[s - lo:s - lo + S]) + _sha(bo[s - lo:s - lo + S]) == shards[s // S] for s in range(lo, hi, S))
 
 
-def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None):
+def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None, min_warm_s=0.0):
     """Times K steps of EvalBinGate(AND) over gates [lo, hi) of a `total`-gate batch on this
     rank; returns the per-rank measurements (elapsed is max-reduced by the caller).  golden: the
     tests/golden/full_<golden>.npz reference hashes the outputs are checked against (default: the
-    65,536-gate batch of the method)."""
+    65,536-gate batch of the method).  min_warm_s: the warmup also lasts at least this long (config 3's
+    4 ms steps: after the seconds of host-side setup the GPU clocks ramp up over its first ~25 ms,
+    tools/c3_ramp.py, profiles/r06_c3_ramp.txt)."""
     from fhe_amd.dist import barrier
     dev, stream, sp = ctx["dev"], ctx["stream"], ctx["stream"].cuda_stream
     ps, method = (bf.STD128, bf.GINX) if method_name == "ginx" else (bf.STD128_LMKCDEY, bf.LMKCDEY)
@@ -149,8 +151,12 @@ def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None):
         if ev:
             ev[2].record(stream)
 
-    for _ in range(args.warmup):
+    t_warm, n_warm = time.perf_counter(), 0
+    while n_warm < args.warmup or time.perf_counter() - t_warm < min_warm_s:
         step()
+        n_warm += 1
+        if min_warm_s:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     barrier()
@@ -171,6 +177,7 @@ def run_config(args, bf, torch, ctx, method_name, total, lo, hi, golden=None):
     kernel = eng.gate_kernel(B)   # the blind-rotation kernel this batch launched (fhe_hip_gate_kernel)
     eng.close()
     return {"elapsed": elapsed, "br_ms": br_ms, "ks_ms": ks_ms, "verified": verified, "exact": exact, "B": B,
+            "warmup_steps": n_warm,
             "keys": keys, "inputs": (a1[lo:hi], b1[lo:hi], a2[lo:hi], b2[lo:hi]), "out": (ao, bo), "ps": ps,
             "method": method, "kernel": kernel}
 
@@ -352,13 +359,14 @@ def main():
                 "hbm_per_gpu": per_gpu_hbm("lmkcdey", hi - lo, lmk_r["elapsed"] / args.steps),
             }
     if world == 1 and not args.no_config3 and args.method == "ginx":
-        c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden="std128_b1024")
+        c3 = run_config(args, bf, torch, ctx, "ginx", 1024, 0, 1024, golden="std128_b1024", min_warm_s=0.2)
         r3, v3 = rooflines("ginx", 1024, c3["br_ms"], c3["ks_ms"], c3["kernel"])
         alg3 = BSK_BYTES["ginx"] + KSK_BYTES["ginx"] + 1024 * (IN_BYTES_PER_GATE["ginx"] + OUT_BYTES_PER_GATE["ginx"])
         step_s = c3["elapsed"] / args.steps
         result["config3"] = {
             "config": "BASELINE config 3: STD128 GINX EvalBinGate(AND), 1024 gates, 1 GPU",
             "value": round(1024 / step_s, 1), "unit": "bootstraps/s", "ms_per_step": round(step_s * 1e3, 3),
+            "warmup_steps": c3["warmup_steps"], "warmup_rule": "max(W steps, 0.2 s): steady clocks (profiles/r06_c3_ramp.txt)",
             "verified": c3["verified"], "bit_exact_vs_reference": c3["exact"],
             "valu_roofline": v3, "blind_rotate_ms": r3["launch_ms"],
             "keyswitch_ms": r3["keyswitch_ms"],
