@@ -111,8 +111,9 @@ bool ginx2_supported(const GateArgs& g, const BootTables& t);
 // K1x: two waves per gate with K1w's one-word exchange (the small-batch GINX kernel), same support as K1s;
 // keys repacked from the resident layout into [i][c][q < 4][k2 < 8][64 lanes][4 words] (launch_repack_ginx2x)
 hipError_t launch_repack_ginx2x(const void* bsk, uint32_t n, void* bskx, hipStream_t s);
+// gw gates per workgroup: 1 (up to one gate per CU) or 2 (FHE_X_GATES)
 hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
-                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
+                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, int gw, hipStream_t s);
 // K1x's range: Q < 2^27, N = 1024, ciphertext modulus <= 2N (gates, BootstrapFunc tables, the seam's accumulators)
 bool ginx2x_supported(const GateArgs& g, const BootTables& t);
 // The same split kernel with three retained digits per component (digitsG = 4 at N = 1024, Q < 2^27:

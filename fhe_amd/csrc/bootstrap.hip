@@ -1991,7 +1991,7 @@ constexpr int kXTiles = FHE_X_TILES;
 // buffer of index i is the forward transform's second tile before it takes the partner's words, see below)
 constexpr int kXWave  = 3 * kG2Tile;
 constexpr int kXAcc   = 53;                            // |acc| < 5.3 Q between indices (units of Q/10)
-constexpr size_t x_lds() { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 2 * kXGates * kXWave) * 4; }
+constexpr size_t x_lds(int gw = kXGates) { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 2 * gw * kXWave) * 4; }
 static_assert(x_lds() <= 160 * 1024, "LDS per workgroup");
 static_assert(kXTiles == 1 || kXTiles == 2, "transpose tiles");
 }  // namespace
@@ -1999,8 +1999,17 @@ static_assert(kXTiles == 1 || kXTiles == 2, "transpose tiles");
 // MF: ciphertext modulus 2N (BootstrapFunc of EvalFunc's arbitrary functions, seam calls at 2N): any exponent, the
 // full-resolution table psi^e - 1 restricted to e in [0, 2N] (as K1s); ACCIO: the Backend::BlindRotate seam
 // (GateArgs::acc_io), as K1 / K1s.  Test-vector tables (g.tv, BootstrapFuncCore) are read as K1 reads them.
-template <bool MF, bool ACCIO>
-__global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
+// GW: gates per workgroup (kXGates; 1 for batches of up to one gate per CU, so that each gate has a CU to itself:
+// with two per workgroup a lone gate shares its CU with the spare waves that shadow it)
+template <bool MF, bool ACCIO, int GW = kXGates>
+#ifndef FHE_X_LB
+#define FHE_X_LB 0  // A/B: 1 = the launch bounds' minimum-blocks form for GW > 1 (round-6 first build)
+#endif
+#if FHE_X_LB
+__global__ void __launch_bounds__(128 * GW, GW >= 4 ? 1 : 2)
+#else
+__global__ void __launch_bounds__(128 * GW) __attribute__((amdgpu_waves_per_eu(GW >= 4 ? 1 : 2, GW >= 4 ? 1 : 2)))
+#endif
     k_blind_rotate_ginx2x(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
                           const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
                           const uint32_t* __restrict__ twAf) {
@@ -2019,7 +2028,7 @@ __global__ void __launch_bounds__(128 * kXGates, kXGates >= 4 ? 1 : 2)
 
     const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
     const int c = wave & 1;  // RLWE component of this wave
-    const uint32_t gslot = blockIdx.x * kXGates + (wave >> 1);
+    const uint32_t gslot = blockIdx.x * GW + (wave >> 1);
     const bool live = gslot < g.count;
     const uint32_t gate = live ? gslot : g.count - 1;  // spare waves shadow the last gate: every wave meets every barrier
     uint32_t* tile = s_wave + wave * kXWave;
@@ -2220,9 +2229,9 @@ bool ginx2x_supported(const GateArgs& g, const BootTables& t) {
 }
 
 hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
-                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, int gw, hipStream_t s) {
     if (g.count == 0) return hipSuccess;
-    if (!ginx2x_supported(g, t)) return hipErrorInvalidValue;
+    if (!ginx2x_supported(g, t) || gw < 1) return hipErrorInvalidValue;  // gw > 1: kXGates
     static const bool attr = [] {
         for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_ginx2x<false, false>),
                               reinterpret_cast<const void*>(&k_blind_rotate_ginx2x<true, false>),
@@ -2232,14 +2241,16 @@ hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, co
         return true;
     }();
     (void)attr;
-    const uint32_t blocks = (g.count + kXGates - 1) / kXGates;
-#define FHE_LAUNCH_X(MF_, IO)                                                                                       \
-    hipLaunchKernelGGL((k_blind_rotate_ginx2x<MF_, IO>), dim3(blocks), dim3(128 * kXGates), x_lds(), s, g, t,         \
-                       static_cast<const uint4*>(bskx), idx, tvb, ext_a, ext_b, t.twA_fwd)
+#define FHE_LAUNCH_X(MF_, IO, GW_)                                                                                  \
+    hipLaunchKernelGGL((k_blind_rotate_ginx2x<MF_, IO, GW_>), dim3((g.count + GW_ - 1) / GW_), dim3(128 * GW_),       \
+                       x_lds(GW_), s, g, t, static_cast<const uint4*>(bskx), idx, tvb, ext_a, ext_b, t.twA_fwd)
+#define FHE_LAUNCH_X2(MF_, IO) \
+    if (gw == 1) FHE_LAUNCH_X(MF_, IO, 1); else FHE_LAUNCH_X(MF_, IO, kXGates)
     const bool mf = g.ctmod == 2 * g.N;
-    if (g.acc_io) { if (mf) FHE_LAUNCH_X(true, true); else FHE_LAUNCH_X(false, true); }
-    else if (mf) FHE_LAUNCH_X(true, false);
-    else FHE_LAUNCH_X(false, false);
+    if (g.acc_io) { if (mf) { FHE_LAUNCH_X2(true, true); } else { FHE_LAUNCH_X2(false, true); } }
+    else if (mf) { FHE_LAUNCH_X2(true, false); }
+    else { FHE_LAUNCH_X2(false, false); }
+#undef FHE_LAUNCH_X2
 #undef FHE_LAUNCH_X
     return hipGetLastError();
 }

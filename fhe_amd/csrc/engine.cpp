@@ -1034,7 +1034,8 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         if (k == 2)
             FHE_HIP_CHECK(launch_blind_rotate_ginx2(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
         else if (k == 3)
-            FHE_HIP_CHECK(launch_blind_rotate_ginx2x(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+            FHE_HIP_CHECK(launch_blind_rotate_ginx2x(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_,
+                                                     2 * (size_t)g.count <= x_batch_ ? 1 : 2, s));
         else
             FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
     } else if (lmk_split(g)) {

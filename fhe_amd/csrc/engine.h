@@ -255,7 +255,8 @@ private:
     // K1x runs batches of up to x_batch_ gates: one two-gate workgroup per CU (2 x the CU count, 512 on
     // MI355X).  Measured (tools/gate_time.py, STD128 AND, profiles/r06_k1x_ab2.txt): 512 gates 2.69 vs 4.16 ms
     // (K1), 768 gates 4.28 vs 4.18, 1024 gates 4.56 vs 4.24: once two of its waves share a SIMD they overlap
-    // poorly, and the one-wave kernel wins
+    // poorly, and the one-wave kernel wins.  Up to x_batch_ / 2 gates each gate has its own 128-thread workgroup
+    // (a CU of its own: 1 gate 2.30 vs 2.64 ms, profiles/r06_k1x_lb_ab.txt); the LMKCDEY two-wave kernel likewise
     uint32_t x_batch_ = 512;
     // LMKCDEY kernel choice on the fast path: 0 by batch size, 1 the one-wave op-list kernel (K1 LMK), 2 two
     // waves per gate (K1m's two-digit form, k_blind_rotate_lmk3<2, ..>) -- FHE_HIP_LMK_KERNEL = wave | split
