@@ -116,6 +116,10 @@ hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, co
                                       const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, int gw, hipStream_t s);
 // K1x's range: Q < 2^27, N = 1024, ciphertext modulus <= 2N (gates, BootstrapFunc tables, the seam's accumulators)
 bool ginx2x_supported(const GateArgs& g, const BootTables& t);
+// K1q: four waves per gate (component x retained digit), one gate per 256-thread workgroup, K1x's keys and range:
+// the latency kernel for batches of up to one gate per CU
+hipError_t launch_blind_rotate_ginx4x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
+                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 // The same split kernel with three retained digits per component (digitsG = 4 at N = 1024, Q < 2^27:
 // STD128_3, STD128Q; with q = 2N: STD128_4, LPF_STD128, LPF_STD128Q) for the sets whose keys otherwise
 // live on the 64-bit accumulator: keys in the g2_key_word layout (nd = 3), u64 ctExt into that

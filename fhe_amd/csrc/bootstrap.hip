@@ -2256,6 +2256,202 @@ hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, co
 }
 
 // ---------------------------------------------------------------------------
+// K1q: GINX at N = 1024 with FOUR waves per gate (k_blind_rotate_ginx4x), the latency kernel for batches of up to
+// one gate per CU.  Wave (c, j) = wave c + 2 j owns component c (layout C, as K1x) and its retained digit j (row
+// 2 j + c).  Per index (AddToAccCGGI, rgsw-acc-cggi.cpp:102-151): the two waves of component c both inverse-
+// transform acc_c (the same values in both), wave (c, j) keeps digit j only and forward-transforms that one
+// polynomial, then multiplies it by the key columns of both components with the monomials: the word for its
+// own component (wave (c, 0) folds acc_c in) and the word for the other one go to its exchange planes; one
+// workgroup barrier; acc_c = own word + the sibling's (c, 1 - j) own-component word + both (1 - c, *) waves'
+// other-component words.  Both waves of a component add the same four words (in another order), so they hold
+// identical accumulators; only the order of the modular additions differs from K1, so the outputs are the same.
+// Per wave and index: one inverse and one forward transform and half of K1x's MAC.
+// Keys: K1x's layout (launch_repack_ginx2x); wave (c, j) reads q = 2 j + o of [i][c][q < 4][k2 < 8][64][4].
+// Bounds (Q < 2^27): |S+-| < (10 Q + 2^9) Q, so each word is below 2^32 Q 2 / 2^32 + 0.02 Q + Q / 2 < 2.52 Q (the
+// lo(S) x plain-monomial products dominate), + A / 32 for the word that folds acc in: A < 4 (2.52 Q) / (1 - 1/32)
+// < 10.5 Q between indices (the inverse plan's BIN; 16 Q of signed headroom).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kQWave = 5 * kG2Tile;  // words per wave: a transpose tile and [parity][o] exchange planes
+constexpr int kQAcc  = 105;          // |acc| < 10.5 Q between indices (units of Q/10)
+constexpr size_t q_lds() { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 4 * kQWave) * 4; }
+static_assert(q_lds() <= 160 * 1024, "LDS per workgroup");
+}  // namespace
+
+template <bool MF, bool ACCIO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+    k_blind_rotate_ginx4x(GateArgs g, BootTables T, const uint4* __restrict__ keys, const uint16_t* __restrict__ idx,
+                          const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
+                          const uint32_t* __restrict__ twAf) {
+    constexpr int ND = 2, kQ = 2 * ND;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_tab  = sm;
+    uint32_t* s_tabI = sm + 1024;
+    uint2* s_mono2   = reinterpret_cast<uint2*>(sm + 2048);
+    uint32_t* s_wave = sm + 2048 + 2 * kMonoHalfWords;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        s_tab[i]  = T.tabF[i];
+        s_tabI[i] = T.tabI[i];
+    }
+    for (int i = threadIdx.x; i < kMonoHalfWords; i += blockDim.x)
+        s_mono2[i] = MF ? make_uint2(T.monoP_full[i], T.mono_full[i]) : make_uint2(T.monoP[i], T.mono[i]);
+
+    const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int c = wave & 1, j = wave >> 1;  // component c, digit j
+    const uint32_t gate = blockIdx.x;
+    uint32_t* tile = s_wave + wave * kQWave;
+    uint32_t* xown = tile + kG2Tile;  // plane [p][o] at xown + (2 p + o) kG2Tile: this wave's word for component c ^ o
+    const uint32_t* xsib = s_wave + (wave ^ 2) * kQWave + kG2Tile + L;            // (c, 1 - j), o = 0
+    const uint32_t* xo0  = s_wave + (1 - c) * kQWave + 2 * kG2Tile + L;           // (1 - c, 0), o = 1
+    const uint32_t* xo1  = s_wave + (3 - c) * kQWave + 2 * kG2Tile + L;           // (1 - c, 1), o = 1
+    const Mod m0 = make_mod(T);
+    const Mod& m = m0;
+    __syncthreads();
+
+    // initial accumulator as K1x: acc1 = NTT(m) (both waves of component 1), acc0 = 0, or the seam's
+    uint32_t acc[16];
+    if (ACCIO && !g.acc_tv) {
+        acc_load_c(acc, g, gate, c, L, T.ninvR, m);
+    } else if (c == 1) {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
+        uint32_t tv[1][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            uint32_t v = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            tv[0][r] = v;
+        }
+        fwd_wave_s<1>(tv, tile, L, twAf, s_tab, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0;
+    }
+
+    const uint16_t* gidx = idx + (size_t)gate * g.n;
+    const DecN dec = make_decn(m.Q, g.gbits, ND);
+    const uint32_t lmul = 8 * (__builtin_bitreverse32((uint32_t)L) >> 26) + 1;
+    const uint4* kc = keys + (size_t)c * (kQ * 8 * 64) + (size_t)(2 * j) * (8 * 64) + L;
+    const uint32_t oneRj = j == 0 ? T.oneR : 0u;  // wave (c, 0) folds acc_c into its own-component word
+    for (uint32_t i = 0; i < g.n; ++i) {
+        const Mod m = fresh_nq(m0);
+        const uint32_t as = __builtin_amdgcn_readfirstlane((uint32_t)gidx[i]) >> (MF ? 0 : 1);
+        const uint4* kb = kc + (size_t)i * (2 * kQ * 8 * 64);
+        uint4 kq[2][2];
+#pragma unroll
+        for (int o = 0; o < 2; ++o) kq[0][o] = kb[(o * 8 + 0) * 64];
+        uint32_t d[ND][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
+        inv_wave_s<kQAcc, true>(d[0], tile, L, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+        uint32_t dj[1][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dj[0][r] = j ? d[1][r] : d[0][r];
+        fwd_wave_s<1>(dj, tile, L, twAf, s_tab, m);
+        uint32_t* xb = xown + (i & 1) * (2 * kG2Tile) + L;
+        const uint32_t fl = (as * lmul) & (MF ? 2047u : 1023u);
+        auto mono_r = [&](int r0, uint2& mp, uint2& mn) {
+            const uint32_t ur = __builtin_amdgcn_readfirstlane(
+                (as * (512u * (__builtin_bitreverse32((uint32_t)(r0 & 3)) >> 30) +
+                       2u * (__builtin_bitreverse32((uint32_t)(r0 >> 2)) >> 30))) & (MF ? 2047u : 1023u));
+            const uint32_t f  = MF ? (fl + ur) & 2047u : fl + ur;
+            const uint32_t fn = 2048u - f;
+            mp = s_mono2[f + (f >> 5)];
+            mn = s_mono2[fn + (fn >> 5)];
+        };
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) {
+            if (k2 + 1 < 8) {
+#pragma unroll
+                for (int o = 0; o < 2; ++o) kq[(k2 + 1) & 1][o] = kb[(o * 8 + k2 + 1) * 64];
+            }
+            asm volatile("" ::: "memory");
+            const int r0 = 2 * k2;
+            uint2 mp, mn;
+            mono_r(r0, mp, mn);
+            const uint4* q4 = kq[k2 & 1];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r = r0 + e;
+                if (MF && e == 1) mono_r(r, mp, mn);
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {  // o = 0: component c, 1: component 1 - c
+                    const uint4 kv = q4[o];
+                    const int64_t S1 = (int64_t)(int32_t)dj[0][r] * (int32_t)(e ? kv.y : kv.x);
+                    const int64_t S2 = (int64_t)(int32_t)dj[0][r] * (int32_t)(e ? kv.w : kv.z);
+                    int64_t S = (int64_t)((uint64_t)(uint32_t)S1 * mp.x) + (int64_t)(int32_t)(S1 >> 32) * (int32_t)mp.y;
+                    S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
+                    if (o == 0) S += (int64_t)(int32_t)acc[r] * (int32_t)oneRj;
+                    const uint32_t w = smont_red(S, m);
+                    xb[o * kG2Tile + (r << 6)] = w;
+                    if (o == 0) acc[r] = w;
+                }
+            }
+        }
+        // every wave's words are in LDS (plane parity i & 1 is written again at index i + 2, after the other
+        // waves have passed the barrier of index i + 1, i.e. after they read it)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const uint32_t po = (i & 1) * (2 * kG2Tile);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)] + xo0[po + (r << 6)] + xo1[po + (r << 6)];
+    }
+
+    if (ACCIO) {
+        if (j == 0) acc_store_c(acc, g, gate, c, L, T.nR, m);
+        return;
+    }
+    if (j != 0) return;  // the digit-1 waves hold the same accumulators
+    inv_wave_s<kQAcc, true>(acc, tile, L, s_tabI, T.w1R, m.oneR, m);
+    if (c == 0) {
+        uint32_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            const uint32_t v = acc[r];
+            const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
+            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+        }
+    } else if (L == 0) {
+        const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
+        ext_b[gate] = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+hipError_t launch_blind_rotate_ginx4x(const GateArgs& g, const BootTables& t, const void* bskx, const uint16_t* idx,
+                                      const uint32_t* tvb, uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!ginx2x_supported(g, t)) return hipErrorInvalidValue;
+    static const bool attr = [] {
+        for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_ginx4x<false, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx4x<true, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx4x<false, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_ginx4x<true, true>)})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)q_lds());
+        return true;
+    }();
+    (void)attr;
+#define FHE_LAUNCH_Q(MF_, IO)                                                                                       \
+    hipLaunchKernelGGL((k_blind_rotate_ginx4x<MF_, IO>), dim3(g.count), dim3(256), q_lds(), s, g, t,                 \
+                       static_cast<const uint4*>(bskx), idx, tvb, ext_a, ext_b, t.twA_fwd)
+    const bool mf = g.ctmod == 2 * g.N;
+    if (g.acc_io) { if (mf) FHE_LAUNCH_Q(true, true); else FHE_LAUNCH_Q(false, true); }
+    else if (mf) FHE_LAUNCH_Q(true, false);
+    else FHE_LAUNCH_Q(false, false);
+#undef FHE_LAUNCH_Q
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // LMKCDEY on the split layout: k_blind_rotate_lmk3 (RingGSWAccumulatorLMKCDEY::EvalAcc,
 // rgsw-acc-lmkcdey.cpp:70-287) for the digitsG = 4 sets at N = 1024, Q < 2^27 (STD128_4_LMKCDEY,
 // STD128Q_3_LMKCDEY, LPF_STD128Q_LMKCDEY), which otherwise run K5's op-list form.  One gate per

@@ -97,8 +97,11 @@ uint32_t Engine::kernel() const {
 int Engine::ginx_choice(const GateArgs& g) const {
     if (!d_bsk2_) return 1;
     if (ginx_kernel_ == 2) return ginx2_supported(g, tabs_) ? 2 : 1;
-    // K1x: gates, BootstrapFunc tables and the seam's accumulators, ciphertext modulus q or 2N
-    if (ginx2x_supported(g, tabs_) && (ginx_kernel_ == 3 || (ginx_kernel_ == 0 && g.count <= x_batch_))) return 3;
+    // K1x: gates, BootstrapFunc tables and the seam's accumulators, ciphertext modulus q or 2N; K1q (four waves
+    // per gate) up to one gate per CU
+    if (!ginx2x_supported(g, tabs_)) return 1;
+    if (ginx_kernel_ == 4 || (ginx_kernel_ == 0 && 2 * (size_t)g.count <= x_batch_)) return 4;
+    if (ginx_kernel_ == 3 || (ginx_kernel_ == 0 && g.count <= x_batch_)) return 3;
     return 1;
 }
 
@@ -121,7 +124,8 @@ const char* Engine::gate_kernel(size_t count) const {
     }
     if (p_.method != M_GINX) return lmk_split(g) ? "k_blind_rotate_lmk3" : "k_blind_rotate_lmk";
     const int k = ginx_choice(g);
-    return k == 2 ? "k_blind_rotate_ginx2" : k == 3 ? "k_blind_rotate_ginx2x" : "k_blind_rotate_ginx";
+    return k == 2 ? "k_blind_rotate_ginx2" : k == 3 ? "k_blind_rotate_ginx2x" : k == 4 ? "k_blind_rotate_ginx4x"
+                                                                                  : "k_blind_rotate_ginx";
 }
 
 bool Engine::ks32_set(const Params& p) {
@@ -370,7 +374,7 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     // batch size (K1x below kXBatch gates, K1 above)
     if (const char* k = std::getenv("FHE_HIP_GINX_KERNEL")) {
         const std::string v(k);
-        ginx_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : v == "xsplit" ? 3 : 0;
+        ginx_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : v == "xsplit" ? 3 : v == "qsplit" ? 4 : 0;
     }
     if (const char* k = std::getenv("FHE_HIP_LMK_KERNEL")) {
         const std::string v(k);
@@ -1033,6 +1037,8 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
         const int k = ginx_choice(g);
         if (k == 2)
             FHE_HIP_CHECK(launch_blind_rotate_ginx2(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
+        else if (k == 4)
+            FHE_HIP_CHECK(launch_blind_rotate_ginx4x(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
         else if (k == 3)
             FHE_HIP_CHECK(launch_blind_rotate_ginx2x(g, tabs_, d_bsk2_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_,
                                                      2 * (size_t)g.count <= x_batch_ ? 1 : 2, s));

@@ -250,7 +250,8 @@ private:
     // every batch size (1024 gates 4.87 vs 4.37 ms: two barriers per index, the partner's digits read in
     // the MAC) and only FHE_HIP_GINX_KERNEL=split pins it; K1x runs batches of up to kXBatch gates.
     int ginx_kernel_ = 0;
-    // GINX kernel of a gate launch (ginx_kernel_ pins, else by batch size): 1 K1, 2 K1s, 3 K1x
+    // GINX kernel of a gate launch (ginx_kernel_ pins, else by batch size): 1 K1, 2 K1s, 3 K1x, 4 K1q (four waves
+    // per gate, up to one gate per CU; FHE_HIP_GINX_KERNEL=qsplit pins it)
     int ginx_choice(const GateArgs& g) const;
     // K1x runs batches of up to x_batch_ gates: one two-gate workgroup per CU (2 x the CU count, 512 on
     // MI355X).  Measured (tools/gate_time.py, STD128 AND, profiles/r06_k1x_ab2.txt): 512 gates 2.69 vs 4.16 ms

@@ -179,20 +179,27 @@ def test_gpu_copy_keys_refuses_contexts_of_other_kernel_layouts(ps, m, knob, val
 
 @pytest.mark.gpu
 def test_gpu_gate_kernel_reports_the_launched_kernel(monkeypatch):
-    """fhe_hip_gate_kernel: the STD128 GINX context runs K1x (k_blind_rotate_ginx2x) up to two gates per CU and
-    K1 above; FHE_HIP_GINX_KERNEL pins it; LMKCDEY runs its op-list kernel"""
+    """fhe_hip_gate_kernel: the STD128 GINX context runs K1q (k_blind_rotate_ginx4x, four waves per gate) up to one
+    gate per CU, K1x (k_blind_rotate_ginx2x) up to two and K1 above; FHE_HIP_GINX_KERNEL pins it; LMKCDEY runs
+    K1m's two-digit form (k_blind_rotate_lmk3) up to two gates per CU and its op-list kernel above"""
     from fhe_amd import binfhe as bf
     keys = bf.keygen(bf.STD128, bf.GINX, 5)
     e = bf.GateEngine(bf.STD128, bf.GINX, 0)
     e.load_keys(keys.bsk, keys.kskA, keys.kskB)
-    assert e.gate_kernel(1) == "k_blind_rotate_ginx2x" and e.gate_kernel(65536) == "k_blind_rotate_ginx"
-    lo, hi = 1, 65536                      # the switch-over: two gates per CU (512 on 256 CUs)
-    while hi - lo > 1:
-        mid = (lo + hi) // 2
-        lo, hi = (mid, hi) if e.gate_kernel(mid) == "k_blind_rotate_ginx2x" else (lo, mid)
-    assert lo % 2 == 0 and 128 <= lo <= 1024, lo
+    assert e.gate_kernel(1) == "k_blind_rotate_ginx4x" and e.gate_kernel(65536) == "k_blind_rotate_ginx"
+
+    def switch(k, kernels):  # the last count launching one of `kernels`
+        lo, hi = 1, 65536
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            lo, hi = (mid, hi) if k.gate_kernel(mid) in kernels else (lo, mid)
+        return lo
+    q = switch(e, ("k_blind_rotate_ginx4x",))
+    x = switch(e, ("k_blind_rotate_ginx4x", "k_blind_rotate_ginx2x"))
+    assert 64 <= q <= 512 and x == 2 * q and e.gate_kernel(q + 1) == "k_blind_rotate_ginx2x", (q, x)   # CUs, 2 x CUs
     assert e.kernel() == 1
-    for val, name in (("wave", "k_blind_rotate_ginx"), ("split", "k_blind_rotate_ginx2"), ("xsplit", "k_blind_rotate_ginx2x")):
+    for val, name in (("wave", "k_blind_rotate_ginx"), ("split", "k_blind_rotate_ginx2"), ("xsplit", "k_blind_rotate_ginx2x"),
+                      ("qsplit", "k_blind_rotate_ginx4x")):
         monkeypatch.setenv("FHE_HIP_GINX_KERNEL", val)
         p = bf.GateEngine(bf.STD128, bf.GINX, 0)
         p.load_keys(keys.bsk, keys.kskA, keys.kskB)
@@ -202,6 +209,7 @@ def test_gpu_gate_kernel_reports_the_launched_kernel(monkeypatch):
     lk = bf.keygen(bf.STD128_LMKCDEY, bf.LMKCDEY, 5)
     l = bf.GateEngine(bf.STD128_LMKCDEY, bf.LMKCDEY, 0)
     l.load_keys(lk.bsk, lk.kskA, lk.kskB)
-    assert l.gate_kernel(1024) == "k_blind_rotate_lmk"
+    assert l.gate_kernel(1024) == "k_blind_rotate_lmk" and l.gate_kernel(1) == "k_blind_rotate_lmk3"
+    assert switch(l, ("k_blind_rotate_lmk3",)) == x
     for x in (e, l):
         x.close()

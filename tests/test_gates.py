@@ -315,11 +315,12 @@ def test_gpu_multi_engine_shards_match_single():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["split", "xsplit"])
+@pytest.mark.parametrize("kind", ["split", "xsplit", "qsplit"])
 def test_gpu_split_ginx_kernel_bit_exact(kind):
-    """the two-wave GINX kernels pinned by FHE_HIP_GINX_KERNEL -- split: k_blind_rotate_ginx2 (digit exchange),
-    xsplit: k_blind_rotate_ginx2x (K1x, one reduced word per slot exchanged) -- == the reference goldens and
-    == the one-wave kernel on ragged batches (1027 gates: K1x's last workgroup holds one live gate)"""
+    """the multi-wave GINX kernels pinned by FHE_HIP_GINX_KERNEL -- split: k_blind_rotate_ginx2 (digit exchange),
+    xsplit: k_blind_rotate_ginx2x (K1x, one reduced word per slot exchanged), qsplit: k_blind_rotate_ginx4x (K1q,
+    four waves per gate) -- == the reference goldens and == the one-wave kernel on ragged batches (1027 gates: K1x's
+    last workgroup holds one live gate)"""
     import os
     from fhe_amd import binfhe as bf
     g, keys, (a1, b1, a2, b2) = fixture("std128")
@@ -350,17 +351,17 @@ def test_gpu_split_ginx_kernel_bit_exact(kind):
 
 @pytest.mark.gpu
 def test_gpu_k1x_bootstrap_func_and_seam_match_one_wave_kernel():
-    """K1x (FHE_HIP_GINX_KERNEL=xsplit) beyond gates: BootstrapFunc with test-vector tables at ciphertext modulus q
-    and 2N (the full-resolution monomials: odd exponents), EvalFuncMultiOutput's per-gate tables (tv_mod), and the
-    seam's BlindRotate on arbitrary accumulators at moduli q and 2N == the one-wave kernel K1 on the same inputs
-    (K1 is pinned to the reference by tests/test_fb.py and tests/test_backend.py); the default context runs K1x on
-    these small batches and reproduces K1 too"""
+    """K1x (FHE_HIP_GINX_KERNEL=xsplit) and K1q (qsplit) beyond gates: BootstrapFunc with test-vector tables at
+    ciphertext modulus q and 2N (the full-resolution monomials: odd exponents), EvalFuncMultiOutput's per-gate tables
+    (tv_mod), and the seam's BlindRotate on arbitrary accumulators at moduli q and 2N == the one-wave kernel K1 on
+    the same inputs (K1 is pinned to the reference by tests/test_fb.py and tests/test_backend.py); the default
+    context runs K1q on these small batches and reproduces K1 too"""
     import os
     from fhe_amd import binfhe as bf
     ps, m = bf.STD128, bf.GINX
     keys = bf.keygen(ps, m, 9)
     eng = {}
-    for kind in ("xsplit", "wave", None):
+    for kind in ("xsplit", "qsplit", "wave", None):
         if kind:
             os.environ["FHE_HIP_GINX_KERNEL"] = kind
         try:
@@ -371,7 +372,7 @@ def test_gpu_k1x_bootstrap_func_and_seam_match_one_wave_kernel():
         eng[kind or "default"] = e
     P = eng["wave"].params
     rng = np.random.default_rng(123)
-    for kind in ("xsplit", "default"):
+    for kind in ("xsplit", "qsplit", "default"):
         x, w = eng[kind], eng["wave"]
         for ctmod in (P.q, 2 * P.N):
             cnt = 37
@@ -388,7 +389,7 @@ def test_gpu_k1x_bootstrap_func_and_seam_match_one_wave_kernel():
         luts = np.stack([((xs * k + 1) % 8) * (P.q // 8) for k in (1, 3, 5)]).astype(np.uint64)
         assert all(np.array_equal(u, v) for u, v in zip(x.eval_func_multi(ca, cb, P.q, luts),
                                                           w.eval_func_multi(ca, cb, P.q, luts)))
-        assert x.gate_kernel(37) == "k_blind_rotate_ginx2x"
+        assert x.gate_kernel(37) == ("k_blind_rotate_ginx2x" if kind == "xsplit" else "k_blind_rotate_ginx4x")
     for e in eng.values():
         e.close()
 
