@@ -143,6 +143,11 @@ hipError_t launch_blind_rotate_lmkx(const GateArgs& g, const BootTables& t, cons
                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
                                     uint32_t* ext_a, uint32_t* ext_b, int gw, hipStream_t s);
 bool lmkx_supported(const GateArgs& g, const BootTables& t);
+// K1m-4: four waves per gate (component x retained digit), one gate per 256-thread workgroup, the same keys
+// (launch_repack_lmkx) and range: the LMKCDEY latency kernel for batches of up to one gate per CU
+hipError_t launch_blind_rotate_lmk4x(const GateArgs& g, const BootTables& t, const void* ekx, uint32_t n,
+                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                     uint32_t* ext_a, uint32_t* ext_b, hipStream_t s);
 // split-kernel key layout, per index i (8192 nd words): [c][p < 2 nd][k2 < 8][64 lanes][4 words]
 // = (K+[r], K+[r+1], K-[r], K-[r+1]) of component c, digit row g2_row(c, p, nd), r = 2 k2, EVAL slot
 // x(L, r) = ((r >> 2) << 8) | (L << 2) | (r & 3): wave c multiplies (own digits D_c, D_{2+c}, ..,

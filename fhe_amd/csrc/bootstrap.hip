@@ -2779,6 +2779,227 @@ hipError_t launch_blind_rotate_lmkx(const GateArgs& g, const BootTables& t, cons
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// K1m-4: LMKCDEY with FOUR waves per gate (k_blind_rotate_lmk4x), the latency kernel of the digitsG = 3 sets for
+// batches of up to one gate per CU (K1q's split applied to the op list).  Wave (c, j) = wave c + 2 j owns component
+// c (layout C) and retained digit j (row 2 j + c); one gate per 256-thread workgroup.  Per op of k_prep_lmk_w:
+//   EXT(i)  (AddToAccLMKCDEY, rgsw-acc-lmkcdey.cpp:228-254): both waves of component c inverse-transform acc_c (the
+//           same values), wave (c, j) forward-transforms digit j and multiplies it by ek[i][row 2 j + c] in both
+//           columns: the column-c word and the column-(1 - c) word go to its exchange planes; one barrier;
+//           acc_c = its column-c word + the sibling's + both (1 - c, *) waves' column-c words (acc replaced);
+//   AUTO(t) (Automorphism, :257-287): every wave permutes its copy of acc_c; the component-0 waves transform
+//           acc0' and multiply digit j by ak[t][row j] in both columns while the component-1 waves reduce
+//           acc1' (one signed Montgomery product by 2^32 mod Q); one barrier; acc0 = the two column-0 words,
+//           acc1 = acc1' + the two column-1 words.
+// Keys: K1m's two-digit layout (k_repack_lmkx): row 2 j + c of column c at ek[i][c][p = j], of column 1 - c at
+// ek[i][1 - c][p = 2 + j]; ak[t][c'][d = j] for column c'.
+// Bounds: a word is one digit x key product reduced, < 6.67 Q^2 / 2^32 + Q/2 < 0.92 Q (Q < 2^28; < 0.68 Q for
+// Q < 2^27), so acc < 3.7 Q after EXT and < 2.4 Q after AUTO (BIN 37; signed headroom 8 Q or 16 Q).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kMWave = 5 * kG2Tile;  // words per wave: a transpose tile and [parity][o] exchange planes
+constexpr int kMAcc  = 37;           // |acc| < 3.7 Q between ops (units of Q/10)
+constexpr size_t m4_lds() { return (size_t)(1024 + 1024 + 4 * kMWave) * 4; }
+static_assert(m4_lds() <= 160 * 1024, "LDS per workgroup");
+}  // namespace
+
+template <bool LZ, bool ACCIO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+    k_blind_rotate_lmk4x(GateArgs g, BootTables T, const uint4* __restrict__ ek, const uint4* __restrict__ ak,
+                         const uint16_t* __restrict__ ops, const uint32_t* __restrict__ nops, uint32_t maxops,
+                         const uint32_t* __restrict__ tvb, uint32_t* __restrict__ ext_a, uint32_t* __restrict__ ext_b,
+                         const uint32_t* __restrict__ twAf) {
+    constexpr int ND = 2;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint32_t* s_tab  = sm;
+    uint32_t* s_tabI = sm + 1024;
+    uint32_t* s_wave = sm + 2048;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        s_tab[i]  = T.tabF[i];
+        s_tabI[i] = T.tabI[i];
+    }
+    const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int c = wave & 1, j = wave >> 1;  // component c, digit j
+    const uint32_t gate = blockIdx.x;
+    uint32_t* tile = s_wave + wave * kMWave;
+    uint32_t* xown = tile + kG2Tile + L;  // plane [p][o] at + (2 p + o) kG2Tile: this wave's word for column c ^ o
+    const uint32_t* xsib = s_wave + (wave ^ 2) * kMWave + kG2Tile + L;   // (c, 1 - j), o = 0
+    const uint32_t* xo0  = s_wave + (1 - c) * kMWave + 2 * kG2Tile + L;  // (1 - c, 0), o = 1
+    const uint32_t* xo1  = s_wave + (3 - c) * kMWave + 2 * kG2Tile + L;  // (1 - c, 1), o = 1
+    const Mod m0 = make_mod(T);
+    const Mod& m = m0;
+    const uint32_t M = 2 * g.N;
+    __syncthreads();
+    auto barrier = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
+
+    // BootstrapGateCore (binfhe-base-scheme.cpp:556-575) / BootstrapFuncCore's table: acc1 = NTT(m) in both
+    // component-1 waves, acc0 = 0; then acc1 <- acc1(X^(2N-5)) (:99)
+    uint32_t acc[16];
+    if (ACCIO && !g.acc_tv) {
+        acc_load_c(acc, g, gate, c, L, T.ninvR, m);
+        if (c == 1) automorphism_c(acc, tile, L, M - 5);
+    } else if (c == 1) {
+        const uint32_t b = tvb[gate], cm = g.ctmod - 1;
+        const uint32_t tvo = g.tv_mod > 1 ? (gate % g.tv_mod) * g.ctmod : 0u;
+        uint32_t tv[1][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            uint32_t v = 0;
+            if (x % g.factor == 0) {
+                const uint32_t bx = (b - x / g.factor) & cm;
+                v = g.tv ? g.tv[tvo + bx] : (bx >= g.lb && bx < g.ub) ? g.lv : g.uv;
+            }
+            if (!LZ) v = v > (m.Q >> 1) ? v - m.Q : v;  // centred: |v| <= Q/2 (8 Q headroom)
+            tv[0][r] = v;
+        }
+        fwd_wave_s<1>(tv, tile, L, twAf, s_tab, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = smont_mul(tv[0][r], T.ninvR, m);
+        automorphism_c(acc, tile, L, M - 5);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0;
+    }
+
+    const DecN dec = make_decn(m.Q, g.gbits, ND);
+    const uint16_t* gops = ops + (size_t)gate * maxops;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(nops[gate]);
+    // digit j of acc (COEF, canonical) forward-transformed to EVAL
+    auto digit = [&](uint32_t (&dj)[1][16], const Mod& m) {
+        uint32_t d[ND][16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) d[0][r] = acc[r];
+        inv_wave_s<kMAcc, LZ>(d[0], tile, L, s_tabI, T.w1R, m.oneR, m);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) decompose_n<ND>(d[0][r], dec, d, r);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dj[0][r] = j ? d[1][r] : d[0][r];
+        fwd_wave_s<1>(dj, tile, L, twAf, s_tab, m);
+    };
+    // the words of digit j against the key columns k0 (column c, or 0) and k1 (the other, or 1), to plane parity p
+    auto words = [&](const uint32_t (&dj)[1][16], const uint4* k0, const uint4* k1, uint32_t* xb, const Mod& m) {
+        uint4 kq[2][2];
+        kq[0][0] = k0[0];
+        kq[0][1] = k1[0];
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            if (k4 + 1 < 4) {
+                kq[(k4 + 1) & 1][0] = k0[(k4 + 1) * 64];
+                kq[(k4 + 1) & 1][1] = k1[(k4 + 1) * 64];
+            }
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * k4 + e;
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    const uint4 q = kq[k4 & 1][o];
+                    const uint32_t kv = e == 0 ? q.x : e == 1 ? q.y : e == 2 ? q.z : q.w;
+                    const uint32_t w = smont_red((int64_t)(int32_t)dj[0][r] * (int32_t)kv, m);
+                    xb[o * kG2Tile + (r << 6)] = w;
+                    if (o == 0) acc[r] = w;
+                }
+            }
+        }
+    };
+    for (uint32_t it = 0; it < cnt; ++it) {
+        const Mod m = fresh_nq(m0);
+        const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
+        const uint32_t po = (it & 1) * (2 * kG2Tile);
+        uint32_t* xb = xown + po;
+        uint32_t dj[1][16];
+        if (!(op & 0x8000u)) {
+            // ---- AddToAccLMKCDEY: acc_c <- sum over the four digits D ek[op][row][c]   (acc replaced)
+            digit(dj, m);
+            words(dj, ek + ((size_t)op * 2 + c) * (4 * 4 * 64) + (size_t)j * (4 * 64) + L,
+                  ek + ((size_t)op * 2 + (1 - c)) * (4 * 4 * 64) + (size_t)(2 + j) * (4 * 64) + L, xb, m);
+            barrier();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)] + xo0[po + (r << 6)] + xo1[po + (r << 6)];
+        } else {
+            // ---- Automorphism(5^t or 2N-5, ak[t])
+            const uint32_t t = op & 0x7fffu;
+            uint32_t kexp = M - 5;
+            if (t) {
+                kexp = 1;
+                for (uint32_t z = 0; z < t; ++z) kexp = (kexp * 5) & (M - 1);
+            }
+            automorphism_c(acc, tile, L, kexp);
+            if (c == 0) {  // acc0' -> digit j -> the column-0 and column-1 words
+                digit(dj, m);
+                words(dj, ak + ((size_t)t * 2 + 0) * (ND * 4 * 64) + (size_t)j * (4 * 64) + L,
+                      ak + ((size_t)t * 2 + 1) * (ND * 4 * 64) + (size_t)j * (4 * 64) + L, xb, m);
+            } else {       // acc1' reduced while component 0 transforms
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = smont_mul(acc[r], m.oneR, m);
+            }
+            barrier();
+            if (c == 0) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)];
+            } else {
+                const uint32_t* w0 = s_wave + 0 * kMWave + 2 * kG2Tile + L + po;  // (0, 0), o = 1
+                const uint32_t* w1 = s_wave + 2 * kMWave + 2 * kG2Tile + L + po;  // (0, 1), o = 1
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] += w0[r << 6] + w1[r << 6];
+            }
+        }
+    }
+
+    if (ACCIO) {
+        if (j == 0) acc_store_c(acc, g, gate, c, L, T.nR, m);
+        return;
+    }
+    if (j != 0) return;  // the digit-1 waves hold the same accumulators
+    // extraction (binfhe-base-scheme.cpp:110-121), as k_blind_rotate_lmk3
+    inv_wave_s<kMAcc, LZ>(acc, tile, L, s_tabI, T.w1R, m.oneR, m);
+    if (c == 0) {
+        uint32_t* oa = ext_a + (size_t)gate * g.N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t x = ((uint32_t)r << 6) | (uint32_t)L;
+            const uint32_t v = acc[r];
+            const uint32_t o = (x == 0 || v == 0) ? v : m.Q - v;
+            oa[(g.N - x) & (g.N - 1)] = g.msb_out ? mod_switch(o, m.Q, g.qKS) : o;
+        }
+    } else if (L == 0) {
+        const uint32_t bb = add_mod(g.b_const, acc[0], m.Q);
+        ext_b[gate] = g.msb_out ? mod_switch(bb, m.Q, g.qKS) : bb;
+    }
+}
+
+hipError_t launch_blind_rotate_lmk4x(const GateArgs& g, const BootTables& t, const void* ekx, uint32_t n,
+                                     const uint16_t* ops, const uint32_t* nops, uint32_t maxops, const uint32_t* tvb,
+                                     uint32_t* ext_a, uint32_t* ext_b, hipStream_t s) {
+    if (g.count == 0) return hipSuccess;
+    if (!lmkx_supported(g, t)) return hipErrorInvalidValue;
+    static const bool attr = [] {
+        for (const void* k : {reinterpret_cast<const void*>(&k_blind_rotate_lmk4x<false, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_lmk4x<true, false>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_lmk4x<false, true>),
+                              reinterpret_cast<const void*>(&k_blind_rotate_lmk4x<true, true>)})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m4_lds());
+        return true;
+    }();
+    (void)attr;
+    const uint4* ek = static_cast<const uint4*>(ekx);
+    const uint4* ak = ek + (size_t)n * 2048;
+#define FHE_LAUNCH_M4(LZ_, IO)                                                                                     \
+    hipLaunchKernelGGL((k_blind_rotate_lmk4x<LZ_, IO>), dim3(g.count), dim3(256), m4_lds(), s, g, t, ek, ak, ops,  \
+                       nops, maxops, tvb, ext_a, ext_b, t.twA_fwd)
+    const bool lz = t.Q < (1u << 27);
+    if (g.acc_io) { if (lz) FHE_LAUNCH_M4(true, true); else FHE_LAUNCH_M4(false, true); }
+    else if (lz) FHE_LAUNCH_M4(true, false);
+    else FHE_LAUNCH_M4(false, false);
+#undef FHE_LAUNCH_M4
+    return hipGetLastError();
+}
+
 // ===========================================================================
 // K1w: GINX at N = 2048 with the accumulator in registers (k_blind_rotate_n2k<ND, ACCIO>) for the
 // Q < 2^27 rows with even monomial exponents (ciphertext modulus q < 2N): STD256Q (digitsG = 4,

@@ -105,9 +105,10 @@ int Engine::ginx_choice(const GateArgs& g) const {
     return 1;
 }
 
-bool Engine::lmk_split(const GateArgs& g) const {
-    if (p_.method != M_LMKCDEY || wide_ || !d_bsk2_ || lmk_kernel_ == 1 || !lmkx_supported(g, tabs_)) return false;
-    return lmk_kernel_ == 2 || g.count <= x_batch_;
+int Engine::lmk_choice(const GateArgs& g) const {
+    if (p_.method != M_LMKCDEY || wide_ || !d_bsk2_ || lmk_kernel_ == 1 || !lmkx_supported(g, tabs_)) return 1;
+    if (lmk_kernel_ == 4 || (lmk_kernel_ == 0 && 2 * (size_t)g.count <= x_batch_)) return 4;
+    return lmk_kernel_ == 2 || g.count <= x_batch_ ? 2 : 1;
 }
 
 const char* Engine::gate_kernel(size_t count) const {
@@ -122,7 +123,10 @@ const char* Engine::gate_kernel(size_t count) const {
         if (g3_ && ginx3_supported(g, tabs_)) return "k_blind_rotate_ginx2";
         return "k_blind_rotate_wide";
     }
-    if (p_.method != M_GINX) return lmk_split(g) ? "k_blind_rotate_lmk3" : "k_blind_rotate_lmk";
+    if (p_.method != M_GINX) {
+        const int k = lmk_choice(g);
+        return k == 4 ? "k_blind_rotate_lmk4x" : k == 2 ? "k_blind_rotate_lmk3" : "k_blind_rotate_lmk";
+    }
     const int k = ginx_choice(g);
     return k == 2 ? "k_blind_rotate_ginx2" : k == 3 ? "k_blind_rotate_ginx2x" : k == 4 ? "k_blind_rotate_ginx4x"
                                                                                   : "k_blind_rotate_ginx";
@@ -378,7 +382,7 @@ Engine::Engine(int paramset, int method, int device) : p_(make_params(paramset, 
     }
     if (const char* k = std::getenv("FHE_HIP_LMK_KERNEL")) {
         const std::string v(k);
-        lmk_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : 0;
+        lmk_kernel_ = v == "split" ? 2 : v == "wave" ? 1 : v == "qsplit" ? 4 : 0;
     }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
@@ -1044,7 +1048,11 @@ void Engine::rotate_device(const GateArgs& g, hipStream_t s) {
                                                      2 * (size_t)g.count <= x_batch_ ? 1 : 2, s));
         else
             FHE_HIP_CHECK(launch_blind_rotate_ginx(g, tabs_, d_bsk_, d_idx_, d_tvb_, d_ext_a_, d_ext_b_, s));
-    } else if (lmk_split(g)) {
+    } else if (lmk_choice(g) == 4) {
+        // four waves per gate up to one gate per CU (K1m-4, as K1q for GINX)
+        FHE_HIP_CHECK(launch_blind_rotate_lmk4x(g, tabs_, d_bsk2_, p_.n, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,
+                                                d_ext_b_, s));
+    } else if (lmk_choice(g) == 2) {
         // two waves per gate up to x_batch_ gates (as K1x for GINX): one gate per 128-thread workgroup up to one
         // per CU, two per 256-thread workgroup above (bootstrap.hip k_blind_rotate_lmk3's GW)
         FHE_HIP_CHECK(launch_blind_rotate_lmkx(g, tabs_, d_bsk2_, p_.n, d_ops_, d_nops_, maxops_, d_tvb_, d_ext_a_,

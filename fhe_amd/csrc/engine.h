@@ -260,10 +260,11 @@ private:
     // (a CU of its own: 1 gate 2.30 vs 2.64 ms, profiles/r06_k1x_lb_ab.txt); the LMKCDEY two-wave kernel likewise
     uint32_t x_batch_ = 512;
     // LMKCDEY kernel choice on the fast path: 0 by batch size, 1 the one-wave op-list kernel (K1 LMK), 2 two
-    // waves per gate (K1m's two-digit form, k_blind_rotate_lmk3<2, ..>) -- FHE_HIP_LMK_KERNEL = wave | split
+    // waves per gate (K1m's two-digit form, k_blind_rotate_lmk3<2, ..>), 4 four waves per gate (K1m-4,
+    // k_blind_rotate_lmk4x) -- FHE_HIP_LMK_KERNEL = wave | split | qsplit
     int lmk_kernel_ = 0;
-    // true: this LMKCDEY launch runs on K1m's two-digit form (lmk_kernel_ pins, else up to x_batch_ gates)
-    bool lmk_split(const GateArgs& g) const;
+    // the kernel of this LMKCDEY launch: 1, 2 (up to x_batch_ gates) or 4 (up to x_batch_ / 2); lmk_kernel_ pins
+    int lmk_choice(const GateArgs& g) const;
     void* d_bsk2_ = nullptr;   // K1s / K1x / K1m-2 key layout (g3_: K1s's nd = 3 layout; n2k_: K1w's)
     void repack_ginx2();
     // digitsG = 4 GINX sets at N = 1024, Q < 2^27 (STD128_3, STD128Q, STD128_4, LPF_STD128, LPF_STD128Q):

@@ -181,7 +181,8 @@ def test_gpu_copy_keys_refuses_contexts_of_other_kernel_layouts(ps, m, knob, val
 def test_gpu_gate_kernel_reports_the_launched_kernel(monkeypatch):
     """fhe_hip_gate_kernel: the STD128 GINX context runs K1q (k_blind_rotate_ginx4x, four waves per gate) up to one
     gate per CU, K1x (k_blind_rotate_ginx2x) up to two and K1 above; FHE_HIP_GINX_KERNEL pins it; LMKCDEY runs
-    K1m's two-digit form (k_blind_rotate_lmk3) up to two gates per CU and its op-list kernel above"""
+    K1m-4 (k_blind_rotate_lmk4x) up to one gate per CU, K1m's two-digit form (k_blind_rotate_lmk3) up to two and
+    its op-list kernel above"""
     from fhe_amd import binfhe as bf
     keys = bf.keygen(bf.STD128, bf.GINX, 5)
     e = bf.GateEngine(bf.STD128, bf.GINX, 0)
@@ -209,7 +210,7 @@ def test_gpu_gate_kernel_reports_the_launched_kernel(monkeypatch):
     lk = bf.keygen(bf.STD128_LMKCDEY, bf.LMKCDEY, 5)
     l = bf.GateEngine(bf.STD128_LMKCDEY, bf.LMKCDEY, 0)
     l.load_keys(lk.bsk, lk.kskA, lk.kskB)
-    assert l.gate_kernel(1024) == "k_blind_rotate_lmk" and l.gate_kernel(1) == "k_blind_rotate_lmk3"
-    assert switch(l, ("k_blind_rotate_lmk3",)) == x
+    assert l.gate_kernel(1024) == "k_blind_rotate_lmk" and l.gate_kernel(1) == "k_blind_rotate_lmk4x"
+    assert switch(l, ("k_blind_rotate_lmk4x",)) == q and switch(l, ("k_blind_rotate_lmk4x", "k_blind_rotate_lmk3")) == x
     for x in (e, l):
         x.close()

@@ -397,8 +397,9 @@ def test_gpu_k1x_bootstrap_func_and_seam_match_one_wave_kernel():
 @pytest.mark.gpu
 @pytest.mark.parametrize("ps_name", ["STD128_LMKCDEY", "STD128Q_LMKCDEY", "MEDIUM"])
 def test_gpu_lmk_split_kernel_matches_one_wave_kernel(ps_name):
-    """LMKCDEY's small-batch kernel, K1m's two-digit form (k_blind_rotate_lmk3<2, ..>: two waves per gate, the default
-    up to two gates per CU, FHE_HIP_LMK_KERNEL=split pins it) == the one-wave op-list kernel K1 LMK
+    """LMKCDEY's small-batch kernels, K1m's two-digit form (k_blind_rotate_lmk3<2, ..>: two waves per gate, the default
+    up to two gates per CU, FHE_HIP_LMK_KERNEL=split pins it) and K1m-4 (k_blind_rotate_lmk4x: four waves per gate,
+    the default up to one gate per CU, qsplit) == the one-wave op-list kernel K1 LMK
     (FHE_HIP_LMK_KERNEL=wave, pinned to the reference by the gate / fb / backend goldens) on gates of every type
     (1, 5, 37 gates and 1027 pinned), BootstrapFunc tables at the moduli q and 2N, EvalFuncMultiOutput and the
     seam's BlindRotate; Q >= 2^27 (STD128_LMKCDEY, MEDIUM: 8 Q of signed headroom) and Q < 2^27 (STD128Q_LMKCDEY)"""
@@ -407,7 +408,7 @@ def test_gpu_lmk_split_kernel_matches_one_wave_kernel(ps_name):
     ps, m = bf.PARAMSETS.index(ps_name), bf.LMKCDEY
     keys = bf.keygen(ps, m, 19)
     eng = {}
-    for kind in ("split", "wave", None):
+    for kind in ("split", "qsplit", "wave", None):
         if kind:
             os.environ["FHE_HIP_LMK_KERNEL"] = kind
         try:
@@ -418,7 +419,7 @@ def test_gpu_lmk_split_kernel_matches_one_wave_kernel(ps_name):
         eng[kind or "default"] = e
     P = eng["wave"].params
     assert eng["split"].gate_kernel(4096) == "k_blind_rotate_lmk3" and eng["wave"].gate_kernel(1) == "k_blind_rotate_lmk"
-    assert eng["default"].gate_kernel(37) == "k_blind_rotate_lmk3"
+    assert eng["default"].gate_kernel(37) == "k_blind_rotate_lmk4x" and eng["qsplit"].gate_kernel(4096) == "k_blind_rotate_lmk4x"
     rng = np.random.default_rng(5)
     w = eng["wave"]
     for count in (1, 5, 1027):
@@ -428,11 +429,12 @@ def test_gpu_lmk_split_kernel_matches_one_wave_kernel(ps_name):
         for gate in (bf.AND, bf.XOR, bf.NOR):
             s = eng["split"].eval_gate(gate, c1, d1, c2, d2)
             assert all(np.array_equal(u, v) for u, v in zip(s, w.eval_gate(gate, c1, d1, c2, d2))), (count, gate)
+            assert all(np.array_equal(u, v) for u, v in zip(eng["qsplit"].eval_gate(gate, c1, d1, c2, d2), s))
             if count < 1000:
                 assert all(np.array_equal(u, v) for u, v in zip(eng["default"].eval_gate(gate, c1, d1, c2, d2), s))
         if count == 5:
             assert np.array_equal(bf.decrypt(ps, m, keys.sk, *s), (1 - (x1 | x2)).astype(np.int64))
-    for kind in ("split", "default"):
+    for kind in ("split", "qsplit", "default"):
         x = eng[kind]
         for ctmod in sorted({P.q, 2 * P.N}):
             cnt = 37
