@@ -1,7 +1,9 @@
-// Wave placement of a K1x-shaped launch: 512 workgroups x 4 waves with 77,824 B of LDS each (two per CU),
-// every wave records its HW_ID (SIMD, CU, SE, workgroup slot, wave slot) and a start timestamp.
+// Wave placement of a launch of `blocks` workgroups x 4 waves with `lds` bytes of LDS each (default: K1x's shape,
+// 512 x 77,824 B, two per CU; `hwid 256 60416`: config 3 on K1), every wave records its HW_ID (SIMD, CU, SE,
+// workgroup slot, wave slot) and a start timestamp.  usage: hwid [blocks] [lds bytes]
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <vector>
 __global__ void k_hwid(uint32_t* out, uint64_t* t) {
@@ -19,12 +21,13 @@ __global__ void k_hwid(uint32_t* out, uint64_t* t) {
         t[w] = t0;
     }
 }
-int main() {
-    const int blocks = 512, threads = 256, waves = blocks * threads / 64;
+int main(int argc, char** argv) {
+    const int blocks = argc > 1 ? atoi(argv[1]) : 512, lds = argc > 2 ? atoi(argv[2]) : 77824;
+    const int threads = 256, waves = blocks * threads / 64;
     uint32_t* d; uint64_t* dt;
     hipMalloc(&d, waves * 8); hipMalloc(&dt, waves * 8);
-    hipFuncSetAttribute((const void*)k_hwid, hipFuncAttributeMaxDynamicSharedMemorySize, 77824);
-    hipLaunchKernelGGL(k_hwid, dim3(blocks), dim3(threads), 77824, 0, d, dt);
+    hipFuncSetAttribute((const void*)k_hwid, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(k_hwid, dim3(blocks), dim3(threads), lds, 0, d, dt);
     std::vector<uint32_t> h(waves * 2);
     hipMemcpy(h.data(), d, waves * 8, hipMemcpyDeviceToHost);
     std::map<std::tuple<int, int, int, int>, std::vector<int>> simd;  // (xcc, se, cu, simd) -> blocks
@@ -38,6 +41,7 @@ int main() {
     }
     std::map<int, int> hist;
     for (auto& kv : simd) hist[(int)kv.second.size()]++;
+    printf("%d workgroups, %d B LDS: %zu SIMDs used\n", blocks, lds, simd.size());
     for (auto& kv : hist) printf("SIMDs holding %d waves: %d\n", kv.first, kv.second);
     int shown = 0;
     for (auto& kv : simd) {
