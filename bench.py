@@ -20,7 +20,9 @@ gate prep + blind rotation (k_blind_rotate_ginx), then key switch + ModSwitch
                       vs the half-rate 32-bit integer multiply issue peak;
   * lmkcdey        -- BASELINE config 5: the same step on STD128_LMKCDEY (T gates,
                       same sharding), with its own roofline / valu_roofline / cpu_baseline;
-  * config3        -- BASELINE config 3: B = 1024 GINX gates on one GPU (N = 1 only);
+  * config3        -- BASELINE config 3: B = 1024 GINX gates on one GPU (N = 1 only; warmup at least 0.2 s);
+  * small_batch    -- one gate's latency on the default (two- / four-waves-per-gate) kernels of STD128 GINX and
+                      STD128_LMKCDEY and on the one-wave kernels (N = 1 only);
   * ntt_roofline   -- BASELINE config 2: 4096-polynomial N = 1024 NTT and iNTT passes,
                       27-bit STD128 modulus (k_ntt1024w) and 60-bit poly-benchmark prime
                       (k_ntt1024w64), GB/s vs HBM peak;
@@ -79,6 +81,7 @@ def parse():
     ap.add_argument("--cpu-sample-1core", type=int, default=24, help="gates in the 1-core CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core available to this job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-small-batch", action="store_true", help="skip the one-gate latency sub-object")
     return ap.parse_args()
 
 
@@ -374,6 +377,8 @@ def main():
             "hbm_basis": "SURVEY 8(d) config 3: BSK + KSK + 1024 x I/O = 474,677,248 B per batch / step time",
         }
     if rank == 0 and world == 1:
+        if not args.no_small_batch:
+            result["small_batch"] = small_batch(bf, torch, dev, stream)
         result["ntt_roofline"] = ntt_rooflines(NttPlan, torch, dev, stream, args.ntt_count)
         result["copy_bw"] = copy_bandwidth(torch, dev, stream, args.ntt_count)
         cpu = None
@@ -426,6 +431,48 @@ def pmc_valu_busy(kernel):
     """the kernel's VALU issue fraction from the committed PMC summary (SQ_ACTIVE_INST_VALU x 4 per SIMD
     over GRBM_GUI_ACTIVE per XCD, tools/pmc_traffic.py); None if not measured"""
     return pmc_summary(kernel, "valu_busy")[0]
+
+
+def small_batch(bf, torch, dev, stream, reps=20):
+    """Latency of one gate (EvalBinGate(AND): prep, blind rotation, key switch; inputs resident, HIP events on
+    the stream, median of `reps`) on the default kernels of STD128 GINX and STD128_LMKCDEY (the two- and
+    four-waves-per-gate forms) and on the one-wave kernels they replace below two
+    gates per CU (FHE_HIP_{GINX,LMK}_KERNEL=wave); checked by decryption."""
+    out = {"gates": 1, "unit": "ms", "basis": "median of %d single-gate calls, HIP events on the stream" % reps}
+    sp = stream.cuda_stream
+    for name, ps, m, knob in (("ginx", bf.STD128, bf.GINX, "FHE_HIP_GINX_KERNEL"),
+                              ("lmkcdey", bf.STD128_LMKCDEY, bf.LMKCDEY, "FHE_HIP_LMK_KERNEL")):
+        keys = bf.keygen(ps, m, 0x5B00 + ps)
+        P = bf.params(ps, m)
+        a1, b1 = bf.encrypt(ps, m, keys.sk, np.array([1]), 11)
+        a2, b2 = bf.encrypt(ps, m, keys.sk, np.array([1]), 12)
+        d_in = [torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev) for x in (a1, b1, a2, b2)]
+        d_ao = torch.empty((1, P.n), dtype=torch.int64, device=dev)
+        d_bo = torch.empty((1,), dtype=torch.int64, device=dev)
+        for kind in ("default", "wave"):
+            if kind == "wave":
+                os.environ[knob] = "wave"
+            try:
+                eng = bf.GateEngine(ps, m, device=dev.index)
+            finally:
+                os.environ.pop(knob, None)
+            eng.load_keys(keys.bsk, keys.kskA, keys.kskB)
+            ts = []
+            for k in range(reps + 40):  # 40 warmup calls: steady clocks (profiles/r06_c3_ramp.txt)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                eng.eval_gate_device(bf.AND, 1, *[t.data_ptr() for t in d_in], d_ao.data_ptr(), d_bo.data_ptr(),
+                                     stream=sp)
+                e1.record(stream)
+                e1.synchronize()
+                if k >= 40:
+                    ts.append(e0.elapsed_time(e1))
+            ao = d_ao.cpu().numpy().view(np.uint64)
+            bo = d_bo.cpu().numpy().view(np.uint64)
+            ok = bool(bf.decrypt(ps, m, keys.sk, ao, bo)[0] == 1)
+            out[f"{name}_{kind}"] = {"ms": round(float(np.median(ts)), 3), "kernel": eng.gate_kernel(1), "verified": ok}
+            eng.close()
+    return out
 
 
 def ntt_rooflines(NttPlan, torch, dev, stream, count, reps=20):
