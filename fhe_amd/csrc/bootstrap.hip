@@ -2272,9 +2272,16 @@ hipError_t launch_blind_rotate_ginx2x(const GateArgs& g, const BootTables& t, co
 // < 10.5 Q between indices (the inverse plan's BIN; 16 Q of signed headroom).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kQWave = 5 * kG2Tile;  // words per wave: a transpose tile and [parity][o] exchange planes
+#ifndef FHE_Q_X128
+#define FHE_Q_X128 1  // the four words of a slot side by side: one ds_read_b128 instead of three b32 reads (0: A/B)
+#endif
+// words per wave: a transpose tile and [parity][o] exchange planes; with FHE_Q_X128 the tiles only, and a shared
+// exchange area [parity][component][r][lane][4] (the word of wave (c', j') for component c at j' + 2 (c' != c),
+// swizzled by lane bits 3..4 so that the 64 lanes' b32 writes hit distinct banks)
+constexpr int kQWave = (FHE_Q_X128 ? 1 : 5) * kG2Tile;
+constexpr int kQX    = FHE_Q_X128 ? 2 * 2 * 16 * 64 * 4 : 0;
 constexpr int kQAcc  = 105;          // |acc| < 10.5 Q between indices (units of Q/10)
-constexpr size_t q_lds() { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 4 * kQWave) * 4; }
+constexpr size_t q_lds() { return (size_t)(1024 + 1024 + 2 * kMonoHalfWords + 4 * kQWave + kQX) * 4; }
 static_assert(q_lds() <= 160 * 1024, "LDS per workgroup");
 }  // namespace
 
@@ -2357,6 +2364,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         for (int r = 0; r < 16; ++r) dj[0][r] = j ? d[1][r] : d[0][r];
         fwd_wave_s<1>(dj, tile, L, twAf, s_tab, m);
         uint32_t* xb = xown + (i & 1) * (2 * kG2Tile) + L;
+        uint32_t* xx = s_wave + 4 * kQWave + (i & 1) * (2 * 16 * 256) + L * 4;  // FHE_Q_X128
+        const uint32_t sw = ((uint32_t)L >> 3) & 3u;
         const uint32_t fl = (as * lmul) & (MF ? 2047u : 1023u);
         auto mono_r = [&](int r0, uint2& mp, uint2& mn) {
             const uint32_t ur = __builtin_amdgcn_readfirstlane(
@@ -2391,8 +2400,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
                     S += (int64_t)((uint64_t)(uint32_t)S2 * mn.x) + (int64_t)(int32_t)(S2 >> 32) * (int32_t)mn.y;
                     if (o == 0) S += (int64_t)(int32_t)acc[r] * (int32_t)oneRj;
                     const uint32_t w = smont_red(S, m);
-                    xb[o * kG2Tile + (r << 6)] = w;
-                    if (o == 0) acc[r] = w;
+                    if (FHE_Q_X128) {
+                        xx[((o ? 1 - c : c) * 16 + r) * 256 + (((uint32_t)(j + 2 * o)) ^ sw)] = w;
+                    } else {
+                        xb[o * kG2Tile + (r << 6)] = w;
+                        if (o == 0) acc[r] = w;
+                    }
                 }
             }
         }
@@ -2401,9 +2414,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        const uint32_t po = (i & 1) * (2 * kG2Tile);
+        if (FHE_Q_X128) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)] + xo0[po + (r << 6)] + xo1[po + (r << 6)];
+            for (int r = 0; r < 16; ++r) {
+                const uint4 q = *reinterpret_cast<const uint4*>(xx + (c * 16 + r) * 256);
+                acc[r] = q.x + q.y + q.z + q.w;
+            }
+        } else {
+            const uint32_t po = (i & 1) * (2 * kG2Tile);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)] + xo0[po + (r << 6)] + xo1[po + (r << 6)];
+        }
     }
 
     if (ACCIO) {
