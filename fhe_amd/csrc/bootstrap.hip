@@ -2818,9 +2818,14 @@ hipError_t launch_blind_rotate_lmkx(const GateArgs& g, const BootTables& t, cons
 // Q < 2^27), so acc < 3.7 Q after EXT and < 2.4 Q after AUTO (BIN 37; signed headroom 8 Q or 16 Q).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kMWave = 5 * kG2Tile;  // words per wave: a transpose tile and [parity][o] exchange planes
+#ifndef FHE_M4_X128
+#define FHE_M4_X128 1  // K1q's shared exchange area: the four words of a slot side by side, one ds_read_b128 (0: A/B)
+#endif
+// words per wave: a transpose tile and [parity][o] exchange planes (FHE_M4_X128: the tile; the area after the tiles)
+constexpr int kMWave = (FHE_M4_X128 ? 1 : 5) * kG2Tile;
+constexpr int kMX    = FHE_M4_X128 ? 2 * 2 * 16 * 64 * 4 : 0;
 constexpr int kMAcc  = 37;           // |acc| < 3.7 Q between ops (units of Q/10)
-constexpr size_t m4_lds() { return (size_t)(1024 + 1024 + 4 * kMWave) * 4; }
+constexpr size_t m4_lds() { return (size_t)(1024 + 1024 + 4 * kMWave + kMX) * 4; }
 static_assert(m4_lds() <= 160 * 1024, "LDS per workgroup");
 }  // namespace
 
@@ -2844,6 +2849,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
     const uint32_t gate = blockIdx.x;
     uint32_t* tile = s_wave + wave * kMWave;
     uint32_t* xown = tile + kG2Tile + L;  // plane [p][o] at + (2 p + o) kG2Tile: this wave's word for column c ^ o
+    uint32_t* xx_ = nullptr;              // FHE_M4_X128: this op's area, at this lane's four slots
+    const uint32_t sw = ((uint32_t)L >> 3) & 3u;
     const uint32_t* xsib = s_wave + (wave ^ 2) * kMWave + kG2Tile + L;   // (c, 1 - j), o = 0
     const uint32_t* xo0  = s_wave + (1 - c) * kMWave + 2 * kG2Tile + L;  // (1 - c, 0), o = 1
     const uint32_t* xo1  = s_wave + (3 - c) * kMWave + 2 * kG2Tile + L;  // (1 - c, 1), o = 1
@@ -2922,10 +2929,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
                     const uint4 q = kq[k4 & 1][o];
                     const uint32_t kv = e == 0 ? q.x : e == 1 ? q.y : e == 2 ? q.z : q.w;
                     const uint32_t w = smont_red((int64_t)(int32_t)dj[0][r] * (int32_t)kv, m);
-                    xb[o * kG2Tile + (r << 6)] = w;
-                    if (o == 0) acc[r] = w;
+                    if (FHE_M4_X128) {  // component c ^ o, slot j + 2 o (swizzled)
+                        xx_[(((uint32_t)(c ^ o)) * 16 + r) * 256 + (((uint32_t)(j + 2 * o)) ^ sw)] = w;
+                    } else {
+                        xb[o * kG2Tile + (r << 6)] = w;
+                        if (o == 0) acc[r] = w;
+                    }
                 }
             }
+        }
+    };
+    auto sum4 = [&](const uint32_t* xx) {  // FHE_M4_X128: acc_c = the four words of its slots
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint4 q = *reinterpret_cast<const uint4*>(xx + (c * 16 + r) * 256);
+            acc[r] = q.x + q.y + q.z + q.w;
         }
     };
     for (uint32_t it = 0; it < cnt; ++it) {
@@ -2933,6 +2951,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)gops[it]);
         const uint32_t po = (it & 1) * (2 * kG2Tile);
         uint32_t* xb = xown + po;
+        xx_ = s_wave + 4 * kMWave + (it & 1) * (2 * 16 * 256) + L * 4;
         uint32_t dj[1][16];
         if (!(op & 0x8000u)) {
             // ---- AddToAccLMKCDEY: acc_c <- sum over the four digits D ek[op][row][c]   (acc replaced)
@@ -2940,8 +2959,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
             words(dj, ek + ((size_t)op * 2 + c) * (4 * 4 * 64) + (size_t)j * (4 * 64) + L,
                   ek + ((size_t)op * 2 + (1 - c)) * (4 * 4 * 64) + (size_t)(2 + j) * (4 * 64) + L, xb, m);
             barrier();
+            if (FHE_M4_X128) {
+                sum4(xx_);
+            } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)] + xo0[po + (r << 6)] + xo1[po + (r << 6)];
+                for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)] + xo0[po + (r << 6)] + xo1[po + (r << 6)];
+            }
         } else {
             // ---- Automorphism(5^t or 2N-5, ak[t])
             const uint32_t t = op & 0x7fffu;
@@ -2958,9 +2981,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
             } else {       // acc1' reduced while component 0 transforms
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = smont_mul(acc[r], m.oneR, m);
+                if (FHE_M4_X128) {  // acc1' (or 0) into slot j of component 1, 0 into slot 2 + j of component 0
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        xx_[(16 + r) * 256 + (((uint32_t)j) ^ sw)] = j == 0 ? acc[r] : 0u;
+                        xx_[r * 256 + (((uint32_t)(2 + j)) ^ sw)] = 0u;
+                    }
+                }
             }
             barrier();
-            if (c == 0) {
+            if (FHE_M4_X128) {
+                sum4(xx_);
+            } else if (c == 0) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] += xsib[po + (r << 6)];
             } else {
